@@ -1,0 +1,1002 @@
+// C-ABI implementation (include/ddshe.h): contexts, stream/buffer pools, per-modulus
+// Montgomery constants, and the host orchestration of the HIP kernels.
+//
+// The per-row arithmetic of every entry point runs on the GPU; the host only
+// parses/serialises the boundary formats and computes O(1) per-call constants.
+#include "ddshe.h"
+
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "bn_host.hpp"
+#include "ddshe_launch.hpp"
+
+using namespace ddshe;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                             \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess) return fail(DDS_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) {
+      (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+    }
+    size_t nb = std::max<size_t>(bytes, 256);
+    hipError_t e = hipMalloc(&p, nb);
+    if (e == hipSuccess) cap = nb;
+    return e;
+  }
+  template <class T>
+  T* as() const {
+    return (T*)p;
+  }
+};
+
+struct Worker {
+  hipStream_t stream = nullptr;
+  DevBuf in, in2, x, x2, p0, p1, out, flags, y, misc, misc2;
+  hipEvent_t ev[4] = {};
+  ~Worker() {
+    for (auto e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+struct ModConsts {
+  int S = 0, TPI = 0;
+  size_t bits = 0, bytes = 0;
+  uint32_t n0 = 0;
+  bn::Limbs N, Rmod;
+  std::vector<uint32_t> host;  // kConstCount * S
+  uint32_t* d = nullptr;       // device copy
+  std::mutex ymu;
+  std::map<uint64_t, std::vector<uint32_t>> ycache;  // k -> R^k mod N (r27)
+  ~ModConsts() {
+    if (d) (void)hipFree(d);
+  }
+  const std::vector<uint32_t>& y_for(uint64_t k) {
+    std::lock_guard<std::mutex> lk(ymu);
+    auto it = ycache.find(k);
+    if (it != ycache.end()) return it->second;
+    if (ycache.size() > 64) ycache.clear();
+    bn::Limbs y = bn::powmod_u64(Rmod, k, N);
+    return ycache.emplace(k, bn::to_r27(y, S)).first->second;
+  }
+};
+
+}  // namespace
+
+struct dds_ctx {
+  int device = 0;
+  int cus = 0;
+  std::mutex mu;
+  std::vector<std::unique_ptr<Worker>> workers;
+  std::vector<Worker*> idle;
+  std::map<bn::Limbs, std::shared_ptr<ModConsts>> mods;
+  hipStream_t ext_stream = nullptr;
+  std::atomic<bool> timing{false};
+  std::mutex tmu;
+  double fold_ms = 0, total_ms = 0;
+  uint64_t fold_launches = 0, fold_modmuls = 0, pending_modmuls = 0;
+};
+
+struct dds_col {
+  dds_ctx* ctx = nullptr;
+  std::shared_ptr<ModConsts> mc;
+  size_t capacity = 0, count = 0, stride = 0;
+  uint32_t* d = nullptr;
+  std::mutex mu;
+  ~dds_col() {
+    if (d) (void)hipFree(d);
+  }
+};
+
+namespace {
+
+struct WorkerLease {
+  dds_ctx* ctx;
+  Worker* w = nullptr;
+  hipStream_t st = nullptr;
+  explicit WorkerLease(dds_ctx* c) : ctx(c) {}
+  int acquire() {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!ctx->idle.empty()) {
+      w = ctx->idle.back();
+      ctx->idle.pop_back();
+    } else {
+      auto nw = std::make_unique<Worker>();
+      if (hipSetDevice(ctx->device) != hipSuccess) return fail(DDS_E_HIP, "hipSetDevice");
+      if (hipStreamCreateWithFlags(&nw->stream, hipStreamNonBlocking) != hipSuccess)
+        return fail(DDS_E_HIP, "hipStreamCreate");
+      for (auto& e : nw->ev)
+        if (hipEventCreate(&e) != hipSuccess) return fail(DDS_E_HIP, "hipEventCreate");
+      w = nw.get();
+      ctx->workers.push_back(std::move(nw));
+    }
+    st = ctx->ext_stream ? ctx->ext_stream : w->stream;
+    return DDS_OK;
+  }
+  ~WorkerLease() {
+    if (w) {
+      std::lock_guard<std::mutex> lk(ctx->mu);
+      ctx->idle.push_back(w);
+    }
+  }
+};
+
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_ptr<ModConsts>* out) {
+  if (!mod_be || mod_bytes == 0) return fail(DDS_E_ARG, "modulus missing");
+  bn::Limbs N = bn::from_be(mod_be, mod_bytes);
+  if (N.empty() || (N[0] & 1u) == 0 || bn::bit_length(N) < 2)
+    return fail(DDS_E_ARG, "modulus must be odd and > 1 (Montgomery)");
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    auto it = ctx->mods.find(N);
+    if (it != ctx->mods.end()) {
+      *out = it->second;
+      return DDS_OK;
+    }
+  }
+  auto mc = std::make_shared<ModConsts>();
+  mc->bits = bn::bit_length(N);
+  mc->bytes = (mc->bits + 7) / 8;
+  mc->S = pick_S(mc->bits);
+  if (!mc->S) return fail(DDS_E_UNSUPPORTED, "modulus too large");
+  mc->TPI = tpi_for(mc->S);
+  const int S = mc->S;
+  mc->N = N;
+  mc->n0 = bn::mont_n0(N[0]);
+  mc->Rmod = bn::mod(bn::pow2((size_t)27 * S), N);
+  bn::Limbs R2 = bn::mod(bn::mul(mc->Rmod, mc->Rmod), N);
+  bn::Limbs N2 = bn::add(N, N);
+  mc->host.assign((size_t)kConstCount * S, 0);
+  auto put = [&](int slot, const bn::Limbs& v) {
+    auto r = bn::to_r27(v, S);
+    std::copy(r.begin(), r.end(), mc->host.begin() + (size_t)slot * S);
+  };
+  put(kConstN, N);
+  put(kConstRmod, mc->Rmod);
+  put(kConstR2, R2);
+  put(kConstOne, bn::Limbs{1});
+  put(kConstN2x, N2);
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(DDS_E_HIP, "hipSetDevice");
+  if (hipMalloc(&mc->d, (mc->host.size() + 1) * 4) != hipSuccess) return fail(DDS_E_NOMEM, "const alloc");
+  std::vector<uint32_t> up(mc->host);
+  up.push_back(0);  // ingest reads 2N limb S (always 0 by construction of S)
+  // 2N lives in the last slot; the extra zero word follows it
+  if (hipMemcpy(mc->d, up.data(), up.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return fail(DDS_E_HIP, "const upload");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  auto it = ctx->mods.find(N);
+  if (it != ctx->mods.end()) {
+    *out = it->second;
+    return DDS_OK;
+  }
+  ctx->mods.emplace(N, mc);
+  *out = mc;
+  return DDS_OK;
+}
+
+void record_time(dds_ctx* ctx, Worker* w, hipStream_t st, bool begin, int slot) {
+  if (!ctx->timing.load()) return;
+  (void)hipEventRecord(w->ev[slot + (begin ? 0 : 1)], st);
+}
+
+size_t max_fold_groups(dds_ctx* ctx, int S) {
+  int bpc = 0;
+  if (fold_occupancy(S, &bpc) != hipSuccess || bpc < 1) bpc = 1;
+  return (size_t)ctx->cus * bpc * (256 / tpi_for(S));
+}
+
+// Fold `count` rows of an r27 column into one un-finalised partial (in `*part`, stride pstride, row 0).
+int fold_partial_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
+                        size_t count, const uint32_t** part, size_t* part_stride) {
+  const int S = mc.S;
+  size_t G = std::min(max_fold_groups(ctx, S), std::max<size_t>(1, count / 2));
+  size_t ps = round_up(G, 64);
+  HIP_TRY(w->p0.ensure((size_t)S * ps * 4));
+  HIP_TRY(w->p1.ensure((size_t)S * round_up((G + 1) / 2, 64) * 4));
+  record_time(ctx, w, st, true, 0);
+  HIP_TRY(launch_fold(S, X, xstride, count, mc.d, mc.n0, w->p0.as<uint32_t>(), ps, G, st));
+  record_time(ctx, w, st, false, 0);
+  if (ctx->timing.load()) {
+    // Montgomery products issued by this launch: every row but each group's first
+    std::lock_guard<std::mutex> lk(ctx->tmu);
+    ctx->pending_modmuls = count > G ? count - G : 0;
+  }
+  uint32_t* cur = w->p0.as<uint32_t>();
+  uint32_t* nxt = w->p1.as<uint32_t>();
+  size_t n = G, cs = ps;
+  while (n > 1) {
+    size_t ng = (n + 1) / 2, ns = round_up(ng, 64);
+    HIP_TRY(launch_fold(S, cur, cs, n, mc.d, mc.n0, nxt, ns, ng, st));
+    std::swap(cur, nxt);
+    n = ng;
+    cs = ns;
+  }
+  *part = cur;
+  *part_stride = cs;
+  return DDS_OK;
+}
+
+int finalize_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* part, size_t pstride,
+                    uint64_t k, std::vector<uint32_t>* result_r27) {
+  const int S = mc.S;
+  const std::vector<uint32_t>& y = mc.y_for(k);
+  HIP_TRY(w->y.ensure((size_t)S * 4));
+  HIP_TRY(w->out.ensure((size_t)S * 4));
+  HIP_TRY(hipMemcpyAsync(w->y.p, y.data(), (size_t)S * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(launch_finalize(S, part, pstride, mc.d, w->y.as<uint32_t>(), mc.n0, w->out.as<uint32_t>(), st));
+  result_r27->assign(S, 0);
+  HIP_TRY(hipMemcpyAsync(result_r27->data(), w->out.p, (size_t)S * 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (ctx->timing.load()) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, w->ev[0], w->ev[1]) == hipSuccess) {
+      std::lock_guard<std::mutex> lk(ctx->tmu);
+      ctx->fold_ms += ms;
+      ctx->fold_launches += 1;
+      ctx->fold_modmuls += ctx->pending_modmuls;
+    }
+  }
+  return DDS_OK;
+}
+
+int emit_be(const bn::Limbs& v, size_t width, uint8_t* out, size_t out_cap, size_t* out_len) {
+  if (out_len) *out_len = width;
+  if (!out || out_cap < width) return fail(DDS_E_BUFSIZE, "output buffer too small");
+  if (!bn::to_be(v, out, width)) return fail(DDS_E_RANGE, "result does not fit");
+  return DDS_OK;
+}
+
+// Upload `count` big-endian operands into an r27 column (X, stride) validated against mc.
+int ingest(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint8_t* ops, size_t width, size_t count,
+           DevBuf& raw, uint32_t* X, size_t stride) {
+  (void)ctx;
+  if (count == 0) return DDS_OK;
+  HIP_TRY(raw.ensure(count * width));
+  HIP_TRY(w->flags.ensure(16));
+  HIP_TRY(hipMemcpyAsync(raw.p, ops, count * width, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, st));
+  HIP_TRY(launch_ingest_be(raw.as<uint8_t>(), width, count, mc.S, mc.d + (size_t)kConstN2x * mc.S, X, stride,
+                           w->flags.as<uint32_t>(), st));
+  uint32_t flags = 0;
+  HIP_TRY(hipMemcpyAsync(&flags, w->flags.p, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (flags & 2u) return fail(DDS_E_RANGE, "operand wider than the modulus limb width");
+  if (flags & 1u) HIP_TRY(launch_reduce_rows(mc.S, X, stride, count, mc.d, mc.n0, st));
+  return DDS_OK;
+}
+
+}  // namespace
+
+// =============================================================================
+extern "C" {
+
+const char* dds_strerror(int s) {
+  switch (s) {
+    case DDS_OK: return "ok";
+    case DDS_E_EMPTY: return "no operand (404)";
+    case DDS_E_RANGE: return "operand out of range";
+    case DDS_E_HIP: return "HIP error";
+    case DDS_E_ARG: return "invalid argument";
+    case DDS_E_NOMEM: return "out of memory";
+    case DDS_E_UNSUPPORTED: return "unsupported";
+    case DDS_E_BUFSIZE: return "buffer too small";
+    case DDS_E_FORMAT: return "number format";
+    default: return "unknown";
+  }
+}
+
+const char* dds_last_error(void) { return g_last_error.c_str(); }
+
+size_t dds_max_modulus_bits(void) { return (size_t)27 * 232 - 2; }
+
+int dds_ctx_create(int device, dds_ctx** out) {
+  if (!out) return fail(DDS_E_ARG, "out");
+  *out = nullptr;
+  try {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(DDS_E_HIP, "no HIP device");
+    if (device < 0 || device >= n) return fail(DDS_E_ARG, "device index");
+    if (hipSetDevice(device) != hipSuccess) return fail(DDS_E_HIP, "hipSetDevice");
+    auto* c = new dds_ctx();
+    c->device = device;
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess) {
+      delete c;
+      return fail(DDS_E_HIP, "hipGetDeviceProperties");
+    }
+    c->cus = p.multiProcessorCount;
+    *out = c;
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  } catch (...) {
+    return fail(DDS_E_HIP, "unexpected exception");
+  }
+}
+
+int dds_ctx_destroy(dds_ctx* ctx) {
+  if (!ctx) return DDS_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();
+  delete ctx;
+  return DDS_OK;
+}
+
+int dds_ctx_set_stream(dds_ctx* ctx, void* stream) {
+  if (!ctx) return fail(DDS_E_ARG, "ctx");
+  ctx->ext_stream = (hipStream_t)stream;
+  return DDS_OK;
+}
+
+int dds_ctx_set_timing(dds_ctx* ctx, int enable) {
+  if (!ctx) return fail(DDS_E_ARG, "ctx");
+  ctx->timing.store(enable != 0);
+  return DDS_OK;
+}
+
+int dds_ctx_get_timing(dds_ctx* ctx, double* fold_ms, uint64_t* fold_launches, double* total_ms) {
+  if (!ctx) return fail(DDS_E_ARG, "ctx");
+  std::lock_guard<std::mutex> lk(ctx->tmu);
+  if (fold_ms) *fold_ms = ctx->fold_ms;
+  if (fold_launches) *fold_launches = ctx->fold_launches;
+  if (total_ms) *total_ms = ctx->total_ms;
+  return DDS_OK;
+}
+
+int dds_ctx_reset_timing(dds_ctx* ctx) {
+  if (!ctx) return fail(DDS_E_ARG, "ctx");
+  std::lock_guard<std::mutex> lk(ctx->tmu);
+  ctx->fold_ms = ctx->total_ms = 0;
+  ctx->fold_launches = ctx->fold_modmuls = 0;
+  return DDS_OK;
+}
+
+int dds_ctx_get_fold_work(dds_ctx* ctx, uint64_t* modmuls) {
+  if (!ctx || !modmuls) return fail(DDS_E_ARG, "ctx");
+  std::lock_guard<std::mutex> lk(ctx->tmu);
+  *modmuls = ctx->fold_modmuls;
+  return DDS_OK;
+}
+
+int dds_modmul_fold(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint8_t* ops, size_t width,
+                    size_t count, uint8_t* out, size_t out_cap, size_t* out_len) {
+  try {
+    if (!ctx || (!ops && count) || width == 0) return fail(DDS_E_ARG, "bad arguments");
+    if (count == 0) return fail(DDS_E_EMPTY, "no operand");
+    if (count == 1) {  // DDSRestServer.scala:416-417: first operand is kept unreduced
+      if (out_len) *out_len = width;
+      if (!out || out_cap < width) return fail(DDS_E_BUFSIZE, "output buffer too small");
+      memcpy(out, ops, width);
+      return DDS_OK;
+    }
+    std::shared_ptr<ModConsts> mc;
+    int rc = get_mod(ctx, mod_be, mod_bytes, &mc);
+    if (rc) return rc;
+    WorkerLease wl(ctx);
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    const size_t stride = round_up(count, 64);
+    HIP_TRY(w->x.ensure((size_t)mc->S * stride * 4));
+    if ((rc = ingest(ctx, w, wl.st, *mc, ops, width, count, w->in, w->x.as<uint32_t>(), stride))) return rc;
+    const uint32_t* part;
+    size_t ps;
+    if ((rc = fold_partial_device(ctx, w, wl.st, *mc, w->x.as<uint32_t>(), stride, count, &part, &ps))) return rc;
+    std::vector<uint32_t> r27;
+    if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, count, &r27))) return rc;
+    return emit_be(bn::from_r27(r27.data(), mc->S), mod_bytes, out, out_cap, out_len);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  } catch (...) {
+    return fail(DDS_E_HIP, "unexpected exception");
+  }
+}
+
+int dds_paillier_sum(dds_ctx* ctx, const uint8_t* nsq, size_t nsq_bytes, const uint8_t* c, size_t width, size_t count,
+                     uint8_t* out, size_t out_cap, size_t* out_len) {
+  return dds_modmul_fold(ctx, nsq, nsq_bytes, c, width, count, out, out_cap, out_len);
+}
+
+int dds_rsa_product(dds_ctx* ctx, const uint8_t* n, size_t n_bytes, const uint8_t* c, size_t width, size_t count,
+                    uint8_t* out, size_t out_cap, size_t* out_len) {
+  return dds_modmul_fold(ctx, n, n_bytes, c, width, count, out, out_cap, out_len);
+}
+
+int dds_modmul_pairs(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint8_t* a, const uint8_t* b,
+                     size_t width, size_t n, uint8_t* out) {
+  try {
+    if (!ctx || width == 0 || (n && (!a || !b || !out))) return fail(DDS_E_ARG, "bad arguments");
+    if (n == 0) return DDS_OK;
+    std::shared_ptr<ModConsts> mc;
+    int rc = get_mod(ctx, mod_be, mod_bytes, &mc);
+    if (rc) return rc;
+    WorkerLease wl(ctx);
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    const int S = mc->S;
+    const size_t stride = round_up(n, 64);
+    HIP_TRY(w->x.ensure((size_t)S * stride * 4));
+    HIP_TRY(w->x2.ensure((size_t)S * stride * 4));
+    HIP_TRY(w->p0.ensure((size_t)S * stride * 4));
+    if ((rc = ingest(ctx, w, wl.st, *mc, a, width, n, w->in, w->x.as<uint32_t>(), stride))) return rc;
+    if ((rc = ingest(ctx, w, wl.st, *mc, b, width, n, w->in2, w->x2.as<uint32_t>(), stride))) return rc;
+    HIP_TRY(launch_pairs(S, w->x.as<uint32_t>(), w->x2.as<uint32_t>(), stride, n, mc->d, mc->n0,
+                         w->p0.as<uint32_t>(), wl.st));
+    std::vector<uint32_t> h((size_t)S * stride);
+    HIP_TRY(hipMemcpyAsync(h.data(), w->p0.p, h.size() * 4, hipMemcpyDeviceToHost, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    std::vector<uint32_t> limbs(S);
+    for (size_t i = 0; i < n; ++i) {
+      for (int l = 0; l < S; ++l) limbs[l] = h[(size_t)l * stride + i];
+      if (!bn::to_be(bn::from_r27(limbs.data(), S), out + i * mod_bytes, mod_bytes))
+        return fail(DDS_E_RANGE, "result does not fit");
+    }
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  } catch (...) {
+    return fail(DDS_E_HIP, "unexpected exception");
+  }
+}
+
+int dds_bigint_sum(dds_ctx* ctx, const uint8_t* ops, size_t width, size_t count, uint8_t* out, size_t out_cap,
+                   size_t* out_len) {
+  try {
+    if (!ctx || width == 0 || (count && !ops)) return fail(DDS_E_ARG, "bad arguments");
+    if (count == 0) return fail(DDS_E_EMPTY, "no operand");
+    WorkerLease wl(ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    const int S = (int)((width * 8 + 26) / 27);
+    const size_t stride = round_up(count, 64);
+    HIP_TRY(w->x.ensure((size_t)S * stride * 4));
+    HIP_TRY(w->in.ensure(count * width));
+    HIP_TRY(w->flags.ensure(16));
+    // 2N sentinel with limb S set: every row compares below it (no range check for plain sums)
+    std::vector<uint32_t> sentinel((size_t)S + 1, 0);
+    sentinel[S] = 1;
+    HIP_TRY(w->misc2.ensure(sentinel.size() * 4));
+    HIP_TRY(hipMemcpyAsync(w->misc2.p, sentinel.data(), sentinel.size() * 4, hipMemcpyHostToDevice, wl.st));
+    HIP_TRY(hipMemcpyAsync(w->in.p, ops, count * width, hipMemcpyHostToDevice, wl.st));
+    HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, wl.st));
+    HIP_TRY(launch_ingest_be(w->in.as<uint8_t>(), width, count, S, w->misc2.as<uint32_t>(), w->x.as<uint32_t>(),
+                             stride, w->flags.as<uint32_t>(), wl.st));
+    const size_t nthreads = std::min<size_t>(count, (size_t)ctx->cus * 1024);
+    HIP_TRY(w->misc.ensure((size_t)S * nthreads * 8));
+    HIP_TRY(w->out.ensure((size_t)S * 8));
+    HIP_TRY(launch_plain_sum(w->x.as<uint32_t>(), stride, count, S, nthreads, w->misc.as<uint64_t>(),
+                             w->out.as<uint64_t>(), wl.st));
+    std::vector<uint64_t> sums(S);
+    HIP_TRY(hipMemcpyAsync(sums.data(), w->out.p, (size_t)S * 8, hipMemcpyDeviceToHost, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    // combine 64-bit limb sums: value = sum_l sums[l] * 2^(27 l)
+    bn::Limbs acc;
+    for (int l = S - 1; l >= 0; --l) {
+      // acc = acc * 2^27 + sums[l]
+      bn::Limbs sh = bn::mul(acc, bn::Limbs{1u << 27});
+      acc = bn::add(sh, bn::from_u64(sums[l]));
+    }
+    const size_t need = std::max<size_t>(1, bn::byte_length(acc));
+    const size_t w_out = std::max(width, need);
+    return emit_be(acc, w_out, out, out_cap, out_len);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  } catch (...) {
+    return fail(DDS_E_HIP, "unexpected exception");
+  }
+}
+
+// ---- device columns -----------------------------------------------------------
+int dds_col_create(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, size_t capacity, dds_col** out) {
+  try {
+    if (!ctx || !out || capacity == 0) return fail(DDS_E_ARG, "bad arguments");
+    *out = nullptr;
+    std::shared_ptr<ModConsts> mc;
+    int rc = get_mod(ctx, mod_be, mod_bytes, &mc);
+    if (rc) return rc;
+    auto* c = new dds_col();
+    c->ctx = ctx;
+    c->mc = mc;
+    c->capacity = capacity;
+    c->stride = round_up(capacity, 64);
+    if (hipSetDevice(ctx->device) != hipSuccess || hipMalloc(&c->d, (size_t)mc->S * c->stride * 4) != hipSuccess) {
+      delete c;
+      return fail(DDS_E_NOMEM, "column allocation");
+    }
+    *out = c;
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_col_destroy(dds_col* col) {
+  delete col;
+  return DDS_OK;
+}
+
+size_t dds_col_count(const dds_col* col) { return col ? col->count : 0; }
+
+size_t dds_col_partial_words(const dds_col* col) { return col ? (size_t)col->mc->S : 0; }
+
+int dds_col_append(dds_col* col, const uint8_t* ops, size_t width, size_t count) {
+  try {
+    if (!col || width == 0 || (count && !ops)) return fail(DDS_E_ARG, "bad arguments");
+    std::lock_guard<std::mutex> lk(col->mu);
+    if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
+    if (count == 0) return DDS_OK;
+    WorkerLease wl(col->ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    // ingest writes with the column's stride starting at row `count`
+    if ((rc = ingest(col->ctx, wl.w, wl.st, *col->mc, ops, width, count, wl.w->in, col->d + col->count, col->stride)))
+      return rc;
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    col->count += count;
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_col_read(dds_col* col, size_t first, size_t count, uint8_t* out) {
+  try {
+    if (!col || (count && !out) || first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
+    const int S = col->mc->S;
+    std::vector<uint32_t> h((size_t)S * count);
+    if (count)
+      HIP_TRY(hipMemcpy2D(h.data(), count * 4, col->d + first, col->stride * 4, count * 4, (size_t)S,
+                          hipMemcpyDeviceToHost));
+    std::vector<uint32_t> limbs(S);
+    for (size_t i = 0; i < count; ++i) {
+      for (int l = 0; l < S; ++l) limbs[l] = h[(size_t)l * count + i];
+      if (!bn::to_be(bn::from_r27(limbs.data(), S), out + i * col->mc->bytes, col->mc->bytes))
+        return fail(DDS_E_RANGE, "row does not fit");
+    }
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_col_fold_partial(dds_col* col, size_t first, size_t count, uint32_t* partial, uint64_t* rows) {
+  try {
+    if (!col || !partial || first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
+    WorkerLease wl(col->ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    ModConsts& mc = *col->mc;
+    if (count == 0) {  // empty partial = R mod N (identity of the partial algebra)
+      std::copy(mc.host.begin() + (size_t)kConstRmod * mc.S, mc.host.begin() + (size_t)(kConstRmod + 1) * mc.S,
+                partial);
+      if (rows) *rows = 0;
+      return DDS_OK;
+    }
+    const uint32_t* part;
+    size_t ps;
+    if ((rc = fold_partial_device(col->ctx, wl.w, wl.st, mc, col->d + first, col->stride, count, &part, &ps)))
+      return rc;
+    HIP_TRY(hipMemcpy2DAsync(partial, 4, part, ps * 4, 4, (size_t)mc.S, hipMemcpyDeviceToHost, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    if (col->ctx->timing.load()) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, wl.w->ev[0], wl.w->ev[1]) == hipSuccess) {
+        std::lock_guard<std::mutex> lk(col->ctx->tmu);
+        col->ctx->fold_ms += ms;
+        col->ctx->fold_launches += 1;
+        col->ctx->fold_modmuls += col->ctx->pending_modmuls;
+      }
+    }
+    if (rows) *rows = count;
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_col_fold(dds_col* col, size_t first, size_t count, uint8_t* out, size_t out_cap, size_t* out_len) {
+  try {
+    if (!col || first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
+    if (count == 0) return fail(DDS_E_EMPTY, "no operand");
+    ModConsts& mc = *col->mc;
+    if (count == 1) {
+      std::vector<uint8_t> tmp(mc.bytes);
+      int rc = dds_col_read(col, first, 1, tmp.data());
+      if (rc) return rc;
+      if (out_len) *out_len = mc.bytes;
+      if (!out || out_cap < mc.bytes) return fail(DDS_E_BUFSIZE, "output buffer too small");
+      memcpy(out, tmp.data(), mc.bytes);
+      return DDS_OK;
+    }
+    WorkerLease wl(col->ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    const uint32_t* part;
+    size_t ps;
+    if ((rc = fold_partial_device(col->ctx, wl.w, wl.st, mc, col->d + first, col->stride, count, &part, &ps)))
+      return rc;
+    std::vector<uint32_t> r27;
+    if ((rc = finalize_device(col->ctx, wl.w, wl.st, mc, part, ps, count, &r27))) return rc;
+    return emit_be(bn::from_r27(r27.data(), mc.S), mc.bytes, out, out_cap, out_len);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint32_t* partials,
+                         const uint64_t* rows, size_t nparts, uint8_t* out, size_t out_cap, size_t* out_len) {
+  try {
+    if (!ctx || !partials || !rows || nparts == 0) return fail(DDS_E_ARG, "bad arguments");
+    std::shared_ptr<ModConsts> mc;
+    int rc = get_mod(ctx, mod_be, mod_bytes, &mc);
+    if (rc) return rc;
+    uint64_t k = 0;
+    for (size_t i = 0; i < nparts; ++i) k += rows[i];
+    if (k == 0) return fail(DDS_E_EMPTY, "no operand");
+    const int S = mc->S;
+    WorkerLease wl(ctx);
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    const size_t stride = round_up(nparts, 64);
+    std::vector<uint32_t> h((size_t)S * stride, 0);
+    for (size_t i = 0; i < nparts; ++i)
+      for (int l = 0; l < S; ++l) h[(size_t)l * stride + i] = partials[i * S + l];
+    HIP_TRY(w->x.ensure(h.size() * 4));
+    HIP_TRY(hipMemcpyAsync(w->x.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, wl.st));
+    const uint32_t* part;
+    size_t ps;
+    if ((rc = fold_partial_device(ctx, w, wl.st, *mc, w->x.as<uint32_t>(), stride, nparts, &part, &ps))) return rc;
+    // partials are already "prod * R^(1-c)": folding n of them gives prod * R^(1-k) as for rows
+    std::vector<uint32_t> r27;
+    if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, k, &r27))) return rc;
+    return emit_be(bn::from_r27(r27.data(), S), mod_bytes, out, out_cap, out_len);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+// ---- Paillier encryption ---------------------------------------------------------
+namespace {
+int encrypt_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const bn::Limbs& n, const bn::Limbs& g,
+                   const uint32_t* d_m, const uint32_t* d_rcol, size_t rstride, size_t count, uint32_t* d_out,
+                   bool use_n_exponent) {
+  (void)ctx;
+  const int S = mc.S;
+  bn::Limbs gR = bn::mod(bn::mul(bn::mod(g, mc.N), mc.Rmod), mc.N);
+  std::vector<uint32_t> gr27 = bn::to_r27(gR, S);
+  std::vector<uint32_t> nbits_words(n.begin(), n.end());
+  if (nbits_words.empty()) nbits_words.push_back(0);
+  const int nbits = use_n_exponent ? (int)bn::bit_length(n) : 0;
+  HIP_TRY(w->y.ensure((gr27.size() + nbits_words.size()) * 4));
+  HIP_TRY(hipMemcpyAsync(w->y.p, gr27.data(), gr27.size() * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(w->y.as<uint32_t>() + gr27.size(), nbits_words.data(), nbits_words.size() * 4,
+                         hipMemcpyHostToDevice, st));
+  HIP_TRY(launch_paillier_encrypt(S, d_rcol, rstride, d_m, count, mc.d, w->y.as<uint32_t>(),
+                                  w->y.as<uint32_t>() + gr27.size(), nbits, mc.n0, d_out, st));
+  HIP_TRY(hipStreamSynchronize(st));  // host vectors above must outlive the async copies
+  return DDS_OK;
+}
+}  // namespace
+
+int dds_paillier_encrypt_batch(dds_ctx* ctx, const uint8_t* n_be, size_t n_bytes, const uint8_t* g_be, size_t g_bytes,
+                               const uint32_t* m, const uint8_t* r_be, size_t r_width, size_t count, uint8_t* out,
+                               size_t nsq_bytes) {
+  try {
+    if (!ctx || !n_be || !g_be || r_width == 0 || (count && (!m || !r_be || !out))) return fail(DDS_E_ARG, "bad args");
+    if (count == 0) return DDS_OK;
+    bn::Limbs n = bn::from_be(n_be, n_bytes);
+    bn::Limbs nsq = bn::mul(n, n);
+    if (nsq_bytes < bn::byte_length(nsq)) return fail(DDS_E_BUFSIZE, "nsq_bytes too small");
+    std::vector<uint8_t> nsq_be(bn::byte_length(nsq));
+    bn::to_be(nsq, nsq_be.data(), nsq_be.size());
+    std::shared_ptr<ModConsts> mc;
+    int rc = get_mod(ctx, nsq_be.data(), nsq_be.size(), &mc);
+    if (rc) return rc;
+    bn::Limbs g = bn::from_be(g_be, g_bytes);
+    WorkerLease wl(ctx);
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    const int S = mc->S;
+    const size_t stride = round_up(count, 64);
+    HIP_TRY(w->x.ensure((size_t)S * stride * 4));
+    HIP_TRY(w->x2.ensure((size_t)S * stride * 4));
+    HIP_TRY(w->misc.ensure(count * 4));
+    if ((rc = ingest(ctx, w, wl.st, *mc, r_be, r_width, count, w->in, w->x.as<uint32_t>(), stride))) return rc;
+    HIP_TRY(hipMemcpyAsync(w->misc.p, m, count * 4, hipMemcpyHostToDevice, wl.st));
+    if ((rc = encrypt_device(ctx, w, wl.st, *mc, n, g, w->misc.as<uint32_t>(), w->x.as<uint32_t>(), stride, count,
+                             w->x2.as<uint32_t>(), true)))
+      return rc;
+    std::vector<uint32_t> h((size_t)S * stride);
+    HIP_TRY(hipMemcpy(h.data(), w->x2.p, h.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> limbs(S);
+    for (size_t i = 0; i < count; ++i) {
+      for (int l = 0; l < S; ++l) limbs[l] = h[(size_t)l * stride + i];
+      if (!bn::to_be(bn::from_r27(limbs.data(), S), out + i * nsq_bytes, nsq_bytes))
+        return fail(DDS_E_RANGE, "result does not fit");
+    }
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+static uint64_t splitmix64_host(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+int dds_col_fill_paillier_synth(dds_col* col, const uint8_t* n_be, size_t n_bytes, const uint8_t* g_be,
+                                size_t g_bytes, uint64_t seed, uint64_t row0, size_t count, uint32_t pool_size) {
+  try {
+    if (!col || !n_be || !g_be || pool_size == 0) return fail(DDS_E_ARG, "bad arguments");
+    std::lock_guard<std::mutex> lk(col->mu);
+    if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
+    ModConsts& mc = *col->mc;
+    bn::Limbs n = bn::from_be(n_be, n_bytes), g = bn::from_be(g_be, g_bytes);
+    if (bn::cmp(bn::mul(n, n), mc.N) != 0) return fail(DDS_E_ARG, "column modulus is not n^2");
+    const int S = mc.S;
+    const uint32_t tcount = 10000;  // DDSDataGenerator.scala:274 Random.nextInt(10000)
+    WorkerLease wl(col->ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    hipStream_t st = wl.st;
+    // table T[m] = g^m (encrypt kernel with r = 1 and exponent n disabled)
+    const size_t ts = round_up(tcount, 64), ps = round_up(pool_size, 64);
+    HIP_TRY(w->misc.ensure((size_t)S * ts * 4));                      // T
+    HIP_TRY(w->misc2.ensure((size_t)S * ps * 4 * 2));                 // pool (plain) + pool (Montgomery)
+    HIP_TRY(w->x.ensure((size_t)S * std::max(ts, ps) * 4));           // r column
+    HIP_TRY(w->in2.ensure((size_t)std::max(ts, ps) * 4));             // exponents m
+    std::vector<uint32_t> ones((size_t)S * ts, 0), ms(ts, 0);
+    for (size_t i = 0; i < ts; ++i) ones[i] = 1;  // limb 0 = 1
+    for (uint32_t i = 0; i < tcount; ++i) ms[i] = i;
+    HIP_TRY(hipMemcpyAsync(w->x.p, ones.data(), ones.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(w->in2.p, ms.data(), ms.size() * 4, hipMemcpyHostToDevice, st));
+    if ((rc = encrypt_device(col->ctx, w, st, mc, n, g, w->in2.as<uint32_t>(), w->x.as<uint32_t>(), ts, tcount,
+                             w->misc.as<uint32_t>(), false)))
+      return rc;
+    // pool P_j = r_j^n (encrypt with m = 0), r_j from seed
+    std::vector<uint32_t> rcol((size_t)S * ps, 0), zeros(ps, 0);
+    for (uint32_t j = 0; j < pool_size; ++j) {
+      bn::Limbs r(n.size(), 0);
+      for (size_t q = 0; q < r.size(); ++q)
+        r[q] = (uint32_t)splitmix64_host(seed * 0x100000001B3ull + ((uint64_t)j << 20) + q);
+      bn::trim(r);
+      r = bn::mod(r, n);
+      if (r.empty()) r = bn::Limbs{1};
+      auto r27 = bn::to_r27(r, S);
+      for (int l = 0; l < S; ++l) rcol[(size_t)l * ps + j] = r27[l];
+    }
+    HIP_TRY(hipMemcpyAsync(w->x.p, rcol.data(), rcol.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(w->in2.p, zeros.data(), zeros.size() * 4, hipMemcpyHostToDevice, st));
+    uint32_t* pool_plain = w->misc2.as<uint32_t>();
+    uint32_t* pool_mont = pool_plain + (size_t)S * ps;
+    if ((rc = encrypt_device(col->ctx, w, st, mc, n, g, w->in2.as<uint32_t>(), w->x.as<uint32_t>(), ps, pool_size,
+                             pool_plain, true)))
+      return rc;
+    // Montgomery form P*R mod N = pairs(P, R mod N)
+    std::vector<uint32_t> rmod_col((size_t)S * ps, 0);
+    for (int l = 0; l < S; ++l)
+      for (size_t j = 0; j < ps; ++j) rmod_col[(size_t)l * ps + j] = mc.host[(size_t)kConstRmod * S + l];
+    HIP_TRY(hipMemcpyAsync(w->x.p, rmod_col.data(), rmod_col.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_pairs(S, pool_plain, w->x.as<uint32_t>(), ps, pool_size, mc.d, mc.n0, pool_mont, st));
+    HIP_TRY(launch_synth_rows(S, w->misc.as<uint32_t>(), ts, tcount, pool_mont, ps, pool_size, seed, row0, count, mc.d,
+                              mc.n0, col->d + col->count, col->stride, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    col->count += count;
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+// ---- OPE filter ------------------------------------------------------------------
+int dds_ope_filter_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_valid, size_t n, int64_t bound, int op,
+                          uint32_t* d_out, size_t* out_n) {
+  try {
+    if (!ctx || !out_n || op < 0 || op > 3 || (n && (!d_col || !d_out))) return fail(DDS_E_ARG, "bad arguments");
+    if (n > 0xFFFFFFFFull) return fail(DDS_E_ARG, "row index exceeds 32 bits");
+    *out_n = 0;
+    if (n == 0) return DDS_OK;
+    WorkerLease wl(ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    const size_t nb = ope_blocks(n);
+    HIP_TRY(w->misc.ensure(nb * 4));
+    HIP_TRY(w->flags.ensure(16));
+    record_time(ctx, w, wl.st, true, 2);
+    HIP_TRY(launch_ope_filter(d_col, d_valid, n, bound, op, w->misc.as<uint32_t>(), w->flags.as<uint64_t>(), d_out,
+                              wl.st));
+    record_time(ctx, w, wl.st, false, 2);
+    uint64_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, w->flags.p, 8, hipMemcpyDeviceToHost, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    if (ctx->timing.load()) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, w->ev[2], w->ev[3]) == hipSuccess) {
+        std::lock_guard<std::mutex> lk(ctx->tmu);
+        ctx->total_ms += ms;
+      }
+    }
+    *out_n = (size_t)total;
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_ope_filter(dds_ctx* ctx, const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op,
+                   uint32_t* out_idx, size_t* out_n) {
+  try {
+    if (!ctx || !out_n || op < 0 || op > 3 || (n && (!col || !out_idx))) return fail(DDS_E_ARG, "bad arguments");
+    *out_n = 0;
+    if (n == 0) return DDS_OK;
+    WorkerLease wl(ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    HIP_TRY(w->in.ensure(n * 8));
+    HIP_TRY(w->in2.ensure(n));
+    HIP_TRY(w->out.ensure(n * 4));
+    HIP_TRY(hipMemcpyAsync(w->in.p, col, n * 8, hipMemcpyHostToDevice, wl.st));
+    if (valid) HIP_TRY(hipMemcpyAsync(w->in2.p, valid, n, hipMemcpyHostToDevice, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    // run on the same worker's buffers through the device entry point
+    const int64_t* dcol = w->in.as<int64_t>();
+    const uint8_t* dvalid = valid ? w->in2.as<uint8_t>() : nullptr;
+    uint32_t* dout = w->out.as<uint32_t>();
+    size_t got = 0;
+    if ((rc = dds_ope_filter_device(ctx, dcol, dvalid, n, bound, op, dout, &got))) return rc;
+    if (got) HIP_TRY(hipMemcpy(out_idx, dout, got * 4, hipMemcpyDeviceToHost));
+    *out_n = got;
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+// ---- decimal route entry points ----------------------------------------------------
+namespace {
+int parse_values(const char* const* values, size_t count, std::vector<bn::Limbs>* mags, std::vector<bool>* negs) {
+  mags->resize(count);
+  negs->assign(count, false);
+  for (size_t i = 0; i < count; ++i) {
+    if (!values[i]) return fail(DDS_E_ARG, "NULL operand");
+    bool neg = false;
+    if (!bn::from_dec(values[i], strlen(values[i]), (*mags)[i], &neg))
+      return fail(DDS_E_FORMAT, std::string("NumberFormatException: ") + values[i]);
+    (*negs)[i] = neg;
+  }
+  return DDS_OK;
+}
+
+int write_dec(const std::string& s, char* out, size_t out_cap, size_t* out_len) {
+  if (out_len) *out_len = s.size();
+  if (!out || out_cap < s.size() + 1) return fail(DDS_E_BUFSIZE, "output buffer too small");
+  memcpy(out, s.c_str(), s.size() + 1);
+  return DDS_OK;
+}
+
+// shared by SumAll (nsqr) and MultAll (pubkey modulus): acc = prod mod M over decimal operands
+int fold_dec(dds_ctx* ctx, const char* const* values, size_t count, const char* mod_dec, bool additive, char* out,
+             size_t out_cap, size_t* out_len) {
+  if (!ctx || (count && !values)) return fail(DDS_E_ARG, "bad arguments");
+  if (count == 0) return fail(DDS_E_EMPTY, "no operand");
+  std::vector<bn::Limbs> mags;
+  std::vector<bool> negs;
+  int rc = parse_values(values, count, &mags, &negs);
+  if (rc) return rc;
+  if (count == 1) return write_dec(bn::to_dec(mags[0], negs[0]), out, out_cap, out_len);  // unreduced (:416-417)
+  if (!mod_dec) {
+    if (!additive) return fail(DDS_E_UNSUPPORTED, "unbounded product (MultAll without pubkey) not implemented");
+    // plain sum: positives and negatives summed separately on the GPU
+    size_t width = 1;
+    for (auto& m : mags) width = std::max(width, bn::byte_length(m));
+    std::vector<uint8_t> pos, neg;
+    size_t npos = 0, nneg = 0;
+    for (size_t i = 0; i < count; ++i) {
+      auto& dst = negs[i] ? neg : pos;
+      size_t off = dst.size();
+      dst.resize(off + width);
+      bn::to_be(mags[i], dst.data() + off, width);
+      (negs[i] ? nneg : npos)++;
+    }
+    bn::Limbs sp, sn;
+    std::vector<uint8_t> buf(width + 16);
+    size_t len = 0;
+    if (npos) {
+      if ((rc = dds_bigint_sum(ctx, pos.data(), width, npos, buf.data(), buf.size(), &len))) return rc;
+      sp = bn::from_be(buf.data(), len);
+    }
+    if (nneg) {
+      if ((rc = dds_bigint_sum(ctx, neg.data(), width, nneg, buf.data(), buf.size(), &len))) return rc;
+      sn = bn::from_be(buf.data(), len);
+    }
+    const bool rneg = bn::cmp(sp, sn) < 0;
+    bn::Limbs r = rneg ? bn::sub(sn, sp) : bn::sub(sp, sn);
+    return write_dec(bn::to_dec(r, rneg), out, out_cap, out_len);
+  }
+  bn::Limbs M;
+  bool mneg = false;
+  if (!bn::from_dec(mod_dec, strlen(mod_dec), M, &mneg) || mneg || M.empty())
+    return fail(DDS_E_FORMAT, "modulus: NumberFormatException / non-positive");
+  const size_t mb = bn::byte_length(M);
+  // operands to residues in [0, M): negatives are mapped to M - (|x| mod M) (Java BigInteger.mod)
+  // operands wider than the modulus (garbage rows) are reduced here so that the
+  // result still matches BigInteger semantics; well-formed ciphertexts are < M.
+  const size_t width = mb;
+  for (size_t i = 0; i < count; ++i) {
+    if (negs[i]) {
+      bn::Limbs r = bn::mod(mags[i], M);
+      mags[i] = r.empty() ? r : bn::sub(M, r);
+    } else if (bn::byte_length(mags[i]) > mb) {
+      mags[i] = bn::mod(mags[i], M);
+    }
+  }
+  std::vector<uint8_t> ops(count * width), mbe(mb), res(mb);
+  for (size_t i = 0; i < count; ++i) bn::to_be(mags[i], ops.data() + i * width, width);
+  bn::to_be(M, mbe.data(), mb);
+  size_t len = 0;
+  rc = dds_modmul_fold(ctx, mbe.data(), mb, ops.data(), width, count, res.data(), res.size(), &len);
+  if (rc) return rc;
+  return write_dec(bn::to_dec(bn::from_be(res.data(), len)), out, out_cap, out_len);
+}
+}  // namespace
+
+int dds_sum_all_dec(dds_ctx* ctx, const char* const* values, size_t count, const char* nsqr_dec, char* out,
+                    size_t out_cap, size_t* out_len) {
+  try {
+    return fold_dec(ctx, values, count, nsqr_dec, true, out, out_cap, out_len);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_mult_all_dec(dds_ctx* ctx, const char* const* values, size_t count, const char* n_dec, char* out,
+                     size_t out_cap, size_t* out_len) {
+  try {
+    return fold_dec(ctx, values, count, n_dec, false, out, out_cap, out_len);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,590 @@
+// HIP kernels of the homomorphic aggregation engine (gfx950 only).
+//
+// Column layout in HBM ("r27 column"): limb-transposed radix-2^27 words,
+//   X[l * stride + row], l in [0, S), stride >= rows (multiple of 64),
+// so that the lanes of a wave touch consecutive rows of one limb (coalesced).
+//
+// Reference operations accelerated (all in /root/reference/src/main/scala/):
+//   SumAll fold   dds/http/DDSRestServer.scala:397-446  -> k_fold + k_finalize
+//   MultAll fold  dds/http/DDSRestServer.scala:491-539  -> k_fold + k_finalize
+//   Sum / Mult    dds/http/DDSRestServer.scala:355-395, 447-490 -> k_pairs
+//   Search{Gt,GtEq,Lt,LtEq} DDSRestServer.scala:682-830 -> k_ope_count / k_ope_scatter
+//   HomoAdd.encrypt  utils/SJHomoLibProvider.scala:58 -> k_paillier_encrypt
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ddshe_device.hpp"
+#include "ddshe_launch.hpp"
+
+namespace ddshe {
+
+// ------------------------------------------------------------------------------
+// group helpers
+// ------------------------------------------------------------------------------
+template <int S, int TPI>
+struct Grp {
+  using M = Mont<S, TPI>;
+  static constexpr int L = M::L;
+  int r;        // lane index in group
+  bool top;     // r == TPI-1
+  bool bottom;  // r == 0
+  __device__ __forceinline__ Grp() {
+    r = (int)(threadIdx.x % TPI);
+    top = r == TPI - 1;
+    bottom = r == 0;
+  }
+  __device__ __forceinline__ void load_col(uint32_t (&a)[L], const uint32_t* __restrict__ col, size_t stride,
+                                           size_t row) const {
+#pragma unroll
+    for (int l = 0; l < L; ++l) a[l] = col[(size_t)(r * L + l) * stride + row];
+  }
+  __device__ __forceinline__ void store_col(const uint32_t (&a)[L], uint32_t* __restrict__ col, size_t stride,
+                                            size_t row) const {
+#pragma unroll
+    for (int l = 0; l < L; ++l) col[(size_t)(r * L + l) * stride + row] = a[l];
+  }
+  __device__ __forceinline__ void load_vec(uint32_t (&a)[L], const uint32_t* __restrict__ v) const {
+#pragma unroll
+    for (int l = 0; l < L; ++l) a[l] = v[r * L + l];
+  }
+  // sign(a - n) for fully normalised a (group-wide result)
+  __device__ __forceinline__ int cmp(const uint32_t (&a)[L], const uint32_t (&n)[L]) const {
+    int c = 0;
+#pragma unroll
+    for (int l = 0; l < L; ++l) c = a[l] > n[l] ? 1 : (a[l] < n[l] ? -1 : c);
+    int res = 0;
+    for (int s = TPI - 1; s >= 0; --s) {
+      int v = (int)M::group_read((uint32_t)c, s, r);
+      res = res != 0 ? res : v;
+    }
+    return res;
+  }
+  // a -= n (a >= n, both fully normalised)
+  __device__ __forceinline__ void sub(uint32_t (&a)[L], const uint32_t (&n)[L]) const {
+    uint32_t br = 0;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      const uint32_t d = a[l] - n[l] - br;
+      br = d >> 31;  // borrow iff wrapped (operands < 2^27)
+      a[l] = d & kMask;
+    }
+    for (int round = 1; round < TPI; ++round) {
+      uint32_t bin = grp_from_prev<TPI>(br);
+      if (bottom) bin = 0;
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        const uint32_t d = a[l] - bin;
+        bin = d >> 31;
+        a[l] = d & kMask;
+      }
+      br = bin;
+    }
+  }
+  // value < 2N, almost normalised -> canonical [0, N), fully normalised
+  __device__ __forceinline__ void canon(uint32_t (&a)[L], const uint32_t (&n)[L]) const {
+    M::normalize(a, bottom);
+    if (cmp(a, n) >= 0) sub(a, n);
+  }
+};
+
+// ------------------------------------------------------------------------------
+// ingest: big-endian fixed-width rows -> r27 column (+ range classification)
+// ------------------------------------------------------------------------------
+// flags[0] |= 1 if some row is >= 2N (needs k_reduce_rows), flags[0] |= 2 if some
+// row does not fit in S r27 limbs (boundary error DDS_E_RANGE).
+__global__ void k_ingest_be(const uint8_t* __restrict__ in, size_t width, size_t count, int S,
+                            const uint32_t* __restrict__ n2x /* 2N in r27, S+1 limbs */, uint32_t* __restrict__ X,
+                            size_t stride, uint32_t* __restrict__ flags) {
+  const size_t row = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= count) return;
+  const uint8_t* p = in + row * width;
+  uint64_t bitbuf = 0;
+  int nbits = 0, l = 0, cmpv = 0;
+  bool overflow = false;
+  for (size_t i = 0; i < width; ++i) {
+    bitbuf |= (uint64_t)p[width - 1 - i] << nbits;
+    nbits += 8;
+    while (nbits >= 27) {
+      uint32_t limb = (uint32_t)bitbuf & kMask;
+      bitbuf >>= 27;
+      nbits -= 27;
+      if (l < S) {
+        X[(size_t)l * stride + row] = limb;
+        uint32_t nl = n2x[l];
+        cmpv = limb > nl ? 1 : (limb < nl ? -1 : cmpv);
+      } else if (limb) {
+        overflow = true;
+      }
+      ++l;
+    }
+  }
+  while (l < S + 1) {
+    uint32_t limb = (uint32_t)bitbuf & kMask;
+    bitbuf >>= 27;
+    if (l < S) {
+      X[(size_t)l * stride + row] = limb;
+      uint32_t nl = n2x[l];
+      cmpv = limb > nl ? 1 : (limb < nl ? -1 : cmpv);
+    } else if (limb) {
+      overflow = true;
+    }
+    ++l;
+  }
+  // 2N may need limb S (if 2N >= 2^(27S)); row limbs beyond S are zero here
+  if (n2x[S] != 0) cmpv = -1;
+  if (overflow) atomicOr(flags, 2u);
+  else if (cmpv >= 0) atomicOr(flags, 1u);
+}
+
+// rows >= 2N: x <- MonPro(MonPro(x, R^2 mod N), 1) = x mod N
+template <int S, int TPI>
+__global__ void __launch_bounds__(256) k_reduce_rows(uint32_t* __restrict__ X, size_t stride, size_t count,
+                                                     const uint32_t* __restrict__ consts, uint32_t n0) {
+  using G = Grp<S, TPI>;
+  using M = Mont<S, TPI>;
+  constexpr int L = G::L;
+  G g;
+  const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
+  if (grp >= count) return;
+  const uint32_t* N = consts + kConstN * S;
+  const uint32_t* N2 = consts + kConstN2x * S;
+  const uint32_t* R2 = consts + kConstR2 * S;
+  const uint32_t* ONE = consts + kConstOne * S;
+  uint32_t n[L], a[L], n2[L];
+  g.load_vec(n, N);
+  g.load_vec(n2, N2);
+  g.load_col(a, X, stride, grp);
+  // 2N fits in S limbs (S chosen with 2 bits of headroom)
+  if (g.cmp(a, n2) < 0) return;
+  M::mul_col(a, n, R2, 1, n0, g.top, g.bottom);
+  M::mul_col(a, n, ONE, 1, n0, g.top, g.bottom);
+  M::normalize(a, g.bottom);
+  g.store_col(a, X, stride, grp);
+}
+
+// ------------------------------------------------------------------------------
+// fold: each group folds rows g, g+G, g+2G, ... with Montgomery products.
+// A group that folded c rows holds prod * R^(1-c); an empty group holds R mod N.
+// ------------------------------------------------------------------------------
+template <int S, int TPI>
+__global__ void __launch_bounds__(256) k_fold(const uint32_t* __restrict__ X, size_t xstride, size_t count,
+                                              const uint32_t* __restrict__ consts, uint32_t n0,
+                                              uint32_t* __restrict__ P, size_t pstride, size_t ngroups) {
+  using G = Grp<S, TPI>;
+  using M = Mont<S, TPI>;
+  constexpr int L = G::L;
+  G g;
+  const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
+  if (grp >= ngroups) return;
+  uint32_t n[L], a[L];
+  g.load_vec(n, consts + kConstN * S);
+  size_t row = grp;
+  if (row < count) {
+    g.load_col(a, X, xstride, row);
+    row += ngroups;
+  } else {
+    g.load_vec(a, consts + kConstRmod * S);
+  }
+  for (; row < count; row += ngroups) M::mul_col(a, n, X + row, xstride, n0, g.top, g.bottom);
+  M::normalize(a, g.bottom);
+  g.store_col(a, P, pstride, grp);
+}
+
+// result = canon(MonPro(P[0], Y)), Y = R^k mod N; writes S r27 limbs to out
+template <int S, int TPI>
+__global__ void __launch_bounds__(64) k_finalize(const uint32_t* __restrict__ P, size_t pstride,
+                                                 const uint32_t* __restrict__ consts, const uint32_t* __restrict__ Y,
+                                                 uint32_t n0, uint32_t* __restrict__ out) {
+  using G = Grp<S, TPI>;
+  using M = Mont<S, TPI>;
+  constexpr int L = G::L;
+  G g;
+  if (threadIdx.x >= TPI) return;
+  uint32_t n[L], a[L];
+  g.load_vec(n, consts + kConstN * S);
+  g.load_col(a, P, pstride, 0);
+  M::mul_col(a, n, Y, 1, n0, g.top, g.bottom);
+  g.canon(a, n);
+#pragma unroll
+  for (int l = 0; l < L; ++l) out[g.r * L + l] = a[l];
+}
+
+// out[i] = A[i]*B[i] mod N (canonical), r27 columns in and out
+template <int S, int TPI>
+__global__ void __launch_bounds__(256) k_pairs(const uint32_t* __restrict__ A, const uint32_t* __restrict__ B,
+                                               size_t stride, size_t count, const uint32_t* __restrict__ consts,
+                                               uint32_t n0, uint32_t* __restrict__ O) {
+  using G = Grp<S, TPI>;
+  using M = Mont<S, TPI>;
+  constexpr int L = G::L;
+  G g;
+  const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
+  if (grp >= count) return;
+  uint32_t n[L], a[L];
+  g.load_vec(n, consts + kConstN * S);
+  g.load_col(a, A, stride, grp);
+  M::mul_col(a, n, B + grp, stride, n0, g.top, g.bottom);               // a*b*R^-1
+  M::mul_col(a, n, consts + kConstR2 * S, 1, n0, g.top, g.bottom);      // a*b
+  g.canon(a, n);
+  g.store_col(a, O, stride, grp);
+}
+
+// ------------------------------------------------------------------------------
+// Montgomery exponentiation helpers (register operands via ds_bpermute)
+// ------------------------------------------------------------------------------
+// acc <- acc^e * acc_in... : left-to-right binary over the bits of a uniform exponent
+template <int S, int TPI, int L>
+__device__ __forceinline__ void mont_pow_uniform(uint32_t (&acc)[L], const uint32_t (&x)[L], const uint32_t (&n)[L],
+                                                 uint32_t n0, const uint32_t* __restrict__ ebits, int nbits,
+                                                 const Grp<S, TPI>& g) {
+  using M = Mont<S, TPI>;
+  for (int i = nbits - 1; i >= 0; --i) {
+    M::normalize(acc, g.bottom);
+    uint32_t sq[M::L];
+#pragma unroll
+    for (int l = 0; l < M::L; ++l) sq[l] = acc[l];
+    M::mul_reg(acc, sq, n, n0, g.r, g.top, g.bottom);
+    if ((ebits[i >> 5] >> (i & 31)) & 1u) M::mul_reg(acc, x, n, n0, g.r, g.top, g.bottom);
+  }
+}
+
+// c_i = g^m_i * r_i^n mod N (N = n^2). Inputs r in r27 column (values < N), m per row.
+// consts: N, gR (g*R mod N, Montgomery form), Rmod (1 in Montgomery form), R2, One
+template <int S, int TPI>
+__global__ void __launch_bounds__(256) k_paillier_encrypt(const uint32_t* __restrict__ Rcol, size_t stride,
+                                                          const uint32_t* __restrict__ m, size_t count,
+                                                          const uint32_t* __restrict__ consts,
+                                                          const uint32_t* __restrict__ gR,
+                                                          const uint32_t* __restrict__ nbits_words, int nbits,
+                                                          uint32_t n0, uint32_t* __restrict__ O) {
+  using G = Grp<S, TPI>;
+  using M = Mont<S, TPI>;
+  constexpr int L = G::L;
+  G g;
+  const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
+  if (grp >= count) return;
+  uint32_t n[L], x[L], acc[L], gx[L], acc2[L];
+  g.load_vec(n, consts + kConstN * S);
+  g.load_col(x, Rcol, stride, grp);
+  M::mul_col(x, n, consts + kConstR2 * S, 1, n0, g.top, g.bottom);  // r*R
+  M::normalize(x, g.bottom);
+  g.load_vec(acc, consts + kConstRmod * S);                         // 1*R
+  mont_pow_uniform<S, TPI, L>(acc, x, n, n0, nbits_words, nbits, g);   // r^n * R
+  // g^m with a per-row exponent: multiply-always with a select to stay uniform
+  g.load_vec(gx, gR);
+  g.load_vec(acc2, consts + kConstRmod * S);
+  const uint32_t mi = m[grp];
+  const uint32_t mbits = mi ? 32u - (uint32_t)__builtin_clz(mi) : 0u;
+  // wave-uniform trip count (max over the wave's groups)
+  uint32_t wb = mbits;
+  for (int off = 32; off >= 1; off >>= 1) wb = max(wb, (uint32_t)__shfl_xor((int)wb, off));
+  uint32_t one[L];
+  g.load_vec(one, consts + kConstRmod * S);
+  for (int i = (int)wb - 1; i >= 0; --i) {
+    M::normalize(acc2, g.bottom);
+    uint32_t sq[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) sq[l] = acc2[l];
+    M::mul_reg(acc2, sq, n, n0, g.r, g.top, g.bottom);
+    uint32_t sel[L];
+    const bool bit = (mi >> i) & 1u;
+#pragma unroll
+    for (int l = 0; l < L; ++l) sel[l] = bit ? gx[l] : one[l];
+    M::mul_reg(acc2, sel, n, n0, g.r, g.top, g.bottom);
+  }
+  M::normalize(acc2, g.bottom);
+  M::mul_reg(acc, acc2, n, n0, g.r, g.top, g.bottom);               // g^m r^n R
+  M::mul_col(acc, n, consts + kConstOne * S, 1, n0, g.top, g.bottom);  // g^m r^n
+  g.canon(acc, n);
+  g.store_col(acc, O, stride, grp);
+}
+
+// ------------------------------------------------------------------------------
+// synthetic Paillier rows (bench / tests): c_i = T[m_i] * P[a_i] * P[b_i] mod N
+// T: table of g^m (plain), P: pool of r^n in Montgomery form (r^n * R mod N).
+// Indices come from splitmix64(seed, row), so the host can recompute sum(m_i).
+// ------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+template <int S, int TPI>
+__global__ void __launch_bounds__(256) k_synth_rows(const uint32_t* __restrict__ T, size_t tstride, uint32_t tcount,
+                                                    const uint32_t* __restrict__ P, size_t pstride, uint32_t pcount,
+                                                    uint64_t seed, uint64_t row0, size_t count,
+                                                    const uint32_t* __restrict__ consts, uint32_t n0,
+                                                    uint32_t* __restrict__ X, size_t xstride) {
+  using G = Grp<S, TPI>;
+  using M = Mont<S, TPI>;
+  constexpr int L = G::L;
+  G g;
+  const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
+  if (grp >= count) return;
+  const uint64_t h = splitmix64(seed ^ splitmix64(row0 + grp));
+  const uint32_t mi = (uint32_t)(h % tcount);
+  const uint32_t ai = (uint32_t)((h >> 20) % pcount);
+  const uint32_t bi = (uint32_t)((h >> 42) % pcount);
+  uint32_t n[L], a[L];
+  g.load_vec(n, consts + kConstN * S);
+  g.load_col(a, T, tstride, mi);
+  M::mul_col(a, n, P + ai, pstride, n0, g.top, g.bottom);
+  M::normalize(a, g.bottom);
+  M::mul_col(a, n, P + bi, pstride, n0, g.top, g.bottom);
+  g.canon(a, n);
+  g.store_col(a, X, xstride, grp);
+}
+
+// ------------------------------------------------------------------------------
+// OPE range filter: keep row i iff valid[i] && col[i] <op> bound (signed int64)
+// DDSRestServer.scala:704 (Gt), :742 (GtEq), :779 (Lt), :816 (LtEq)
+// ------------------------------------------------------------------------------
+__device__ __forceinline__ bool ope_pred(int64_t c, int64_t b, int op) {
+  switch (op) {
+    case 0: return c > b;
+    case 1: return c >= b;
+    case 2: return c < b;
+    default: return c <= b;
+  }
+}
+
+constexpr int kOpeBlock = 256;
+constexpr int kOpeItems = 16;  // rows per thread
+constexpr size_t kOpeTile = (size_t)kOpeBlock * kOpeItems;
+
+__device__ __forceinline__ uint32_t ope_thread_mask(const int64_t* __restrict__ col, const uint8_t* __restrict__ valid,
+                                                    size_t n, int64_t bound, int op, size_t base) {
+  uint32_t mask = 0;
+#pragma unroll
+  for (int k = 0; k < kOpeItems; ++k) {
+    const size_t i = base + (size_t)k * kOpeBlock;
+    if (i < n) {
+      const bool v = valid ? valid[i] != 0 : true;
+      if (v && ope_pred(col[i], bound, op)) mask |= 1u << k;
+    }
+  }
+  return mask;
+}
+
+__global__ void __launch_bounds__(kOpeBlock) k_ope_count(const int64_t* __restrict__ col,
+                                                         const uint8_t* __restrict__ valid, size_t n, int64_t bound,
+                                                         int op, uint32_t* __restrict__ block_counts) {
+  __shared__ uint32_t wsum[kOpeBlock / 64];
+  const size_t base = (size_t)blockIdx.x * kOpeTile + threadIdx.x;
+  const uint32_t c = __builtin_popcount(ope_thread_mask(col, valid, n, bound, op, base));
+  uint32_t s = c;
+  for (int off = 32; off >= 1; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kOpeBlock / 64; ++w) t += wsum[w];
+    block_counts[blockIdx.x] = t;
+  }
+}
+
+// exclusive scan of block counts (single block; nblocks up to 64k handled by a serial tail per thread)
+__global__ void __launch_bounds__(1024) k_ope_scan(uint32_t* __restrict__ counts, size_t nblocks,
+                                                   uint64_t* __restrict__ total) {
+  __shared__ uint64_t part[1024];
+  const size_t per = (nblocks + 1023) / 1024;
+  const size_t b0 = threadIdx.x * per, b1 = min(nblocks, b0 + per);
+  uint64_t s = 0;
+  for (size_t b = b0; b < b1; ++b) s += counts[b];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    uint64_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint64_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+  for (size_t b = b0; b < b1; ++b) {
+    uint32_t c = counts[b];
+    counts[b] = (uint32_t)run;
+    run += c;
+  }
+  if (threadIdx.x == 1023) *total = part[1023];
+}
+
+__global__ void __launch_bounds__(kOpeBlock) k_ope_scatter(const int64_t* __restrict__ col,
+                                                           const uint8_t* __restrict__ valid, size_t n, int64_t bound,
+                                                           int op, const uint32_t* __restrict__ block_offsets,
+                                                           uint32_t* __restrict__ out) {
+  // Stable order: rows of a tile are numbered k*256 + tid, so scan over (k, tid) in row order.
+  __shared__ uint32_t wtot[kOpeItems][kOpeBlock / 64];
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const size_t base = (size_t)blockIdx.x * kOpeTile + tid;
+  const uint32_t mask = ope_thread_mask(col, valid, n, bound, op, base);
+  uint32_t before_in_wave[kOpeItems];
+#pragma unroll
+  for (int k = 0; k < kOpeItems; ++k) {
+    const uint64_t bal = __ballot((mask >> k) & 1u);
+    before_in_wave[k] = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wtot[k][wid] = (uint32_t)__popcll(bal);
+  }
+  __syncthreads();
+  uint32_t off = block_offsets[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kOpeItems; ++k) {
+    uint32_t pre = 0;
+    for (int w = 0; w < kOpeBlock / 64; ++w) pre += (w < wid) ? wtot[k][w] : 0u;
+    if ((mask >> k) & 1u) out[off + pre + before_in_wave[k]] = (uint32_t)(base + (size_t)k * kOpeBlock);
+    uint32_t tot = 0;
+    for (int w = 0; w < kOpeBlock / 64; ++w) tot += wtot[k][w];
+    off += tot;
+  }
+}
+
+// ------------------------------------------------------------------------------
+// plain (unmodular) big-integer sum: SumAll without nsqr (DDSRestServer.scala:425)
+// Each thread accumulates 64-bit lazy limb sums over a strided slice of rows.
+// ------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_plain_sum(const uint32_t* __restrict__ X, size_t stride, size_t count,
+                                                   int S, size_t nthreads, uint64_t* __restrict__ part) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nthreads) return;
+  for (int l = 0; l < S; ++l) {
+    uint64_t s = 0;
+    for (size_t row = t; row < count; row += nthreads) s += X[(size_t)l * stride + row];
+    part[(size_t)l * nthreads + t] = s;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_plain_sum_reduce(const uint64_t* __restrict__ part, size_t nthreads, int S,
+                                                          uint64_t* __restrict__ out) {
+  __shared__ uint64_t sh[256];
+  const int l = blockIdx.x;
+  uint64_t s = 0;
+  for (size_t t = threadIdx.x; t < nthreads; t += 256) s += part[(size_t)l * nthreads + t];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off >= 1; off >>= 1) {
+    if ((int)threadIdx.x < off) sh[threadIdx.x] += sh[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[l] = sh[0];
+}
+
+// ------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------
+#define DDSHE_DISPATCH(S_, TPI_, ...) \
+  case S_: {                          \
+    constexpr int S = S_, TPI = TPI_; \
+    __VA_ARGS__;                      \
+  } break;
+
+#define DDSHE_SWITCH(S_RT, ...)                 \
+  switch (S_RT) {                               \
+    DDSHE_DISPATCH(40, 1, __VA_ARGS__)          \
+    DDSHE_DISPATCH(76, 2, __VA_ARGS__)          \
+    DDSHE_DISPATCH(152, 4, __VA_ARGS__)         \
+    DDSHE_DISPATCH(232, 8, __VA_ARGS__)         \
+    default: return hipErrorInvalidValue;       \
+  }
+
+int tpi_for(int S) {
+  switch (S) {
+    case 40: return 1;
+    case 76: return 2;
+    case 152: return 4;
+    case 232: return 8;
+    default: return 0;
+  }
+}
+
+int pick_S(size_t mod_bits) {
+  const size_t need = mod_bits + 2;
+  const int choices[] = {40, 76, 152, 232};
+  for (int s : choices)
+    if ((size_t)27 * s >= need) return s;
+  return 0;
+}
+
+static inline unsigned grid_for(size_t threads) { return (unsigned)((threads + 255) / 256); }
+
+hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, const uint32_t* n2x, uint32_t* X,
+                            size_t stride, uint32_t* flags, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ingest_be, dim3(grid_for(count)), dim3(256), 0, st, in, width, count, S, n2x, X, stride, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, const uint32_t* consts, uint32_t n0,
+                              hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_reduce_rows<S, TPI>), dim3(grid_for(count * TPI)), dim3(256), 0, st, X, stride,
+                                     count, consts, n0));
+  return hipGetLastError();
+}
+
+hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts, uint32_t n0,
+                       uint32_t* P, size_t pstride, size_t ngroups, hipStream_t st) {
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X, xstride,
+                                     count, consts, n0, P, pstride, ngroups));
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize(int S, const uint32_t* P, size_t pstride, const uint32_t* consts, const uint32_t* Y,
+                           uint32_t n0, uint32_t* out, hipStream_t st) {
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_finalize<S, TPI>), dim3(1), dim3(64), 0, st, P, pstride, consts, Y, n0, out));
+  return hipGetLastError();
+}
+
+hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stride, size_t count,
+                        const uint32_t* consts, uint32_t n0, uint32_t* O, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_pairs<S, TPI>), dim3(grid_for(count * TPI)), dim3(256), 0, st, A, B, stride,
+                                     count, consts, n0, O));
+  return hipGetLastError();
+}
+
+hipError_t launch_paillier_encrypt(int S, const uint32_t* Rcol, size_t stride, const uint32_t* m, size_t count,
+                                   const uint32_t* consts, const uint32_t* gR, const uint32_t* nbits_words, int nbits,
+                                   uint32_t n0, uint32_t* O, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_paillier_encrypt<S, TPI>), dim3(grid_for(count * TPI)), dim3(256), 0, st,
+                                     Rcol, stride, m, count, consts, gR, nbits_words, nbits, n0, O));
+  return hipGetLastError();
+}
+
+hipError_t launch_synth_rows(int S, const uint32_t* T, size_t tstride, uint32_t tcount, const uint32_t* P,
+                             size_t pstride, uint32_t pcount, uint64_t seed, uint64_t row0, size_t count,
+                             const uint32_t* consts, uint32_t n0, uint32_t* X, size_t xstride, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_synth_rows<S, TPI>), dim3(grid_for(count * TPI)), dim3(256), 0, st, T, tstride,
+                                     tcount, P, pstride, pcount, seed, row0, count, consts, n0, X, xstride));
+  return hipGetLastError();
+}
+
+size_t ope_blocks(size_t n) { return (n + kOpeTile - 1) / kOpeTile; }
+
+hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op,
+                             uint32_t* block_counts, uint64_t* total, uint32_t* out, hipStream_t st) {
+  const size_t nb = ope_blocks(n);
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ope_count, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, bound, op, block_counts);
+  hipLaunchKernelGGL(k_ope_scan, dim3(1), dim3(1024), 0, st, block_counts, nb, total);
+  hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, bound, op, block_counts,
+                     out);
+  return hipGetLastError();
+}
+
+hipError_t launch_plain_sum(const uint32_t* X, size_t stride, size_t count, int S, size_t nthreads, uint64_t* part,
+                            uint64_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_plain_sum, dim3(grid_for(nthreads)), dim3(256), 0, st, X, stride, count, S, nthreads, part);
+  hipLaunchKernelGGL(k_plain_sum_reduce, dim3(S), dim3(256), 0, st, part, nthreads, S, out);
+  return hipGetLastError();
+}
+
+hipError_t fold_occupancy(int S, int* blocks_per_cu) {
+  DDSHE_SWITCH(S, return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (const void*)k_fold<S, TPI>, 256,
+                                                                       0));
+  return hipSuccess;
+}
+
+}  // namespace ddshe

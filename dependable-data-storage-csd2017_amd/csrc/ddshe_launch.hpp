@@ -1,0 +1,38 @@
+// Internal launcher interface between the C-ABI (ddshe_capi.cpp) and the HIP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace ddshe {
+
+// per-modulus constant block: 5 vectors of S r27 limbs each
+enum { kConstN = 0, kConstRmod = 1, kConstR2 = 2, kConstOne = 3, kConstN2x = 4, kConstCount = 5 };
+
+int pick_S(size_t mod_bits);  // limb count for a modulus of mod_bits bits (0 = unsupported)
+int tpi_for(int S);           // lanes per bignum for that S
+
+hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, const uint32_t* n2x, uint32_t* X,
+                            size_t stride, uint32_t* flags, hipStream_t st);
+hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, const uint32_t* consts, uint32_t n0,
+                              hipStream_t st);
+hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts, uint32_t n0,
+                       uint32_t* P, size_t pstride, size_t ngroups, hipStream_t st);
+hipError_t launch_finalize(int S, const uint32_t* P, size_t pstride, const uint32_t* consts, const uint32_t* Y,
+                           uint32_t n0, uint32_t* out, hipStream_t st);
+hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stride, size_t count,
+                        const uint32_t* consts, uint32_t n0, uint32_t* O, hipStream_t st);
+hipError_t launch_paillier_encrypt(int S, const uint32_t* Rcol, size_t stride, const uint32_t* m, size_t count,
+                                   const uint32_t* consts, const uint32_t* gR, const uint32_t* nbits_words, int nbits,
+                                   uint32_t n0, uint32_t* O, hipStream_t st);
+hipError_t launch_synth_rows(int S, const uint32_t* T, size_t tstride, uint32_t tcount, const uint32_t* P,
+                             size_t pstride, uint32_t pcount, uint64_t seed, uint64_t row0, size_t count,
+                             const uint32_t* consts, uint32_t n0, uint32_t* X, size_t xstride, hipStream_t st);
+size_t ope_blocks(size_t n);
+hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op,
+                             uint32_t* block_counts, uint64_t* total, uint32_t* out, hipStream_t st);
+hipError_t launch_plain_sum(const uint32_t* X, size_t stride, size_t count, int S, size_t nthreads, uint64_t* part,
+                            uint64_t* out, hipStream_t st);
+hipError_t fold_occupancy(int S, int* blocks_per_cu);
+
+}  // namespace ddshe

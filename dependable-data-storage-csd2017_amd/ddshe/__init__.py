@@ -1,0 +1,333 @@
+"""ddshe — Python binding of the MI355X homomorphic-aggregation engine (C-ABI in include/ddshe.h).
+
+The engine replaces the BigInteger fold/filter loops of the reference REST proxy
+(``src/main/scala/dds/http/DDSRestServer.scala``) and hlib's ``HomoAdd`` /
+``HomoMult`` primitives. This module only marshals arguments; every arithmetic
+entry point runs HIP kernels inside ``libddshe.so``. There is no CPU fallback:
+importing this package fails loudly if the shared library is missing, and every
+call raises :class:`DDSError` on a non-zero status.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libddshe.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"libddshe.so not built at {LIB_PATH}: run `make -C dependable-data-storage-csd2017_amd/csrc` "
+                      "or __graft_entry__.build()")
+_lib = C.CDLL(LIB_PATH)
+
+# status codes (include/ddshe.h)
+DDS_OK, DDS_E_EMPTY, DDS_E_RANGE, DDS_E_HIP, DDS_E_ARG = 0, 1, 2, 3, 4
+DDS_E_NOMEM, DDS_E_UNSUPPORTED, DDS_E_BUFSIZE, DDS_E_FORMAT = 5, 6, 7, 8
+OPE_OPS = {"gt": 0, "ge": 1, "lt": 2, "le": 3}
+
+# every symbol the header declares (checked by tests/test_abi.py without a GPU)
+EXPORTS = [
+    "dds_ctx_create", "dds_ctx_destroy", "dds_strerror", "dds_last_error", "dds_max_modulus_bits",
+    "dds_ctx_set_stream", "dds_ctx_set_timing", "dds_ctx_get_timing", "dds_ctx_reset_timing", "dds_ctx_get_fold_work",
+    "dds_modmul_fold", "dds_paillier_sum", "dds_rsa_product", "dds_modmul_pairs", "dds_bigint_sum",
+    "dds_col_create", "dds_col_destroy", "dds_col_append", "dds_col_count", "dds_col_read", "dds_col_fold",
+    "dds_col_fold_partial", "dds_col_partial_words", "dds_combine_partials", "dds_col_fill_paillier_synth",
+    "dds_ope_filter", "dds_ope_filter_device", "dds_paillier_encrypt_batch", "dds_sum_all_dec", "dds_mult_all_dec",
+]
+
+_u8p = C.POINTER(C.c_uint8)
+_sz = C.c_size_t
+_szp = C.POINTER(C.c_size_t)
+
+
+def _sig(name, res, *args):
+    f = getattr(_lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+_sig("dds_ctx_create", C.c_int, C.c_int, C.POINTER(C.c_void_p))
+_sig("dds_ctx_destroy", C.c_int, C.c_void_p)
+_sig("dds_strerror", C.c_char_p, C.c_int)
+_sig("dds_last_error", C.c_char_p)
+_sig("dds_max_modulus_bits", _sz)
+_sig("dds_ctx_set_stream", C.c_int, C.c_void_p, C.c_void_p)
+_sig("dds_ctx_set_timing", C.c_int, C.c_void_p, C.c_int)
+_sig("dds_ctx_get_timing", C.c_int, C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_double))
+_sig("dds_ctx_reset_timing", C.c_int, C.c_void_p)
+_sig("dds_ctx_get_fold_work", C.c_int, C.c_void_p, C.POINTER(C.c_uint64))
+for _n in ("dds_modmul_fold", "dds_paillier_sum", "dds_rsa_product"):
+    _sig(_n, C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, _sz, _u8p, _sz, _szp)
+_sig("dds_modmul_pairs", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, C.c_char_p, _sz, _sz, _u8p)
+_sig("dds_bigint_sum", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz, _u8p, _sz, _szp)
+_sig("dds_col_create", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz, C.POINTER(C.c_void_p))
+_sig("dds_col_destroy", C.c_int, C.c_void_p)
+_sig("dds_col_append", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz)
+_sig("dds_col_count", _sz, C.c_void_p)
+_sig("dds_col_read", C.c_int, C.c_void_p, _sz, _sz, _u8p)
+_sig("dds_col_fold", C.c_int, C.c_void_p, _sz, _sz, _u8p, _sz, _szp)
+_sig("dds_col_fold_partial", C.c_int, C.c_void_p, _sz, _sz, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64))
+_sig("dds_col_partial_words", _sz, C.c_void_p)
+_sig("dds_combine_partials", C.c_int, C.c_void_p, C.c_char_p, _sz, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), _sz,
+     _u8p, _sz, _szp)
+_sig("dds_col_fill_paillier_synth", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, C.c_uint64, C.c_uint64,
+     _sz, C.c_uint32)
+_sig("dds_ope_filter", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int64, C.c_int, C.c_void_p, _szp)
+_sig("dds_ope_filter_device", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int64, C.c_int, C.c_void_p, _szp)
+_sig("dds_paillier_encrypt_batch", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, C.POINTER(C.c_uint32),
+     C.c_char_p, _sz, _sz, _u8p, _sz)
+for _n in ("dds_sum_all_dec", "dds_mult_all_dec"):
+    _sig(_n, C.c_int, C.c_void_p, C.POINTER(C.c_char_p), _sz, C.c_char_p, C.c_char_p, _sz, _szp)
+
+
+class DDSError(RuntimeError):
+    def __init__(self, status: int, where: str):
+        self.status = status
+        detail = _lib.dds_last_error().decode(errors="replace")
+        super().__init__(f"{where}: {_lib.dds_strerror(status).decode()} ({detail})")
+
+
+class NotFound(DDSError):
+    """DDS_E_EMPTY: the reference route answers HTTP 404."""
+
+
+def _check(rc: int, where: str):
+    if rc == DDS_E_EMPTY:
+        raise NotFound(rc, where)
+    if rc != DDS_OK:
+        raise DDSError(rc, where)
+
+
+def int_to_be(x: int, width: int) -> bytes:
+    return int(x).to_bytes(width, "big")
+
+
+def ints_to_be(xs, width: int) -> bytes:
+    return b"".join(int(x).to_bytes(width, "big") for x in xs)
+
+
+def nbytes(x: int) -> int:
+    return max(1, (int(x).bit_length() + 7) // 8)
+
+
+class Engine:
+    """One dds_ctx on one GPU."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        _check(_lib.dds_ctx_create(device, C.byref(h)), "dds_ctx_create")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            _lib.dds_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- context controls ----
+    def set_stream(self, stream_ptr: int | None):
+        _check(_lib.dds_ctx_set_stream(self._h, C.c_void_p(stream_ptr or 0)), "set_stream")
+
+    def set_timing(self, on: bool):
+        _check(_lib.dds_ctx_set_timing(self._h, int(on)), "set_timing")
+
+    def reset_timing(self):
+        _check(_lib.dds_ctx_reset_timing(self._h), "reset_timing")
+
+    def timing(self):
+        """(fold_ms, fold_launches, other_ms, fold_modmuls) accumulated since reset_timing()."""
+        ms, n, tot, mm = C.c_double(), C.c_uint64(), C.c_double(), C.c_uint64()
+        _check(_lib.dds_ctx_get_timing(self._h, C.byref(ms), C.byref(n), C.byref(tot)), "get_timing")
+        _check(_lib.dds_ctx_get_fold_work(self._h, C.byref(mm)), "get_fold_work")
+        return ms.value, n.value, tot.value, mm.value
+
+    # ---- folds ----
+    def _fold(self, fn, modulus: int, ops, width: int | None = None) -> int:
+        ops = [int(x) for x in ops]
+        mb = nbytes(modulus)
+        width = width or max([mb] + [nbytes(x) for x in ops])
+        buf = ints_to_be(ops, width)
+        out = (C.c_uint8 * max(width, mb))()
+        olen = C.c_size_t()
+        _check(fn(self._h, int_to_be(modulus, mb), mb, buf, width, len(ops), out, len(out), C.byref(olen)), fn.__name__)
+        return int.from_bytes(bytes(out[: olen.value]), "big")
+
+    def modmul_fold(self, modulus: int, ops, width=None) -> int:
+        return self._fold(_lib.dds_modmul_fold, modulus, ops, width)
+
+    def paillier_sum(self, nsquare: int, ciphertexts, width=None) -> int:
+        """HomoAdd fold: DDSRestServer.scala:412-430."""
+        return self._fold(_lib.dds_paillier_sum, nsquare, ciphertexts, width)
+
+    def rsa_product(self, n: int, ciphertexts, width=None) -> int:
+        """HomoMult fold: DDSRestServer.scala:506-524."""
+        return self._fold(_lib.dds_rsa_product, n, ciphertexts, width)
+
+    def modmul_pairs(self, modulus: int, a, b) -> list[int]:
+        a, b = [int(x) for x in a], [int(x) for x in b]
+        assert len(a) == len(b)
+        mb = nbytes(modulus)
+        width = max([mb] + [nbytes(x) for x in a + b])
+        out = (C.c_uint8 * (mb * max(1, len(a))))()
+        _check(_lib.dds_modmul_pairs(self._h, int_to_be(modulus, mb), mb, ints_to_be(a, width), ints_to_be(b, width),
+                                     width, len(a), out), "dds_modmul_pairs")
+        raw = bytes(out)
+        return [int.from_bytes(raw[i * mb:(i + 1) * mb], "big") for i in range(len(a))]
+
+    def bigint_sum(self, ops) -> int:
+        ops = [int(x) for x in ops]
+        width = max([1] + [nbytes(x) for x in ops])
+        out = (C.c_uint8 * (width + 16))()
+        olen = C.c_size_t()
+        _check(_lib.dds_bigint_sum(self._h, ints_to_be(ops, width), width, len(ops), out, len(out), C.byref(olen)),
+               "dds_bigint_sum")
+        return int.from_bytes(bytes(out[: olen.value]), "big")
+
+    # ---- decimal route entry points ----
+    def _dec(self, fn, values, modulus: str | None) -> str:
+        arr = (C.c_char_p * max(1, len(values)))(*[str(v).encode() for v in values])
+        cap = sum(len(str(v)) for v in values) * 2 + 64 + (len(modulus) * 2 if modulus else 0)
+        out = C.create_string_buffer(cap)
+        olen = C.c_size_t()
+        _check(fn(self._h, arr, len(values), modulus.encode() if modulus is not None else None, out, cap,
+                  C.byref(olen)), fn.__name__)
+        return out.value.decode()
+
+    def sum_all_dec(self, values, nsqr: str | None) -> str:
+        return self._dec(_lib.dds_sum_all_dec, values, nsqr)
+
+    def mult_all_dec(self, values, n: str | None) -> str:
+        return self._dec(_lib.dds_mult_all_dec, values, n)
+
+    # ---- OPE filter ----
+    def ope_filter(self, col, valid, bound: int, op: str) -> np.ndarray:
+        col = np.ascontiguousarray(col, dtype=np.int64)
+        v = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
+        out = np.empty(max(1, len(col)), dtype=np.uint32)
+        got = C.c_size_t()
+        _check(_lib.dds_ope_filter(self._h, col.ctypes.data, None if v is None else v.ctypes.data, len(col),
+                                   int(bound), OPE_OPS[op], out.ctypes.data, C.byref(got)), "dds_ope_filter")
+        return out[: got.value].copy()
+
+    def ope_filter_device(self, d_col: int, d_valid: int | None, n: int, bound: int, op: str, d_out: int) -> int:
+        got = C.c_size_t()
+        _check(_lib.dds_ope_filter_device(self._h, C.c_void_p(d_col), C.c_void_p(d_valid or 0), n, int(bound),
+                                          OPE_OPS[op], C.c_void_p(d_out), C.byref(got)), "dds_ope_filter_device")
+        return got.value
+
+    # ---- encryption ----
+    def paillier_encrypt_batch(self, n: int, g: int, ms, rs) -> list[int]:
+        ms = np.ascontiguousarray(ms, dtype=np.uint32)
+        rs = [int(r) for r in rs]
+        nsq = n * n
+        nb, rw = nbytes(nsq), max([1] + [nbytes(r) for r in rs])
+        out = (C.c_uint8 * (nb * max(1, len(rs))))()
+        _check(_lib.dds_paillier_encrypt_batch(self._h, int_to_be(n, nbytes(n)), nbytes(n), int_to_be(g, nbytes(g)),
+                                               nbytes(g), ms.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                               ints_to_be(rs, rw), rw, len(rs), out, nb), "dds_paillier_encrypt_batch")
+        raw = bytes(out)
+        return [int.from_bytes(raw[i * nb:(i + 1) * nb], "big") for i in range(len(rs))]
+
+    def column(self, modulus: int, capacity: int) -> "Column":
+        return Column(self, modulus, capacity)
+
+    def combine_partials(self, modulus: int, partials: np.ndarray, rows) -> int:
+        partials = np.ascontiguousarray(partials, dtype=np.uint32)
+        rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        mb = nbytes(modulus)
+        out = (C.c_uint8 * mb)()
+        olen = C.c_size_t()
+        _check(_lib.dds_combine_partials(self._h, int_to_be(modulus, mb), mb,
+                                         partials.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                         rows.ctypes.data_as(C.POINTER(C.c_uint64)), len(rows), out, mb,
+                                         C.byref(olen)), "dds_combine_partials")
+        return int.from_bytes(bytes(out[: olen.value]), "big")
+
+
+class Column:
+    """Device-resident ciphertext column (dds_col)."""
+
+    def __init__(self, eng: Engine, modulus: int, capacity: int):
+        self.eng, self.modulus, self.mb = eng, int(modulus), nbytes(modulus)
+        h = C.c_void_p()
+        _check(_lib.dds_col_create(eng._h, int_to_be(modulus, self.mb), self.mb, capacity, C.byref(h)),
+               "dds_col_create")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            _lib.dds_col_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return _lib.dds_col_count(self._h)
+
+    @property
+    def partial_words(self) -> int:
+        return _lib.dds_col_partial_words(self._h)
+
+    def append(self, ops):
+        ops = [int(x) for x in ops]
+        width = max([self.mb] + [nbytes(x) for x in ops])
+        _check(_lib.dds_col_append(self._h, ints_to_be(ops, width), width, len(ops)), "dds_col_append")
+
+    def read(self, first: int, count: int) -> list[int]:
+        out = (C.c_uint8 * (self.mb * max(1, count)))()
+        _check(_lib.dds_col_read(self._h, first, count, out), "dds_col_read")
+        raw = bytes(out)
+        return [int.from_bytes(raw[i * self.mb:(i + 1) * self.mb], "big") for i in range(count)]
+
+    def fold(self, first: int = 0, count: int | None = None) -> int:
+        count = len(self) - first if count is None else count
+        out = (C.c_uint8 * self.mb)()
+        olen = C.c_size_t()
+        _check(_lib.dds_col_fold(self._h, first, count, out, self.mb, C.byref(olen)), "dds_col_fold")
+        return int.from_bytes(bytes(out[: olen.value]), "big")
+
+    def fold_partial(self, first: int = 0, count: int | None = None):
+        count = len(self) - first if count is None else count
+        part = np.zeros(self.partial_words, dtype=np.uint32)
+        rows = C.c_uint64()
+        _check(_lib.dds_col_fold_partial(self._h, first, count, part.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                         C.byref(rows)), "dds_col_fold_partial")
+        return part, rows.value
+
+    def fill_paillier_synth(self, n: int, g: int, seed: int, row0: int, count: int, pool: int = 1024):
+        _check(_lib.dds_col_fill_paillier_synth(self._h, int_to_be(n, nbytes(n)), nbytes(n), int_to_be(g, nbytes(g)),
+                                                nbytes(g), seed, row0, count, pool), "dds_col_fill_paillier_synth")
+
+
+# ---- synthetic-row plaintexts (mirror of k_synth_rows' index derivation) ----
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _splitmix64_np(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def synth_plaintexts(seed: int, row0: int, count: int, chunk: int = 1 << 22) -> np.ndarray:
+    """m_i of dds_col_fill_paillier_synth rows [row0, row0+count) (uint32)."""
+    out = np.empty(count, dtype=np.uint32)
+    for s in range(0, count, chunk):
+        idx = np.arange(row0 + s, row0 + min(count, s + chunk), dtype=np.uint64)
+        h = _splitmix64_np(np.uint64(seed) ^ _splitmix64_np(idx))
+        out[s:s + len(idx)] = (h % np.uint64(10000)).astype(np.uint32)
+    return out

@@ -1,0 +1,158 @@
+/*
+ * ddshe.h — C-ABI of the MI355X homomorphic-aggregation engine.
+ *
+ * Drop-in boundary for the server-side aggregation path of
+ * fmiguelgodinho/dependable-data-storage-csd2017. Every entry point names the
+ * reference interface it replaces (paths relative to /root/reference/):
+ *
+ *   hlib  HomoAdd.sum(c1, c2, nsquare)        src/main/scala/dds/http/DDSRestServer.scala:385, :423
+ *   hlib  HomoMult.multiply(c1, c2, pubkey)   src/main/scala/dds/http/DDSRestServer.scala:479, :518
+ *   hlib  HomoAdd.encrypt(m, PaillierKey)     src/main/scala/utils/SJHomoLibProvider.scala:58
+ *   route SumAll fold loop                    src/main/scala/dds/http/DDSRestServer.scala:397-446
+ *   route MultAll fold loop                   src/main/scala/dds/http/DDSRestServer.scala:491-539
+ *   route Search{Gt,GtEq,Lt,LtEq} loops       src/main/scala/dds/http/DDSRestServer.scala:682-830
+ *
+ * Conventions
+ *  - Big integers cross the boundary as fixed-width BIG-ENDIAN unsigned
+ *    magnitudes (what a JNA shim gets from BigInteger.toByteArray() after
+ *    stripping the sign byte and left-padding), `width` bytes per value.
+ *  - Every function returns a dds_status; no C++ exception crosses the ABI.
+ *    DDS_E_EMPTY maps to the reference's HTTP 404 path, every other non-zero
+ *    status to its HTTP 500 path (DDSRestServer.scala:432-442).
+ *  - Thread-safe: any number of threads may call into one dds_ctx; each call
+ *    runs on its own HIP stream taken from the context's pool.
+ *  - The caller owns every host buffer. Device columns (dds_col) are owned by
+ *    the library and freed only by dds_col_destroy / dds_ctx_destroy.
+ *  - There is NO CPU fallback: every arithmetic entry point runs HIP kernels on
+ *    the context's GPU and fails with DDS_E_HIP if it cannot.
+ */
+#ifndef DDSHE_H
+#define DDSHE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum dds_status {
+  DDS_OK = 0,
+  DDS_E_EMPTY = 1,       /* no operand qualified: reference answers 404      */
+  DDS_E_RANGE = 2,       /* operand does not fit the modulus' limb width      */
+  DDS_E_HIP = 3,         /* HIP runtime / kernel failure                      */
+  DDS_E_ARG = 4,         /* bad argument (NULL, zero width, even modulus, ...)*/
+  DDS_E_NOMEM = 5,       /* device or host allocation failed                  */
+  DDS_E_UNSUPPORTED = 6, /* modulus larger than the largest kernel instance   */
+  DDS_E_BUFSIZE = 7,     /* output buffer too small (required size returned)  */
+  DDS_E_FORMAT = 8       /* NumberFormatException on a decimal operand        */
+} dds_status;
+
+typedef struct dds_ctx dds_ctx;
+typedef struct dds_col dds_col;
+
+/* OPE predicates of SearchGt / SearchGtEq / SearchLt / SearchLtEq:
+ * keep row iff col <op> bound (DDSRestServer.scala:704, :742, :779, :816). */
+typedef enum dds_ope_op { DDS_OPE_GT = 0, DDS_OPE_GE = 1, DDS_OPE_LT = 2, DDS_OPE_LE = 3 } dds_ope_op;
+
+/* ---- context ------------------------------------------------------------- */
+int dds_ctx_create(int device, dds_ctx** out);
+int dds_ctx_destroy(dds_ctx* ctx);
+const char* dds_strerror(int status);
+/* last error detail of the calling thread ("" if none) */
+const char* dds_last_error(void);
+/* largest supported modulus, in bits */
+size_t dds_max_modulus_bits(void);
+/* Run this context's work on `stream` (a hipStream_t) instead of its pool; NULL restores the pool. */
+int dds_ctx_set_stream(dds_ctx* ctx, void* stream);
+/* Kernel timing with HIP events on the launch stream (for bench.py's roofline). */
+int dds_ctx_set_timing(dds_ctx* ctx, int enable);
+/* Accumulated device time (ms) and launch count of the dominant fold kernel
+ * (first fold level over the input rows) since the last reset. */
+int dds_ctx_get_timing(dds_ctx* ctx, double* fold_ms, uint64_t* fold_launches, double* total_ms);
+int dds_ctx_reset_timing(dds_ctx* ctx);
+/* Montgomery products issued by the timed fold launches (for algorithmic-work accounting). */
+int dds_ctx_get_fold_work(dds_ctx* ctx, uint64_t* modmuls);
+
+/* ---- batched modular products (replace the fold loops) ---------------------
+ * dds_modmul_fold: SumAll/MultAll semantics over `count` operands:
+ *   count == 0 -> DDS_E_EMPTY (404); count == 1 -> operand copied verbatim
+ *   (the reference keeps the first operand unreduced, DDSRestServer.scala:416-417);
+ *   count >= 2 -> prod(operands) mod modulus, canonical residue.
+ * out receives `*out_len` = byte length of the modulus, big-endian, left-padded
+ * (for count == 1: the operand's `width` bytes). out_cap is checked. */
+int dds_modmul_fold(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint8_t* operands_be,
+                    size_t width, size_t count, uint8_t* out, size_t out_cap, size_t* out_len);
+/* Paillier HomoAdd over a column: modulus = nsquare (DDSRestServer.scala:422-423). */
+int dds_paillier_sum(dds_ctx* ctx, const uint8_t* nsquare_be, size_t nsq_bytes, const uint8_t* ciphertexts_be,
+                     size_t width, size_t count, uint8_t* out, size_t out_cap, size_t* out_len);
+/* RSA HomoMult over a column: modulus = n of the X.509 pubkey (DDSRestServer.scala:515-518). */
+int dds_rsa_product(dds_ctx* ctx, const uint8_t* n_be, size_t n_bytes, const uint8_t* ciphertexts_be, size_t width,
+                    size_t count, uint8_t* out, size_t out_cap, size_t* out_len);
+/* Pairwise Sum / Mult routes (DDSRestServer.scala:385, :479), batched over n pairs:
+ * out[i] = a[i]*b[i] mod modulus, each mod_bytes wide. */
+int dds_modmul_pairs(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint8_t* a_be, const uint8_t* b_be,
+                     size_t width, size_t n, uint8_t* out);
+/* SumAll without nsqr (plain BigInteger add, DDSRestServer.scala:425): sum of count
+ * operands; result big-endian in out (min(out_cap) = width + 8 is always enough). */
+int dds_bigint_sum(dds_ctx* ctx, const uint8_t* operands_be, size_t width, size_t count, uint8_t* out,
+                   size_t out_cap, size_t* out_len);
+
+/* ---- device-resident columns (ciphertexts stay in HBM across requests) ----
+ * A column holds `count` residues of one modulus in the engine's resident
+ * format (limb-transposed radix-2^27). */
+int dds_col_create(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, size_t capacity, dds_col** out);
+int dds_col_destroy(dds_col* col);
+/* append `count` big-endian operands (validated against the modulus) */
+int dds_col_append(dds_col* col, const uint8_t* operands_be, size_t width, size_t count);
+size_t dds_col_count(const dds_col* col);
+/* download rows [first, first+count) as big-endian, mod_bytes each */
+int dds_col_read(dds_col* col, size_t first, size_t count, uint8_t* out);
+/* fold rows [first, first+count) (SumAll/MultAll semantics as dds_modmul_fold) */
+int dds_col_fold(dds_col* col, size_t first, size_t count, uint8_t* out, size_t out_cap, size_t* out_len);
+/* fold rows to one un-finalised partial for multi-GPU combination:
+ * partial_r27 receives limbs() words, *rows the row count it covers. */
+int dds_col_fold_partial(dds_col* col, size_t first, size_t count, uint32_t* partial_r27, uint64_t* rows);
+/* number of 32-bit words in a partial of this column's modulus */
+size_t dds_col_partial_words(const dds_col* col);
+/* combine partials from several GPUs (same modulus): result = prod of all rows mod N */
+int dds_combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint32_t* partials_r27,
+                         const uint64_t* rows, size_t nparts, uint8_t* out, size_t out_cap, size_t* out_len);
+/* Synthetic Paillier rows for benchmarks/tests (config 2 of BASELINE.json):
+ * c_i = g^m_i * r_a^n * r_b^n mod n^2 with m_i, a, b from splitmix64(seed, row0+i);
+ * m_i = splitmix64(seed ^ splitmix64(row0+i)) % 10000 (DDSDataGenerator.scala:274).
+ * Needs the Paillier key (n, g) big-endian; pool_size r^n values from seed. */
+int dds_col_fill_paillier_synth(dds_col* col, const uint8_t* n_be, size_t n_bytes, const uint8_t* g_be,
+                                size_t g_bytes, uint64_t seed, uint64_t row0, size_t count, uint32_t pool_size);
+
+/* ---- OPE range filter (SearchGt/GtEq/Lt/LtEq) ---------------------------
+ * Keeps row i iff valid[i] != 0 (reference guard contents.length-1 > position,
+ * DDSRestServer.scala:703) and col[i] <op> bound (signed 64-bit: OPE
+ * ciphertexts are Java Long, SJHomoLibProvider.scala:55). valid may be NULL.
+ * out_idx receives the matching row indices in ascending order. */
+int dds_ope_filter(dds_ctx* ctx, const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op,
+                   uint32_t* out_idx, size_t* out_n);
+/* same on device-resident arrays (pointers are device pointers) */
+int dds_ope_filter_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_valid, size_t n, int64_t bound, int op,
+                          uint32_t* d_out_idx, size_t* out_n);
+
+/* ---- batched Paillier encryption (HomoAdd.encrypt, SJHomoLibProvider.scala:58) ----
+ * c_i = g^m_i * r_i^n mod n^2 with caller-supplied r_i (big-endian, r_width bytes,
+ * values in [1, n^2)). out receives n of nsq_bytes each. */
+int dds_paillier_encrypt_batch(dds_ctx* ctx, const uint8_t* n_be, size_t n_bytes, const uint8_t* g_be, size_t g_bytes,
+                               const uint32_t* m, const uint8_t* r_be, size_t r_width, size_t count, uint8_t* out,
+                               size_t nsq_bytes);
+
+/* ---- route-level entry points on decimal strings (what the Scala route holds) ----
+ * values: count NUL-terminated decimal strings (contents(position) of the rows that
+ * passed the guard). modulus_dec NULL selects the plain add / multiply branch.
+ * out receives the decimal result (NUL-terminated) — DDSValueResult(acc.toString). */
+int dds_sum_all_dec(dds_ctx* ctx, const char* const* values, size_t count, const char* nsqr_dec, char* out,
+                    size_t out_cap, size_t* out_len);
+int dds_mult_all_dec(dds_ctx* ctx, const char* const* values, size_t count, const char* n_dec, char* out,
+                     size_t out_cap, size_t* out_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DDSHE_H */

@@ -1,0 +1,295 @@
+"""CPU restatement (Python ints) of the reference's homomorphic aggregation path.
+
+TEST INFRASTRUCTURE ONLY — the checker, never the product. Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+anything under ``oracle/``.
+
+Parity status: the arithmetic lives in hlib (``hlib.hj.mlib``, a proprietary jar
+that is ABSENT from the reference: ``/root/reference/lib/README.txt:1``; version
+unknown/unpinned) and the reference has no tests, fixtures or golden vectors
+(SURVEY.md §4, §8c). There is no JVM in this image, so the reference cannot be
+run. This oracle is pinned instead by
+  (1) the committed key material (``client.conf:85-86``), which satisfies the
+      standard Paillier / RSA identities checked in ``tests/test_oracle.py``;
+  (2) the published algorithms hlib implements (Paillier 1999, textbook RSA), with
+      ``HomoAdd.sum(c1,c2,nsq) = c1·c2 mod nsq`` and
+      ``HomoMult.multiply(c1,c2,pk) = c1·c2 mod n`` as the assumed definitions;
+  (3) the route semantics of ``DDSRestServer.scala`` restated line by line below;
+  (4) an independent cross-check against OpenSSL ``BN_mod_mul`` (tests).
+It is therefore "partially pinned": no reference-produced output exists.
+"""
+from __future__ import annotations
+
+import math
+import random
+
+# ---------------------------------------------------------------------------
+# hlib primitives (absent jar; call sites cited)
+# ---------------------------------------------------------------------------
+
+
+def homo_add_sum(c1: int, c2: int, nsquare: int) -> int:
+    """``HomoAdd.sum(c1, c2, nsquare)`` — Paillier homomorphic addition.
+    Call sites: ``DDSRestServer.scala:385`` (Sum) and ``:423`` (SumAll)."""
+    return (c1 * c2) % nsquare
+
+
+def homo_mult_multiply(c1: int, c2: int, n: int) -> int:
+    """``HomoMult.multiply(c1, c2, RSAPublicKey)`` — RSA multiplicative homomorphism.
+    Call sites: ``DDSRestServer.scala:479`` (Mult) and ``:518`` (MultAll)."""
+    return (c1 * c2) % n
+
+
+def paillier_encrypt(m: int, r: int, key: dict) -> int:
+    """``HomoAdd.encrypt(BigInteger m, PaillierKey)`` (``SJHomoLibProvider.scala:58``):
+    c = g^m · r^n mod n² with caller-supplied r (hlib draws r at random)."""
+    n, nsq = key["n"], key["nsquare"]
+    return (pow(key["g"], m, nsq) * pow(r, n, nsq)) % nsq
+
+
+def paillier_decrypt(c: int, key: dict) -> int:
+    """``HomoAdd.decrypt`` (``SJHomoLibProvider.scala:68``): m = L(c^λ mod n²)·μ mod n."""
+    n, nsq = key["n"], key["nsquare"]
+    u = pow(c, key["lambda"], nsq)
+    return ((u - 1) // n) * key["mu"] % n
+
+
+def rsa_encrypt(m: int, key: dict) -> int:
+    """``HomoMult.encrypt(pk, m)`` (``SJHomoLibProvider.scala:59``): textbook RSA."""
+    return pow(m, key["e"], key["n"])
+
+
+def rsa_decrypt(c: int, key: dict) -> int:
+    """``HomoMult.decrypt(sk, c)`` (``SJHomoLibProvider.scala:69``)."""
+    return pow(c, key["d"], key["n"])
+
+
+# ---------------------------------------------------------------------------
+# Route semantics (DDSRestServer.scala)
+# ---------------------------------------------------------------------------
+
+
+class NotFound(Exception):
+    """HTTP 404 from a route (``complete(StatusCodes.NotFound)``)."""
+
+
+class ServerError(Exception):
+    """HTTP 500 from a route (``case Failure(ex) => InternalServerError``)."""
+
+
+def java_biginteger(s) -> int:
+    """``new BigInteger(String)``: optional sign, decimal digits only."""
+    s = str(s)
+    body = s[1:] if s[:1] in "+-" else s
+    if not body or not body.isdigit() or not body.isascii():
+        raise ServerError(f"NumberFormatException: {s!r}")
+    return int(s)
+
+
+def dedup_rows(rows):
+    """``storedKeys.map(fetchSet)`` + ``Future.sequence`` over a Set collapses equal
+    DDSSets (``DDSRestServer.scala:401-403``) and ``filter(nonEmpty)`` drops
+    missing ones (``:408``). Rows are lists of column values; None = missing."""
+    seen, out = set(), []
+    for r in rows:
+        if r is None:
+            continue
+        key = tuple(str(v) for v in r)
+        if key in seen:
+            continue
+        seen.add(key)
+        out.append(r)
+    return out
+
+
+def sum_all(rows, position: int, nsqr=None) -> str:
+    """``GET /SumAll?position&nsqr`` — ``DDSRestServer.scala:397-446``.
+    Strict guard ``contents.length-1 > position`` (``:415``); first operand is
+    taken unreduced (``:416-417``); each later one is folded with HomoAdd.sum
+    (``:422-423``) or plain ``add`` when nsqr is absent (``:425``)."""
+    rows = dedup_rows(rows)
+    if not rows:
+        raise NotFound()
+    acc = None
+    nsq = java_biginteger(nsqr) if nsqr is not None else None
+    for r in rows:
+        if len(r) - 1 > position:
+            x = java_biginteger(r[position])
+            if acc is None:
+                acc = x
+            elif nsq is not None:
+                acc = homo_add_sum(acc, x, nsq)
+            else:
+                acc = acc + x
+    if acc is None:
+        raise NotFound()
+    return str(acc)
+
+
+def mult_all(rows, position: int, n=None) -> str:
+    """``GET /MultAll?position&pubkey`` — ``DDSRestServer.scala:491-539``.
+    ``n`` is the modulus of the X.509 pubkey (``:515-517``); None = plain product (``:520``)."""
+    rows = dedup_rows(rows)
+    if not rows:
+        raise NotFound()
+    acc = None
+    for r in rows:
+        if len(r) - 1 > position:
+            x = java_biginteger(r[position])
+            if acc is None:
+                acc = x
+            elif n is not None:
+                acc = homo_mult_multiply(acc, x, n)
+            else:
+                acc = acc * x
+    if acc is None:
+        raise NotFound()
+    return str(acc)
+
+
+def pair_sum(set1, set2, position: int, nsqr=None) -> str:
+    """``GET /Sum?key1&key2&position&nsqr`` — ``DDSRestServer.scala:355-395``
+    (guard ``length-1 < position`` → 404 at ``:376``)."""
+    if set1 is None or set2 is None:
+        raise NotFound()
+    if len(set1) - 1 < position or len(set2) - 1 < position:
+        raise NotFound()
+    a, b = java_biginteger(set1[position]), java_biginteger(set2[position])
+    if nsqr is not None:
+        return str(homo_add_sum(a, b, java_biginteger(nsqr)))
+    return str(a + b)
+
+
+def pair_mult(set1, set2, position: int, n=None) -> str:
+    """``GET /Mult?key1&key2&position&pubkey`` — ``DDSRestServer.scala:447-490``."""
+    if set1 is None or set2 is None:
+        raise NotFound()
+    if len(set1) - 1 < position or len(set2) - 1 < position:
+        raise NotFound()
+    a, b = java_biginteger(set1[position]), java_biginteger(set2[position])
+    if n is not None:
+        return str(homo_mult_multiply(a, b, n))
+    return str(a * b)
+
+
+OPS = {
+    # route -> predicate on (col, item); DDSRestServer.scala compares
+    # item.compareTo(col) {<0, <=0, >0, >=0}
+    "SearchGt": lambda col, item: item < col,     # :704
+    "SearchGtEq": lambda col, item: item <= col,  # :742
+    "SearchLt": lambda col, item: item > col,     # :779
+    "SearchLtEq": lambda col, item: item >= col,  # :816
+}
+
+
+def search(route: str, keyed_rows, position: int, value) -> set:
+    """``POST /Search{Gt,GtEq,Lt,LtEq}?position`` — ``DDSRestServer.scala:682-830``.
+    ``keyed_rows`` = list of (key, row). Returns the matching key SET (the
+    reference prepends into a list, so order is unspecified: ``:705``)."""
+    pred = OPS[route]
+    item = java_biginteger(value)
+    out = set()
+    seen = set()
+    for key, row in keyed_rows:
+        if row is None or key in seen:
+            continue
+        seen.add(key)
+        if len(row) - 1 > position and pred(java_biginteger(row[position]), item):
+            out.add(key)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Fold primitives used by the tests at sizes beyond route-level vectors
+# ---------------------------------------------------------------------------
+
+
+def modmul_fold(xs, N: int) -> int:
+    """SumAll/MultAll fold over k≥1 operands: x0 unreduced when k == 1, else ∏ mod N."""
+    if not xs:
+        raise NotFound()
+    if len(xs) == 1:
+        return xs[0]
+    acc = xs[0]
+    for x in xs[1:]:
+        acc = (acc * x) % N
+    return acc
+
+
+def ope_filter(col, valid, bound: int, op: str):
+    """Indices i with valid[i] and col[i] <op> bound (ascending)."""
+    f = {"gt": lambda c: c > bound, "ge": lambda c: c >= bound,
+         "lt": lambda c: c < bound, "le": lambda c: c <= bound}[op]
+    return [i for i, (c, v) in enumerate(zip(col, valid)) if v and f(int(c))]
+
+
+# ---------------------------------------------------------------------------
+# Synthetic keys (deterministic, seeded)
+# ---------------------------------------------------------------------------
+
+_SMALL_PRIMES = [p for p in range(3, 2000, 2) if all(p % q for q in range(3, int(p ** 0.5) + 1, 2))]
+
+
+def is_probable_prime(n: int, rng: random.Random, rounds: int = 40) -> bool:
+    if n < 2:
+        return False
+    for p in _SMALL_PRIMES:
+        if n % p == 0:
+            return n == p
+    d, s = n - 1, 0
+    while d % 2 == 0:
+        d //= 2
+        s += 1
+    for _ in range(rounds):
+        a = rng.randrange(2, n - 1)
+        x = pow(a, d, n)
+        if x in (1, n - 1):
+            continue
+        for _ in range(s - 1):
+            x = x * x % n
+            if x == n - 1:
+                break
+        else:
+            return False
+    return True
+
+
+def gen_prime(bits: int, rng: random.Random) -> int:
+    while True:
+        c = rng.getrandbits(bits) | (1 << (bits - 1)) | (1 << (bits - 2)) | 1
+        if is_probable_prime(c, rng):
+            return c
+
+
+def gen_paillier_key(bits: int, seed: int) -> dict:
+    """Paillier key with an n of exactly ``bits`` bits and a random g ∈ Z*_{n²}
+    (like the committed key, whose g is random: SURVEY.md F6)."""
+    rng = random.Random(seed)
+    while True:
+        p = gen_prime(bits // 2, rng)
+        q = gen_prime(bits // 2, rng)
+        n = p * q
+        if p != q and n.bit_length() == bits and math.gcd(n, (p - 1) * (q - 1)) == 1:
+            break
+    nsq = n * n
+    lam = (p - 1) * (q - 1) // math.gcd(p - 1, q - 1)
+    while True:
+        g = rng.randrange(2, nsq)
+        if math.gcd(g, n) != 1:
+            continue
+        L = (pow(g, lam, nsq) - 1) // n
+        if math.gcd(L, n) == 1:
+            mu = pow(L, -1, n)
+            break
+    return {"g": g, "lambda": lam, "mu": mu, "n": n, "nsquare": nsq, "p": p, "q": q}
+
+
+def gen_rsa_key(bits: int, seed: int, e: int = 65537) -> dict:
+    rng = random.Random(seed)
+    while True:
+        p = gen_prime(bits // 2, rng)
+        q = gen_prime(bits // 2, rng)
+        n = p * q
+        phi = (p - 1) * (q - 1)
+        if p != q and n.bit_length() == bits and math.gcd(e, phi) == 1:
+            return {"n": n, "e": e, "d": pow(e, -1, phi), "p": p, "q": q}

@@ -1,0 +1,243 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the oracle and the golden
+fixtures, bit-exact. Route references: DDSRestServer.scala:355-539 (Sum/SumAll/Mult/MultAll),
+:682-830 (Search*), SJHomoLibProvider.scala:58 (encrypt)."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import homo
+
+pytestmark = pytest.mark.gpu
+
+
+def H(x):
+    return int(x, 16)
+
+
+# ---------------------------------------------------------------------------
+# golden fixtures
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["paillier2048_committed", "paillier1024_seed1", "paillier3072_seed4"])
+def test_paillier_fold_golden(eng, keys, vectors, name):
+    k, v = keys[name], vectors[name]
+    cs = [H(r["c"]) for r in v["rows"]]
+    assert eng.paillier_sum(k["nsquare"], cs) == H(v["fold"])
+    assert homo.paillier_decrypt(H(v["fold"]), k) == v["dec_sum"]
+
+
+@pytest.mark.parametrize("name", ["rsa1024_committed", "rsa2048_seed3"])
+def test_rsa_fold_golden(eng, keys, vectors, name):
+    k, v = keys[name], vectors[name]
+    assert eng.rsa_product(k["n"], [H(r["c"]) for r in v["rows"]]) == H(v["fold"])
+
+
+@pytest.mark.parametrize("name,key,field", [("edges_nsq2048", "paillier2048_committed", "nsquare"),
+                                            ("edges_n1024", "rsa1024_committed", "n"),
+                                            ("edges_nsq3072", "paillier3072_seed4", "nsquare")])
+def test_fold_edge_cases_golden(eng, keys, vectors, name, key, field):
+    import ddshe
+    N = keys[key][field]
+    for case in vectors[name]:
+        ops = [H(x) for x in case["ops"]]
+        if case["result"] is None:
+            with pytest.raises(ddshe.NotFound):
+                eng.modmul_fold(N, ops)
+        else:
+            assert eng.modmul_fold(N, ops) == H(case["result"]), case["name"]
+
+
+@pytest.mark.parametrize("name", ["paillier2048_committed", "paillier1024_seed1"])
+def test_pairs_golden(eng, keys, vectors, name):
+    k, v = keys[name], vectors[name]
+    a = [H(p["a"]) for p in v["pairs"]]
+    b = [H(p["b"]) for p in v["pairs"]]
+    assert eng.modmul_pairs(k["nsquare"], a, b) == [H(p["c"]) for p in v["pairs"]]
+
+
+def test_routes_golden(eng, vectors):
+    """Route-level SumAll / MultAll / Search* through the decimal C-ABI entry points."""
+    from ddshe import routes
+    rv = vectors["routes"]
+    rows = rv["rows"]
+    keyed = [(f"k{i}", r) for i, r in enumerate(rows)]
+    for c in rv["cases"]:
+        if c["route"] == "SumAll":
+            if c["result"] is None:
+                with pytest.raises(routes.NotFound):
+                    routes.sum_all(eng, rows, c["position"], c["nsqr"])
+            else:
+                assert routes.sum_all(eng, rows, c["position"], c["nsqr"]) == c["result"]
+        elif c["route"] == "MultAll":
+            if c["n"] is None:
+                continue  # unbounded product: DDS_E_UNSUPPORTED this round
+            assert routes.mult_all(eng, rows, c["position"], c["n"]) == c["result"]
+        else:
+            assert sorted(routes.search(eng, c["route"], keyed, c["position"], c["value"])) == c["result"]
+
+
+# ---------------------------------------------------------------------------
+# randomized parity at sizes the oracle finishes in seconds
+# ---------------------------------------------------------------------------
+SIZES = [2, 3, 7, 64, 65, 127, 1000, 4099]
+
+
+@pytest.mark.parametrize("bits", [512, 1024, 2048, 2050, 3072, 4095, 4096, 6144])
+def test_fold_random_moduli(eng, bits):
+    rng = random.Random(bits)
+    N = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+    for k in (2, 5, 333):
+        xs = [rng.randrange(N) for _ in range(k)]
+        assert eng.modmul_fold(N, xs) == homo.modmul_fold(xs, N), (bits, k)
+
+
+@pytest.mark.parametrize("k", SIZES)
+def test_fold_sizes_committed_nsq(eng, keys, k):
+    N = keys["paillier2048_committed"]["nsquare"]
+    rng = random.Random(k)
+    xs = [rng.randrange(N) for _ in range(k)]
+    assert eng.paillier_sum(N, xs) == homo.modmul_fold(xs, N)
+
+
+def test_fold_small_modulus_and_wide_operands(eng):
+    N = 0xFFFFFFFFFFFFFFC5  # 64-bit prime
+    rng = random.Random(3)
+    xs = [rng.randrange(N) for _ in range(100)]
+    assert eng.modmul_fold(N, xs) == homo.modmul_fold(xs, N)
+    # operands >= 2N but within the limb width are reduced on the GPU (k_reduce_rows)
+    xs2 = [N * 3 + 5, N * 7 + 11, 2**70 + 3]
+    assert eng.modmul_fold(N, xs2) == homo.modmul_fold(xs2, N)
+
+
+def test_fold_operand_too_wide_is_range_error(eng):
+    import ddshe
+    N = (1 << 61) - 1
+    with pytest.raises(ddshe.DDSError) as ei:
+        eng.modmul_fold(N, [1 << 200, 3])
+    assert ei.value.status == ddshe.DDS_E_RANGE
+
+
+def test_even_modulus_rejected(eng):
+    import ddshe
+    with pytest.raises(ddshe.DDSError) as ei:
+        eng.modmul_fold(1 << 100, [3, 5])
+    assert ei.value.status == ddshe.DDS_E_ARG
+
+
+def test_pairs_random(eng, keys):
+    N = keys["rsa2048_seed3"]["n"]
+    rng = random.Random(11)
+    a = [rng.randrange(N) for _ in range(300)]
+    b = [rng.randrange(N) for _ in range(300)]
+    assert eng.modmul_pairs(N, a, b) == [x * y % N for x, y in zip(a, b)]
+
+
+def test_bigint_sum(eng):
+    rng = random.Random(12)
+    xs = [rng.getrandbits(4096) for _ in range(5000)]
+    assert eng.bigint_sum(xs) == sum(xs)
+    assert eng.bigint_sum([5]) == 5
+
+
+def test_decimal_routes_signs_and_formats(eng, keys):
+    N = keys["paillier1024_seed1"]["nsquare"]
+    vals = ["-12345", "+777", "0000042", str(N + 99)]
+    got = eng.sum_all_dec(vals, str(N))
+    acc = int(vals[0])
+    for v in vals[1:]:
+        acc = acc * int(v) % N
+    assert got == str(acc)
+    assert eng.sum_all_dec(["0007"], str(N)) == "7"      # single operand: BigInteger(str).toString
+    assert eng.sum_all_dec(["-5", "3", "10"], None) == "8"
+    with pytest.raises(Exception):
+        eng.sum_all_dec(["12a"], str(N))
+
+
+# ---------------------------------------------------------------------------
+# encryption
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name,count", [("paillier1024_seed1", 40), ("paillier2048_committed", 24),
+                                        ("paillier3072_seed4", 6)])
+def test_encrypt_batch(eng, keys, vectors, name, count):
+    k = keys[name]
+    rows = vectors[name]["rows"][:count]
+    ms = [r["m"] for r in rows]
+    rs = [H(r["r"]) for r in rows]
+    got = eng.paillier_encrypt_batch(k["n"], k["g"], ms, rs)
+    assert got == [H(r["c"]) for r in rows]
+
+
+def test_encrypt_then_sum_decrypts(eng, keys):
+    k = keys["paillier1024_seed1"]
+    rng = random.Random(21)
+    ms = [rng.randrange(10000) for _ in range(256)] + [0, 2**31 - 1]
+    rs = [rng.randrange(1, k["n"]) for _ in ms]
+    cs = eng.paillier_encrypt_batch(k["n"], k["g"], ms, rs)
+    assert homo.paillier_decrypt(eng.paillier_sum(k["nsquare"], cs), k) == sum(ms) % k["n"]
+
+
+# ---------------------------------------------------------------------------
+# device columns, synthetic rows, partial combination (multi-GPU algebra)
+# ---------------------------------------------------------------------------
+def test_column_append_fold_read(eng, keys):
+    N = keys["paillier2048_committed"]["nsquare"]
+    rng = random.Random(31)
+    xs = [rng.randrange(N) for _ in range(777)]
+    col = eng.column(N, 1000)
+    col.append(xs[:500])
+    col.append(xs[500:])
+    assert len(col) == 777
+    assert col.read(10, 5) == xs[10:15]
+    assert col.fold() == homo.modmul_fold(xs, N)
+    assert col.fold(100, 1) == xs[100]
+    assert col.fold(3, 200) == homo.modmul_fold(xs[3:203], N)
+    parts, rows = [], []
+    for a, b in ((0, 100), (100, 377), (377, 777)):
+        p, r = col.fold_partial(a, b - a)
+        parts.append(p)
+        rows.append(r)
+    assert eng.combine_partials(N, np.stack(parts), rows) == homo.modmul_fold(xs, N)
+
+
+@pytest.mark.parametrize("name", ["paillier2048_committed", "paillier1024_seed1"])
+def test_synthetic_rows_decrypt(eng, keys, name):
+    import ddshe
+    k = keys[name]
+    count = 20000
+    col = eng.column(k["nsquare"], count)
+    col.fill_paillier_synth(k["n"], k["g"], seed=2, row0=0, count=count, pool=64)
+    ms = ddshe.synth_plaintexts(2, 0, count)
+    sample = col.read(0, 300)
+    for i in (0, 1, 299):
+        assert homo.paillier_decrypt(sample[i], k) == ms[i]
+    assert col.fold(0, 300) == homo.modmul_fold(sample, k["nsquare"])
+    assert homo.paillier_decrypt(col.fold(), k) == int(ms.astype(np.int64).sum()) % k["n"]
+
+
+def test_large_fold_property(eng, keys):
+    """Full-size-style property check: Dec(fold of 1M synthetic rows) == sum(m_i)."""
+    import ddshe
+    k = keys["paillier2048_committed"]
+    count = 1_000_003
+    col = eng.column(k["nsquare"], count)
+    col.fill_paillier_synth(k["n"], k["g"], seed=5, row0=0, count=count, pool=256)
+    ms = ddshe.synth_plaintexts(5, 0, count)
+    assert homo.paillier_decrypt(col.fold(), k) == int(ms.astype(np.int64).sum()) % k["n"]
+
+
+# ---------------------------------------------------------------------------
+# OPE range filter
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [1, 63, 4096, 4097, 100_000, 3_000_001])
+def test_ope_filter_vs_numpy(eng, n):
+    rng = np.random.default_rng(n)
+    col = rng.integers(-2**63, 2**63 - 1, size=n, dtype=np.int64)
+    col[: min(n, 10)] = np.array([-2**63, 2**63 - 1, 0, -1, 1, 5, 5, 5, 7, -7], dtype=np.int64)[: min(n, 10)]
+    valid = (rng.random(n) > 0.1).astype(np.uint8)
+    for bound in (int(col[n // 2]), -2**63, 2**63 - 1, 5):
+        for op, f in (("gt", np.greater), ("ge", np.greater_equal), ("lt", np.less), ("le", np.less_equal)):
+            exp = np.nonzero(f(col, bound) & (valid != 0))[0].astype(np.uint32)
+            got = eng.ope_filter(col, valid, bound, op)
+            assert np.array_equal(got, exp), (n, bound, op)
+    got = eng.ope_filter(col, None, 0, "ge")
+    assert np.array_equal(got, np.nonzero(col >= 0)[0].astype(np.uint32))

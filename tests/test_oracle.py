@@ -1,0 +1,198 @@
+"""CPU tests of the oracle (tests/ infrastructure) against the reference's committed key
+material and the golden vectors — no GPU. The oracle is pinned here; see oracle/homo.py."""
+import ctypes
+import ctypes.util
+import math
+import os
+import random
+
+import pytest
+
+from oracle import homo
+
+REF_CONF = "/root/reference/src/main/resources/client.conf"
+
+
+def test_keys_json_matches_reference_conf(keys):
+    if not os.path.exists(REF_CONF):
+        pytest.skip("reference tree not present (GPU box)")
+    from oracle.javaser import decode_client_conf
+    ref = decode_client_conf(open(REF_CONF).read())
+    for k, v in ref["paillier"].items():
+        assert keys["paillier2048_committed"][k] == v
+    assert keys["rsa1024_committed"]["n"] == ref["rsa"]["n"]
+    assert keys["ope_key"] == ref["ope_key"]
+
+
+@pytest.mark.parametrize("name", ["paillier2048_committed", "paillier1024_seed1", "paillier3072_seed4"])
+def test_paillier_key_identities(keys, name):
+    k = keys[name]
+    n, nsq = k["n"], k["nsquare"]
+    assert k["p"] * k["q"] == n and n * n == nsq
+    lam = (k["p"] - 1) * (k["q"] - 1) // math.gcd(k["p"] - 1, k["q"] - 1)
+    assert lam == k["lambda"]
+    L = (pow(k["g"], lam, nsq) - 1) // n
+    assert L * k["mu"] % n == 1
+
+
+def test_committed_key_sizes(keys):
+    assert keys["paillier2048_committed"]["n"].bit_length() == 2048
+    assert keys["paillier2048_committed"]["nsquare"].bit_length() == 4095   # 128 x 32-bit limbs
+    assert keys["rsa1024_committed"]["n"].bit_length() == 1024
+    assert keys["rsa1024_committed"]["e"] == 65537
+
+
+@pytest.mark.parametrize("name", ["rsa1024_committed", "rsa2048_seed3"])
+def test_rsa_roundtrip(keys, name):
+    k = keys[name]
+    for m in (1, 2, 9999, 123456789):
+        assert homo.rsa_decrypt(homo.rsa_encrypt(m, k), k) == m
+
+
+def test_paillier_vectors_recompute(keys, vectors):
+    for name in ("paillier2048_committed", "paillier1024_seed1", "paillier3072_seed4"):
+        k, v = keys[name], vectors[name]
+        rows = v["rows"]
+        for row in rows[:4]:
+            assert homo.paillier_encrypt(row["m"], int(row["r"], 16), k) == int(row["c"], 16)
+        cs = [int(r["c"], 16) for r in rows]
+        assert homo.modmul_fold(cs, k["nsquare"]) == int(v["fold"], 16)
+        assert homo.paillier_decrypt(int(v["fold"], 16), k) == sum(r["m"] for r in rows) % k["n"] == v["dec_sum"]
+
+
+def test_edge_vectors_recompute(keys, vectors):
+    for name in ("edges_nsq2048", "edges_n1024", "edges_nsq3072"):
+        N = {"edges_nsq2048": keys["paillier2048_committed"]["nsquare"],
+             "edges_n1024": keys["rsa1024_committed"]["n"],
+             "edges_nsq3072": keys["paillier3072_seed4"]["nsquare"]}[name]
+        for case in vectors[name]:
+            ops = [int(x, 16) for x in case["ops"]]
+            if case["result"] is None:
+                with pytest.raises(homo.NotFound):
+                    homo.modmul_fold(ops, N)
+            else:
+                assert homo.modmul_fold(ops, N) == int(case["result"], 16), case["name"]
+
+
+def test_route_vectors_recompute(vectors):
+    rv = vectors["routes"]
+    rows = rv["rows"]
+    keyed = [(f"k{i}", r) for i, r in enumerate(rows)]
+    for c in rv["cases"]:
+        if c["route"] == "SumAll":
+            if c["result"] is None:
+                with pytest.raises(homo.NotFound):
+                    homo.sum_all(rows, c["position"], c["nsqr"])
+            else:
+                assert homo.sum_all(rows, c["position"], c["nsqr"]) == c["result"]
+        elif c["route"] == "MultAll":
+            n = int(c["n"]) if c["n"] else None
+            assert homo.mult_all(rows, c["position"], n) == c["result"]
+        else:
+            assert sorted(homo.search(c["route"], keyed, c["position"], c["value"])) == c["result"]
+
+
+def test_route_semantics_unit():
+    # strict guard (DDSRestServer.scala:415): a row whose last index == position is skipped
+    assert homo.sum_all([["1", "7"], ["2", "5", "x"]], 1, "1000") == "5"
+    # first operand unreduced when alone (:416-417)
+    assert homo.sum_all([["0", "12345", "z"]], 1, "100") == "12345"
+    # plain add without nsqr (:425)
+    assert homo.sum_all([["0", "3", "z"], ["0", "4", "z"]], 1, None) == "7"
+    # duplicates collapse (Set semantics of storedKeys.map, :401-403)
+    assert homo.sum_all([["0", "3", "z"], ["0", "3", "z"]], 1, None) == "3"
+    with pytest.raises(homo.NotFound):
+        homo.sum_all([], 1, None)
+    with pytest.raises(homo.ServerError):
+        homo.sum_all([["0", "abc", "z"]], 1, None)
+    assert homo.pair_sum(["1", "9"], ["1", "8"], 1, "10") == "2"
+    with pytest.raises(homo.NotFound):
+        homo.pair_sum(["1"], ["1", "8"], 1, "10")
+
+
+def _openssl():
+    path = ctypes.util.find_library("crypto")
+    if not path:
+        pytest.skip("libcrypto not available")
+    lib = ctypes.CDLL(path)
+    lib.BN_new.restype = ctypes.c_void_p
+    lib.BN_CTX_new.restype = ctypes.c_void_p
+    lib.BN_bin2bn.restype = ctypes.c_void_p
+    lib.BN_bin2bn.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p]
+    lib.BN_bn2bin.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    lib.BN_num_bits.argtypes = [ctypes.c_void_p]
+    lib.BN_mod_mul.argtypes = [ctypes.c_void_p] * 5
+    lib.BN_free.argtypes = [ctypes.c_void_p]
+    lib.BN_CTX_free.argtypes = [ctypes.c_void_p]
+    return lib
+
+
+def test_oracle_vs_openssl_bn_mod_mul(keys):
+    """Independent cross-check of the fold arithmetic with OpenSSL BN_mod_mul."""
+    lib = _openssl()
+    ctx = lib.BN_CTX_new()
+
+    def bn(x):
+        b = x.to_bytes(max(1, (x.bit_length() + 7) // 8), "big")
+        return lib.BN_bin2bn(b, len(b), None)
+
+    def toint(p):
+        nb = (lib.BN_num_bits(p) + 7) // 8
+        buf = ctypes.create_string_buffer(max(1, nb))
+        lib.BN_bn2bin(p, buf)
+        return int.from_bytes(buf.raw[:nb], "big") if nb else 0
+
+    rng = random.Random(5)
+    for N in (keys["paillier2048_committed"]["nsquare"], keys["rsa2048_seed3"]["n"],
+              keys["paillier3072_seed4"]["nsquare"]):
+        xs = [rng.randrange(N) for _ in range(50)]
+        acc, m = bn(xs[0]), bn(N)
+        for x in xs[1:]:
+            b = bn(x)
+            r = lib.BN_new()
+            assert lib.BN_mod_mul(r, acc, b, m, ctx) == 1
+            lib.BN_free(acc)
+            lib.BN_free(b)
+            acc = r
+        assert toint(acc) == homo.modmul_fold(xs, N)
+    lib.BN_CTX_free(ctx)
+
+
+def test_partial_algebra():
+    """Montgomery partial algebra used by the multi-GPU combine: v(S) = prod(S) * R^(1-|S|)."""
+    rng = random.Random(9)
+    N = rng.randrange(2**300, 2**301) | 1
+    R = 2 ** (27 * 12)
+    Rinv = pow(R, -1, N)
+
+    def monpro(a, b):
+        return a * b * Rinv % N
+
+    xs = [rng.randrange(N) for _ in range(37)]
+    parts = []
+    for i in range(0, 37, 10):
+        v = R % N
+        for x in xs[i:i + 10]:
+            v = monpro(v, x)
+        parts.append(v)
+    v = R % N
+    for p in parts:
+        v = monpro(v, p)
+    # v(all) = prod * R^(1-k) * R^(1-#parts)... combine folds partials as rows: R^(1 - k) overall
+    v_all = parts[0]
+    for p in parts[1:]:
+        v_all = monpro(v_all, p)
+    assert monpro(v_all, pow(R, len(xs), N)) == homo.modmul_fold(xs, N)
+
+
+def test_c_restatement_matches_python_oracle(keys):
+    from oracle import cref
+    rng = random.Random(77)
+    for N in (keys["paillier2048_committed"]["nsquare"], keys["rsa1024_committed"]["n"],
+              keys["paillier3072_seed4"]["nsquare"], (1 << 127) - 1):
+        for k in (2, 3, 50):
+            xs = [rng.randrange(N) for _ in range(k)]
+            assert cref.fold(N, xs) == homo.modmul_fold(xs, N)
+        xs = [N + 5, 3 * N + 1, rng.randrange(N)]        # unreduced inputs
+        assert cref.fold(N, xs) == homo.modmul_fold(xs, N)
+        assert cref.fold(N, [N + 5]) == N + 5              # k == 1 verbatim
