@@ -64,6 +64,7 @@ def main():
     torch.cuda.set_device(local)
 
     import ddshe
+    import ddshe.dist as ddist
 
     key = load_key()
     nsq = key["nsquare"]
@@ -73,9 +74,8 @@ def main():
 
     # shard rows by contiguous key range; weak scaling: each rank owns --rows rows
     total = args.rows if args.strong else args.rows * world
+    row0, mine = ddist.shard_range(total, world, rank)
     per = (total + world - 1) // world
-    row0 = rank * per
-    mine = max(0, min(per, total - row0))
     col = eng.column(nsq, max(1, mine))
     t_fill = time.time()
     if mine:
@@ -89,16 +89,9 @@ def main():
         if world == 1:
             return col.fold()
         part, rows = col.fold_partial()
-        t = torch.from_numpy(np.concatenate([part.view(np.uint32),
-                                             np.array([rows & 0xFFFFFFFF, rows >> 32], dtype=np.uint32)]))
-        t = t.view(torch.int32).cuda()
-        gathered = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(gathered, t)
+        parts, rows_all = ddist.gather_partials(part, rows, device=torch.device("cuda", local))
         if rank != 0:
             return None
-        g = torch.stack(gathered).cpu().numpy().view(np.uint32)
-        parts = g[:, :-2]
-        rows_all = g[:, -2].astype(np.uint64) | (g[:, -1].astype(np.uint64) << np.uint64(32))
         return eng.combine_partials(nsq, parts, rows_all)
 
     for _ in range(args.warmup):
