@@ -247,25 +247,25 @@ inline std::string to_dec(Limbs a, bool neg = false) {
   return s;
 }
 
-// radix-2^27 limbs (S of them, zero-padded); requires value < 2^(27*S)
-inline std::vector<uint32_t> to_r27(const Limbs& a, int S) {
+// radix-2^W limbs (S of them, zero-padded); requires value < 2^(W*S)
+inline std::vector<uint32_t> to_rw(const Limbs& a, int S, int W) {
   std::vector<uint32_t> r(S, 0);
   for (int l = 0; l < S; ++l) {
-    size_t bit = (size_t)27 * l;
+    size_t bit = (size_t)W * l;
     uint64_t w = 0;
     size_t wi = bit / 32, sh = bit % 32;
     if (wi < a.size()) w = a[wi];
     if (wi + 1 < a.size()) w |= (uint64_t)a[wi + 1] << 32;
-    r[l] = (uint32_t)(w >> sh) & ((1u << 27) - 1);
+    r[l] = (uint32_t)(w >> sh) & ((1u << W) - 1);
   }
   return r;
 }
 
-// radix-2^27 limbs (possibly unnormalised, each < 2^32) -> value
-inline Limbs from_r27(const uint32_t* r, int S) {
-  Limbs acc(((size_t)27 * S + 64) / 32 + 2, 0);
+// radix-2^W limbs (possibly unnormalised, each < 2^32) -> value
+inline Limbs from_rw(const uint32_t* r, int S, int W) {
+  Limbs acc(((size_t)W * S + 64) / 32 + 2, 0);
   for (int l = 0; l < S; ++l) {
-    size_t bit = (size_t)27 * l;
+    size_t bit = (size_t)W * l;
     uint64_t v = (uint64_t)r[l] << (bit % 32);
     size_t wi = bit / 32;
     uint64_t c = 0;
@@ -280,11 +280,11 @@ inline Limbs from_r27(const uint32_t* r, int S) {
   return acc;
 }
 
-// -N^{-1} mod 2^27 (N odd)
-inline uint32_t mont_n0(uint32_t n_low) {
+// -N^{-1} mod 2^W (N odd)
+inline uint32_t mont_n0(uint32_t n_low, int W) {
   uint32_t inv = n_low;  // Newton: inv = inv*(2 - n*inv), 5 iterations for 32 bits
   for (int i = 0; i < 5; ++i) inv *= 2u - n_low * inv;
-  return (0u - inv) & ((1u << 27) - 1);
+  return (0u - inv) & ((1u << W) - 1);
 }
 
 }  // namespace bn

@@ -73,24 +73,26 @@ struct Worker {
 };
 
 struct ModConsts {
-  int S = 0, TPI = 0;
+  int S = 0, TPI = 0, W = 0;
   size_t bits = 0, bytes = 0;
   uint32_t n0 = 0;
   bn::Limbs N, Rmod;
   std::vector<uint32_t> host;  // kConstCount * S
   uint32_t* d = nullptr;       // device copy
   std::mutex ymu;
-  std::map<uint64_t, std::vector<uint32_t>> ycache;  // k -> R^k mod N (r27)
+  std::map<uint64_t, std::vector<uint32_t>> ycache;  // k -> R^k mod N (rW)
   ~ModConsts() {
     if (d) (void)hipFree(d);
   }
+  std::vector<uint32_t> rw(const bn::Limbs& v) const { return bn::to_rw(v, S, W); }
+  bn::Limbs value(const uint32_t* limbs) const { return bn::from_rw(limbs, S, W); }
   const std::vector<uint32_t>& y_for(uint64_t k) {
     std::lock_guard<std::mutex> lk(ymu);
     auto it = ycache.find(k);
     if (it != ycache.end()) return it->second;
     if (ycache.size() > 64) ycache.clear();
     bn::Limbs y = bn::powmod_u64(Rmod, k, N);
-    return ycache.emplace(k, bn::to_r27(y, S)).first->second;
+    return ycache.emplace(k, rw(y)).first->second;
   }
 };
 
@@ -172,18 +174,20 @@ int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_p
   auto mc = std::make_shared<ModConsts>();
   mc->bits = bn::bit_length(N);
   mc->bytes = (mc->bits + 7) / 8;
-  mc->S = pick_S(mc->bits);
-  if (!mc->S) return fail(DDS_E_UNSUPPORTED, "modulus too large");
-  mc->TPI = tpi_for(mc->S);
+  const Shape sh = pick_shape(mc->bits);
+  if (!sh.S) return fail(DDS_E_UNSUPPORTED, "modulus too large");
+  mc->S = sh.S;
+  mc->TPI = sh.TPI;
+  mc->W = sh.W;
   const int S = mc->S;
   mc->N = N;
-  mc->n0 = bn::mont_n0(N[0]);
-  mc->Rmod = bn::mod(bn::pow2((size_t)27 * S), N);
+  mc->n0 = bn::mont_n0(N[0], mc->W);
+  mc->Rmod = bn::mod(bn::pow2((size_t)mc->W * S), N);
   bn::Limbs R2 = bn::mod(bn::mul(mc->Rmod, mc->Rmod), N);
   bn::Limbs N2 = bn::add(N, N);
   mc->host.assign((size_t)kConstCount * S, 0);
   auto put = [&](int slot, const bn::Limbs& v) {
-    auto r = bn::to_r27(v, S);
+    auto r = mc->rw(v);
     std::copy(r.begin(), r.end(), mc->host.begin() + (size_t)slot * S);
   };
   put(kConstN, N);
@@ -214,13 +218,22 @@ void record_time(dds_ctx* ctx, Worker* w, hipStream_t st, bool begin, int slot) 
   (void)hipEventRecord(w->ev[slot + (begin ? 0 : 1)], st);
 }
 
+int pick_tpi(int S) {
+  for (size_t b = 8; b < 1u << 16; b += 8) {
+    Shape sh = pick_shape(b);
+    if (sh.S == S) return sh.TPI;
+    if (!sh.S) break;
+  }
+  return 1;
+}
+
 size_t max_fold_groups(dds_ctx* ctx, int S) {
   int bpc = 0;
   if (fold_occupancy(S, &bpc) != hipSuccess || bpc < 1) bpc = 1;
-  return (size_t)ctx->cus * bpc * (256 / tpi_for(S));
+  return (size_t)ctx->cus * bpc * (256 / pick_tpi(S));
 }
 
-// Fold `count` rows of an r27 column into one un-finalised partial (in `*part`, stride pstride, row 0).
+// Fold `count` rows of an rW column into one un-finalised partial (in `*part`, stride pstride, row 0).
 int fold_partial_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
                         size_t count, const uint32_t** part, size_t* part_stride) {
   const int S = mc.S;
@@ -252,15 +265,15 @@ int fold_partial_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, 
 }
 
 int finalize_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* part, size_t pstride,
-                    uint64_t k, std::vector<uint32_t>* result_r27) {
+                    uint64_t k, std::vector<uint32_t>* result_rw) {
   const int S = mc.S;
   const std::vector<uint32_t>& y = mc.y_for(k);
   HIP_TRY(w->y.ensure((size_t)S * 4));
   HIP_TRY(w->out.ensure((size_t)S * 4));
   HIP_TRY(hipMemcpyAsync(w->y.p, y.data(), (size_t)S * 4, hipMemcpyHostToDevice, st));
   HIP_TRY(launch_finalize(S, part, pstride, mc.d, w->y.as<uint32_t>(), mc.n0, w->out.as<uint32_t>(), st));
-  result_r27->assign(S, 0);
-  HIP_TRY(hipMemcpyAsync(result_r27->data(), w->out.p, (size_t)S * 4, hipMemcpyDeviceToHost, st));
+  result_rw->assign(S, 0);
+  HIP_TRY(hipMemcpyAsync(result_rw->data(), w->out.p, (size_t)S * 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (ctx->timing.load()) {
     float ms = 0;
@@ -281,7 +294,7 @@ int emit_be(const bn::Limbs& v, size_t width, uint8_t* out, size_t out_cap, size
   return DDS_OK;
 }
 
-// Upload `count` big-endian operands into an r27 column (X, stride) validated against mc.
+// Upload `count` big-endian operands into an rW column (X, stride) validated against mc.
 int ingest(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint8_t* ops, size_t width, size_t count,
            DevBuf& raw, uint32_t* X, size_t stride) {
   (void)ctx;
@@ -290,7 +303,7 @@ int ingest(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint8_t
   HIP_TRY(w->flags.ensure(16));
   HIP_TRY(hipMemcpyAsync(raw.p, ops, count * width, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, st));
-  HIP_TRY(launch_ingest_be(raw.as<uint8_t>(), width, count, mc.S, mc.d + (size_t)kConstN2x * mc.S, X, stride,
+  HIP_TRY(launch_ingest_be(raw.as<uint8_t>(), width, count, mc.S, mc.W, mc.d + (size_t)kConstN2x * mc.S, X, stride,
                            w->flags.as<uint32_t>(), st));
   uint32_t flags = 0;
   HIP_TRY(hipMemcpyAsync(&flags, w->flags.p, 4, hipMemcpyDeviceToHost, st));
@@ -322,7 +335,7 @@ const char* dds_strerror(int s) {
 
 const char* dds_last_error(void) { return g_last_error.c_str(); }
 
-size_t dds_max_modulus_bits(void) { return (size_t)27 * 232 - 2; }
+size_t dds_max_modulus_bits(void) { return max_modulus_bits(); }
 
 int dds_ctx_create(int device, dds_ctx** out) {
   if (!out) return fail(DDS_E_ARG, "out");
@@ -416,9 +429,9 @@ int dds_modmul_fold(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const
     const uint32_t* part;
     size_t ps;
     if ((rc = fold_partial_device(ctx, w, wl.st, *mc, w->x.as<uint32_t>(), stride, count, &part, &ps))) return rc;
-    std::vector<uint32_t> r27;
-    if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, count, &r27))) return rc;
-    return emit_be(bn::from_r27(r27.data(), mc->S), mod_bytes, out, out_cap, out_len);
+    std::vector<uint32_t> res;
+    if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, count, &res))) return rc;
+    return emit_be(mc->value(res.data()), mod_bytes, out, out_cap, out_len);
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");
   } catch (...) {
@@ -462,7 +475,7 @@ int dds_modmul_pairs(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, cons
     std::vector<uint32_t> limbs(S);
     for (size_t i = 0; i < n; ++i) {
       for (int l = 0; l < S; ++l) limbs[l] = h[(size_t)l * stride + i];
-      if (!bn::to_be(bn::from_r27(limbs.data(), S), out + i * mod_bytes, mod_bytes))
+      if (!bn::to_be(mc->value(limbs.data()), out + i * mod_bytes, mod_bytes))
         return fail(DDS_E_RANGE, "result does not fit");
     }
     return DDS_OK;
@@ -490,11 +503,12 @@ int dds_bigint_sum(dds_ctx* ctx, const uint8_t* ops, size_t width, size_t count,
     // 2N sentinel with limb S set: every row compares below it (no range check for plain sums)
     std::vector<uint32_t> sentinel((size_t)S + 1, 0);
     sentinel[S] = 1;
+    constexpr int kPlainW = 27;
     HIP_TRY(w->misc2.ensure(sentinel.size() * 4));
     HIP_TRY(hipMemcpyAsync(w->misc2.p, sentinel.data(), sentinel.size() * 4, hipMemcpyHostToDevice, wl.st));
     HIP_TRY(hipMemcpyAsync(w->in.p, ops, count * width, hipMemcpyHostToDevice, wl.st));
     HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, wl.st));
-    HIP_TRY(launch_ingest_be(w->in.as<uint8_t>(), width, count, S, w->misc2.as<uint32_t>(), w->x.as<uint32_t>(),
+    HIP_TRY(launch_ingest_be(w->in.as<uint8_t>(), width, count, S, kPlainW, w->misc2.as<uint32_t>(), w->x.as<uint32_t>(),
                              stride, w->flags.as<uint32_t>(), wl.st));
     const size_t nthreads = std::min<size_t>(count, (size_t)ctx->cus * 1024);
     HIP_TRY(w->misc.ensure((size_t)S * nthreads * 8));
@@ -585,7 +599,7 @@ int dds_col_read(dds_col* col, size_t first, size_t count, uint8_t* out) {
     std::vector<uint32_t> limbs(S);
     for (size_t i = 0; i < count; ++i) {
       for (int l = 0; l < S; ++l) limbs[l] = h[(size_t)l * count + i];
-      if (!bn::to_be(bn::from_r27(limbs.data(), S), out + i * col->mc->bytes, col->mc->bytes))
+      if (!bn::to_be(col->mc->value(limbs.data()), out + i * col->mc->bytes, col->mc->bytes))
         return fail(DDS_E_RANGE, "row does not fit");
     }
     return DDS_OK;
@@ -650,9 +664,9 @@ int dds_col_fold(dds_col* col, size_t first, size_t count, uint8_t* out, size_t 
     size_t ps;
     if ((rc = fold_partial_device(col->ctx, wl.w, wl.st, mc, col->d + first, col->stride, count, &part, &ps)))
       return rc;
-    std::vector<uint32_t> r27;
-    if ((rc = finalize_device(col->ctx, wl.w, wl.st, mc, part, ps, count, &r27))) return rc;
-    return emit_be(bn::from_r27(r27.data(), mc.S), mc.bytes, out, out_cap, out_len);
+    std::vector<uint32_t> res;
+    if ((rc = finalize_device(col->ctx, wl.w, wl.st, mc, part, ps, count, &res))) return rc;
+    return emit_be(mc.value(res.data()), mc.bytes, out, out_cap, out_len);
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");
   }
@@ -682,9 +696,9 @@ int dds_combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, 
     size_t ps;
     if ((rc = fold_partial_device(ctx, w, wl.st, *mc, w->x.as<uint32_t>(), stride, nparts, &part, &ps))) return rc;
     // partials are already "prod * R^(1-c)": folding n of them gives prod * R^(1-k) as for rows
-    std::vector<uint32_t> r27;
-    if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, k, &r27))) return rc;
-    return emit_be(bn::from_r27(r27.data(), S), mod_bytes, out, out_cap, out_len);
+    std::vector<uint32_t> res;
+    if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, k, &res))) return rc;
+    return emit_be(mc->value(res.data()), mod_bytes, out, out_cap, out_len);
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");
   }
@@ -698,7 +712,7 @@ int encrypt_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const
   (void)ctx;
   const int S = mc.S;
   bn::Limbs gR = bn::mod(bn::mul(bn::mod(g, mc.N), mc.Rmod), mc.N);
-  std::vector<uint32_t> gr27 = bn::to_r27(gR, S);
+  std::vector<uint32_t> gr27 = mc.rw(gR);
   std::vector<uint32_t> nbits_words(n.begin(), n.end());
   if (nbits_words.empty()) nbits_words.push_back(0);
   const int nbits = use_n_exponent ? (int)bn::bit_length(n) : 0;
@@ -746,7 +760,7 @@ int dds_paillier_encrypt_batch(dds_ctx* ctx, const uint8_t* n_be, size_t n_bytes
     std::vector<uint32_t> limbs(S);
     for (size_t i = 0; i < count; ++i) {
       for (int l = 0; l < S; ++l) limbs[l] = h[(size_t)l * stride + i];
-      if (!bn::to_be(bn::from_r27(limbs.data(), S), out + i * nsq_bytes, nsq_bytes))
+      if (!bn::to_be(mc->value(limbs.data()), out + i * nsq_bytes, nsq_bytes))
         return fail(DDS_E_RANGE, "result does not fit");
     }
     return DDS_OK;
@@ -801,8 +815,8 @@ int dds_col_fill_paillier_synth(dds_col* col, const uint8_t* n_be, size_t n_byte
       bn::trim(r);
       r = bn::mod(r, n);
       if (r.empty()) r = bn::Limbs{1};
-      auto r27 = bn::to_r27(r, S);
-      for (int l = 0; l < S; ++l) rcol[(size_t)l * ps + j] = r27[l];
+      auto rl = mc.rw(r);
+      for (int l = 0; l < S; ++l) rcol[(size_t)l * ps + j] = rl[l];
     }
     HIP_TRY(hipMemcpyAsync(w->x.p, rcol.data(), rcol.size() * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(w->in2.p, zeros.data(), zeros.size() * 4, hipMemcpyHostToDevice, st));

@@ -1,6 +1,6 @@
 // HIP kernels of the homomorphic aggregation engine (gfx950 only).
 //
-// Column layout in HBM ("r27 column"): limb-transposed radix-2^27 words,
+// Column layout in HBM ("rW column"): limb-transposed radix-2^W words (W = 28 or 27),
 //   X[l * stride + row], l in [0, S), stride >= rows (multiple of 64),
 // so that the lanes of a wave touch consecutive rows of one limb (coalesced).
 //
@@ -21,9 +21,10 @@ namespace ddshe {
 // ------------------------------------------------------------------------------
 // group helpers
 // ------------------------------------------------------------------------------
-template <int S, int TPI>
+template <int S, int TPI, int W>
 struct Grp {
-  using M = Mont<S, TPI>;
+  using M = Mont<S, TPI, W>;
+  static constexpr uint32_t kMask = M::kMask;
   static constexpr int L = M::L;
   int r;        // lane index in group
   bool top;     // r == TPI-1
@@ -65,7 +66,7 @@ struct Grp {
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       const uint32_t d = a[l] - n[l] - br;
-      br = d >> 31;  // borrow iff wrapped (operands < 2^27)
+      br = d >> 31;  // borrow iff wrapped (operands < 2^W)
       a[l] = d & kMask;
     }
     for (int round = 1; round < TPI; ++round) {
@@ -88,12 +89,12 @@ struct Grp {
 };
 
 // ------------------------------------------------------------------------------
-// ingest: big-endian fixed-width rows -> r27 column (+ range classification)
+// ingest: big-endian fixed-width rows -> rW column (+ range classification)
 // ------------------------------------------------------------------------------
 // flags[0] |= 1 if some row is >= 2N (needs k_reduce_rows), flags[0] |= 2 if some
-// row does not fit in S r27 limbs (boundary error DDS_E_RANGE).
-__global__ void k_ingest_be(const uint8_t* __restrict__ in, size_t width, size_t count, int S,
-                            const uint32_t* __restrict__ n2x /* 2N in r27, S+1 limbs */, uint32_t* __restrict__ X,
+// row does not fit in S rW limbs (boundary error DDS_E_RANGE).
+__global__ void k_ingest_be(const uint8_t* __restrict__ in, size_t width, size_t count, int S, int W,
+                            const uint32_t* __restrict__ n2x /* 2N in rW, S+1 limbs */, uint32_t* __restrict__ X,
                             size_t stride, uint32_t* __restrict__ flags) {
   const size_t row = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= count) return;
@@ -101,13 +102,14 @@ __global__ void k_ingest_be(const uint8_t* __restrict__ in, size_t width, size_t
   uint64_t bitbuf = 0;
   int nbits = 0, l = 0, cmpv = 0;
   bool overflow = false;
+  const uint32_t kMask = (1u << W) - 1u;
   for (size_t i = 0; i < width; ++i) {
     bitbuf |= (uint64_t)p[width - 1 - i] << nbits;
     nbits += 8;
-    while (nbits >= 27) {
+    while (nbits >= W) {
       uint32_t limb = (uint32_t)bitbuf & kMask;
-      bitbuf >>= 27;
-      nbits -= 27;
+      bitbuf >>= W;
+      nbits -= W;
       if (l < S) {
         X[(size_t)l * stride + row] = limb;
         uint32_t nl = n2x[l];
@@ -120,7 +122,7 @@ __global__ void k_ingest_be(const uint8_t* __restrict__ in, size_t width, size_t
   }
   while (l < S + 1) {
     uint32_t limb = (uint32_t)bitbuf & kMask;
-    bitbuf >>= 27;
+    bitbuf >>= W;
     if (l < S) {
       X[(size_t)l * stride + row] = limb;
       uint32_t nl = n2x[l];
@@ -137,11 +139,11 @@ __global__ void k_ingest_be(const uint8_t* __restrict__ in, size_t width, size_t
 }
 
 // rows >= 2N: x <- MonPro(MonPro(x, R^2 mod N), 1) = x mod N
-template <int S, int TPI>
+template <int S, int TPI, int W>
 __global__ void __launch_bounds__(256) k_reduce_rows(uint32_t* __restrict__ X, size_t stride, size_t count,
                                                      const uint32_t* __restrict__ consts, uint32_t n0) {
-  using G = Grp<S, TPI>;
-  using M = Mont<S, TPI>;
+  using G = Grp<S, TPI, W>;
+  using M = Mont<S, TPI, W>;
   constexpr int L = G::L;
   G g;
   const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
@@ -156,8 +158,8 @@ __global__ void __launch_bounds__(256) k_reduce_rows(uint32_t* __restrict__ X, s
   g.load_col(a, X, stride, grp);
   // 2N fits in S limbs (S chosen with 2 bits of headroom)
   if (g.cmp(a, n2) < 0) return;
-  M::mul_col(a, n, R2, 1, n0, g.top, g.bottom);
-  M::mul_col(a, n, ONE, 1, n0, g.top, g.bottom);
+  M::mul_col(a, n, R2, 1, 0, n0, g.top, g.bottom);
+  M::mul_col(a, n, ONE, 1, 0, n0, g.top, g.bottom);
   M::normalize(a, g.bottom);
   g.store_col(a, X, stride, grp);
 }
@@ -166,12 +168,12 @@ __global__ void __launch_bounds__(256) k_reduce_rows(uint32_t* __restrict__ X, s
 // fold: each group folds rows g, g+G, g+2G, ... with Montgomery products.
 // A group that folded c rows holds prod * R^(1-c); an empty group holds R mod N.
 // ------------------------------------------------------------------------------
-template <int S, int TPI>
+template <int S, int TPI, int W>
 __global__ void __launch_bounds__(256) k_fold(const uint32_t* __restrict__ X, size_t xstride, size_t count,
                                               const uint32_t* __restrict__ consts, uint32_t n0,
                                               uint32_t* __restrict__ P, size_t pstride, size_t ngroups) {
-  using G = Grp<S, TPI>;
-  using M = Mont<S, TPI>;
+  using G = Grp<S, TPI, W>;
+  using M = Mont<S, TPI, W>;
   constexpr int L = G::L;
   G g;
   const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
@@ -185,37 +187,37 @@ __global__ void __launch_bounds__(256) k_fold(const uint32_t* __restrict__ X, si
   } else {
     g.load_vec(a, consts + kConstRmod * S);
   }
-  for (; row < count; row += ngroups) M::mul_col(a, n, X + row, xstride, n0, g.top, g.bottom);
+  for (; row < count; row += ngroups) M::mul_col(a, n, X, xstride, (uint32_t)row, n0, g.top, g.bottom);
   M::normalize(a, g.bottom);
   g.store_col(a, P, pstride, grp);
 }
 
-// result = canon(MonPro(P[0], Y)), Y = R^k mod N; writes S r27 limbs to out
-template <int S, int TPI>
+// result = canon(MonPro(P[0], Y)), Y = R^k mod N; writes S rW limbs to out
+template <int S, int TPI, int W>
 __global__ void __launch_bounds__(64) k_finalize(const uint32_t* __restrict__ P, size_t pstride,
                                                  const uint32_t* __restrict__ consts, const uint32_t* __restrict__ Y,
                                                  uint32_t n0, uint32_t* __restrict__ out) {
-  using G = Grp<S, TPI>;
-  using M = Mont<S, TPI>;
+  using G = Grp<S, TPI, W>;
+  using M = Mont<S, TPI, W>;
   constexpr int L = G::L;
   G g;
   if (threadIdx.x >= TPI) return;
   uint32_t n[L], a[L];
   g.load_vec(n, consts + kConstN * S);
   g.load_col(a, P, pstride, 0);
-  M::mul_col(a, n, Y, 1, n0, g.top, g.bottom);
+  M::mul_col(a, n, Y, 1, 0, n0, g.top, g.bottom);
   g.canon(a, n);
 #pragma unroll
   for (int l = 0; l < L; ++l) out[g.r * L + l] = a[l];
 }
 
-// out[i] = A[i]*B[i] mod N (canonical), r27 columns in and out
-template <int S, int TPI>
+// out[i] = A[i]*B[i] mod N (canonical), rW columns in and out
+template <int S, int TPI, int W>
 __global__ void __launch_bounds__(256) k_pairs(const uint32_t* __restrict__ A, const uint32_t* __restrict__ B,
                                                size_t stride, size_t count, const uint32_t* __restrict__ consts,
                                                uint32_t n0, uint32_t* __restrict__ O) {
-  using G = Grp<S, TPI>;
-  using M = Mont<S, TPI>;
+  using G = Grp<S, TPI, W>;
+  using M = Mont<S, TPI, W>;
   constexpr int L = G::L;
   G g;
   const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
@@ -223,8 +225,8 @@ __global__ void __launch_bounds__(256) k_pairs(const uint32_t* __restrict__ A, c
   uint32_t n[L], a[L];
   g.load_vec(n, consts + kConstN * S);
   g.load_col(a, A, stride, grp);
-  M::mul_col(a, n, B + grp, stride, n0, g.top, g.bottom);               // a*b*R^-1
-  M::mul_col(a, n, consts + kConstR2 * S, 1, n0, g.top, g.bottom);      // a*b
+  M::mul_col(a, n, B, stride, (uint32_t)grp, n0, g.top, g.bottom);       // a*b*R^-1
+  M::mul_col(a, n, consts + kConstR2 * S, 1, 0, n0, g.top, g.bottom);   // a*b
   g.canon(a, n);
   g.store_col(a, O, stride, grp);
 }
@@ -233,11 +235,11 @@ __global__ void __launch_bounds__(256) k_pairs(const uint32_t* __restrict__ A, c
 // Montgomery exponentiation helpers (register operands via ds_bpermute)
 // ------------------------------------------------------------------------------
 // acc <- acc^e * acc_in... : left-to-right binary over the bits of a uniform exponent
-template <int S, int TPI, int L>
+template <int S, int TPI, int W, int L>
 __device__ __forceinline__ void mont_pow_uniform(uint32_t (&acc)[L], const uint32_t (&x)[L], const uint32_t (&n)[L],
                                                  uint32_t n0, const uint32_t* __restrict__ ebits, int nbits,
-                                                 const Grp<S, TPI>& g) {
-  using M = Mont<S, TPI>;
+                                                 const Grp<S, TPI, W>& g) {
+  using M = Mont<S, TPI, W>;
   for (int i = nbits - 1; i >= 0; --i) {
     M::normalize(acc, g.bottom);
     uint32_t sq[M::L];
@@ -248,17 +250,17 @@ __device__ __forceinline__ void mont_pow_uniform(uint32_t (&acc)[L], const uint3
   }
 }
 
-// c_i = g^m_i * r_i^n mod N (N = n^2). Inputs r in r27 column (values < N), m per row.
+// c_i = g^m_i * r_i^n mod N (N = n^2). Inputs r in rW column (values < N), m per row.
 // consts: N, gR (g*R mod N, Montgomery form), Rmod (1 in Montgomery form), R2, One
-template <int S, int TPI>
+template <int S, int TPI, int W>
 __global__ void __launch_bounds__(256) k_paillier_encrypt(const uint32_t* __restrict__ Rcol, size_t stride,
                                                           const uint32_t* __restrict__ m, size_t count,
                                                           const uint32_t* __restrict__ consts,
                                                           const uint32_t* __restrict__ gR,
                                                           const uint32_t* __restrict__ nbits_words, int nbits,
                                                           uint32_t n0, uint32_t* __restrict__ O) {
-  using G = Grp<S, TPI>;
-  using M = Mont<S, TPI>;
+  using G = Grp<S, TPI, W>;
+  using M = Mont<S, TPI, W>;
   constexpr int L = G::L;
   G g;
   const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
@@ -266,10 +268,10 @@ __global__ void __launch_bounds__(256) k_paillier_encrypt(const uint32_t* __rest
   uint32_t n[L], x[L], acc[L], gx[L], acc2[L];
   g.load_vec(n, consts + kConstN * S);
   g.load_col(x, Rcol, stride, grp);
-  M::mul_col(x, n, consts + kConstR2 * S, 1, n0, g.top, g.bottom);  // r*R
+  M::mul_col(x, n, consts + kConstR2 * S, 1, 0, n0, g.top, g.bottom);  // r*R
   M::normalize(x, g.bottom);
   g.load_vec(acc, consts + kConstRmod * S);                         // 1*R
-  mont_pow_uniform<S, TPI, L>(acc, x, n, n0, nbits_words, nbits, g);   // r^n * R
+  mont_pow_uniform<S, TPI, W, L>(acc, x, n, n0, nbits_words, nbits, g);   // r^n * R
   // g^m with a per-row exponent: multiply-always with a select to stay uniform
   g.load_vec(gx, gR);
   g.load_vec(acc2, consts + kConstRmod * S);
@@ -294,7 +296,7 @@ __global__ void __launch_bounds__(256) k_paillier_encrypt(const uint32_t* __rest
   }
   M::normalize(acc2, g.bottom);
   M::mul_reg(acc, acc2, n, n0, g.r, g.top, g.bottom);               // g^m r^n R
-  M::mul_col(acc, n, consts + kConstOne * S, 1, n0, g.top, g.bottom);  // g^m r^n
+  M::mul_col(acc, n, consts + kConstOne * S, 1, 0, n0, g.top, g.bottom);  // g^m r^n
   g.canon(acc, n);
   g.store_col(acc, O, stride, grp);
 }
@@ -311,14 +313,14 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
-template <int S, int TPI>
+template <int S, int TPI, int W>
 __global__ void __launch_bounds__(256) k_synth_rows(const uint32_t* __restrict__ T, size_t tstride, uint32_t tcount,
                                                     const uint32_t* __restrict__ P, size_t pstride, uint32_t pcount,
                                                     uint64_t seed, uint64_t row0, size_t count,
                                                     const uint32_t* __restrict__ consts, uint32_t n0,
                                                     uint32_t* __restrict__ X, size_t xstride) {
-  using G = Grp<S, TPI>;
-  using M = Mont<S, TPI>;
+  using G = Grp<S, TPI, W>;
+  using M = Mont<S, TPI, W>;
   constexpr int L = G::L;
   G g;
   const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
@@ -330,9 +332,9 @@ __global__ void __launch_bounds__(256) k_synth_rows(const uint32_t* __restrict__
   uint32_t n[L], a[L];
   g.load_vec(n, consts + kConstN * S);
   g.load_col(a, T, tstride, mi);
-  M::mul_col(a, n, P + ai, pstride, n0, g.top, g.bottom);
+  M::mul_col(a, n, P, pstride, ai, n0, g.top, g.bottom);
   M::normalize(a, g.bottom);
-  M::mul_col(a, n, P + bi, pstride, n0, g.top, g.bottom);
+  M::mul_col(a, n, P, pstride, bi, n0, g.top, g.bottom);
   g.canon(a, n);
   g.store_col(a, X, xstride, grp);
 }
@@ -472,73 +474,68 @@ __global__ void __launch_bounds__(256) k_plain_sum_reduce(const uint64_t* __rest
 // ------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------
-#define DDSHE_DISPATCH(S_, TPI_, ...) \
-  case S_: {                          \
-    constexpr int S = S_, TPI = TPI_; \
-    __VA_ARGS__;                      \
+// Instantiated shapes (S limbs of W bits on TPI lanes); a modulus uses the first that holds
+// bits+2 bits. Keep in sync with kShapes below.
+#define DDSHE_DISPATCH(S_, TPI_, W_, ...)            \
+  case S_: {                                         \
+    constexpr int S = S_, TPI = TPI_, W = W_;        \
+    __VA_ARGS__;                                     \
   } break;
 
-#define DDSHE_SWITCH(S_RT, ...)                 \
-  switch (S_RT) {                               \
-    DDSHE_DISPATCH(40, 1, __VA_ARGS__)          \
-    DDSHE_DISPATCH(76, 2, __VA_ARGS__)          \
-    DDSHE_DISPATCH(152, 4, __VA_ARGS__)         \
-    DDSHE_DISPATCH(232, 8, __VA_ARGS__)         \
-    default: return hipErrorInvalidValue;       \
+#define DDSHE_SWITCH(S_RT, ...)                      \
+  switch (S_RT) {                                    \
+    DDSHE_DISPATCH(40, 1, 28, __VA_ARGS__)           \
+    DDSHE_DISPATCH(74, 2, 28, __VA_ARGS__)           \
+    DDSHE_DISPATCH(148, 4, 28, __VA_ARGS__)          \
+    DDSHE_DISPATCH(232, 8, 27, __VA_ARGS__)          \
+    default: return hipErrorInvalidValue;            \
   }
 
-int tpi_for(int S) {
-  switch (S) {
-    case 40: return 1;
-    case 76: return 2;
-    case 152: return 4;
-    case 232: return 8;
-    default: return 0;
-  }
+static const Shape kShapes[] = {{40, 1, 28}, {74, 2, 28}, {148, 4, 28}, {232, 8, 27}};
+
+Shape pick_shape(size_t mod_bits) {
+  for (const Shape& s : kShapes)
+    if ((size_t)s.W * s.S >= mod_bits + 2) return s;
+  return Shape{0, 0, 0};
 }
 
-int pick_S(size_t mod_bits) {
-  const size_t need = mod_bits + 2;
-  const int choices[] = {40, 76, 152, 232};
-  for (int s : choices)
-    if ((size_t)27 * s >= need) return s;
-  return 0;
-}
+size_t max_modulus_bits() { return (size_t)kShapes[3].W * kShapes[3].S - 2; }
 
 static inline unsigned grid_for(size_t threads) { return (unsigned)((threads + 255) / 256); }
 
-hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, const uint32_t* n2x, uint32_t* X,
-                            size_t stride, uint32_t* flags, hipStream_t st) {
+hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, int W, const uint32_t* n2x,
+                            uint32_t* X, size_t stride, uint32_t* flags, hipStream_t st) {
   if (count == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ingest_be, dim3(grid_for(count)), dim3(256), 0, st, in, width, count, S, n2x, X, stride, flags);
+  hipLaunchKernelGGL(k_ingest_be, dim3(grid_for(count)), dim3(256), 0, st, in, width, count, S, W, n2x, X, stride,
+                     flags);
   return hipGetLastError();
 }
 
 hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, const uint32_t* consts, uint32_t n0,
                               hipStream_t st) {
   if (count == 0) return hipSuccess;
-  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_reduce_rows<S, TPI>), dim3(grid_for(count * TPI)), dim3(256), 0, st, X, stride,
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_reduce_rows<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), 0, st, X, stride,
                                      count, consts, n0));
   return hipGetLastError();
 }
 
 hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts, uint32_t n0,
                        uint32_t* P, size_t pstride, size_t ngroups, hipStream_t st) {
-  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X, xstride,
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X, xstride,
                                      count, consts, n0, P, pstride, ngroups));
   return hipGetLastError();
 }
 
 hipError_t launch_finalize(int S, const uint32_t* P, size_t pstride, const uint32_t* consts, const uint32_t* Y,
                            uint32_t n0, uint32_t* out, hipStream_t st) {
-  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_finalize<S, TPI>), dim3(1), dim3(64), 0, st, P, pstride, consts, Y, n0, out));
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_finalize<S, TPI, W>), dim3(1), dim3(64), 0, st, P, pstride, consts, Y, n0, out));
   return hipGetLastError();
 }
 
 hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stride, size_t count,
                         const uint32_t* consts, uint32_t n0, uint32_t* O, hipStream_t st) {
   if (count == 0) return hipSuccess;
-  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_pairs<S, TPI>), dim3(grid_for(count * TPI)), dim3(256), 0, st, A, B, stride,
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_pairs<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), 0, st, A, B, stride,
                                      count, consts, n0, O));
   return hipGetLastError();
 }
@@ -547,7 +544,7 @@ hipError_t launch_paillier_encrypt(int S, const uint32_t* Rcol, size_t stride, c
                                    const uint32_t* consts, const uint32_t* gR, const uint32_t* nbits_words, int nbits,
                                    uint32_t n0, uint32_t* O, hipStream_t st) {
   if (count == 0) return hipSuccess;
-  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_paillier_encrypt<S, TPI>), dim3(grid_for(count * TPI)), dim3(256), 0, st,
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_paillier_encrypt<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), 0, st,
                                      Rcol, stride, m, count, consts, gR, nbits_words, nbits, n0, O));
   return hipGetLastError();
 }
@@ -556,7 +553,7 @@ hipError_t launch_synth_rows(int S, const uint32_t* T, size_t tstride, uint32_t 
                              size_t pstride, uint32_t pcount, uint64_t seed, uint64_t row0, size_t count,
                              const uint32_t* consts, uint32_t n0, uint32_t* X, size_t xstride, hipStream_t st) {
   if (count == 0) return hipSuccess;
-  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_synth_rows<S, TPI>), dim3(grid_for(count * TPI)), dim3(256), 0, st, T, tstride,
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_synth_rows<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), 0, st, T, tstride,
                                      tcount, P, pstride, pcount, seed, row0, count, consts, n0, X, xstride));
   return hipGetLastError();
 }
@@ -582,7 +579,7 @@ hipError_t launch_plain_sum(const uint32_t* X, size_t stride, size_t count, int 
 }
 
 hipError_t fold_occupancy(int S, int* blocks_per_cu) {
-  DDSHE_SWITCH(S, return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (const void*)k_fold<S, TPI>, 256,
+  DDSHE_SWITCH(S, return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (const void*)k_fold<S, TPI, W>, 256,
                                                                        0));
   return hipSuccess;
 }

@@ -9,11 +9,16 @@ namespace ddshe {
 // per-modulus constant block: 5 vectors of S r27 limbs each
 enum { kConstN = 0, kConstRmod = 1, kConstR2 = 2, kConstOne = 3, kConstN2x = 4, kConstCount = 5 };
 
-int pick_S(size_t mod_bits);  // limb count for a modulus of mod_bits bits (0 = unsupported)
-int tpi_for(int S);           // lanes per bignum for that S
+struct Shape {
+  int S;    // limbs
+  int TPI;  // lanes per bignum
+  int W;    // radix bits
+};
+Shape pick_shape(size_t mod_bits);  // S == 0: unsupported
+size_t max_modulus_bits();
 
-hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, const uint32_t* n2x, uint32_t* X,
-                            size_t stride, uint32_t* flags, hipStream_t st);
+hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, int W, const uint32_t* n2x,
+                            uint32_t* X, size_t stride, uint32_t* flags, hipStream_t st);
 hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, const uint32_t* consts, uint32_t n0,
                               hipStream_t st);
 hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts, uint32_t n0,

@@ -111,9 +111,9 @@ def test_fold_small_modulus_and_wide_operands(eng):
 
 def test_fold_operand_too_wide_is_range_error(eng):
     import ddshe
-    N = (1 << 61) - 1      # 40 r27 limbs = 1080 bits of operand width
+    N = (1 << 61) - 1      # smallest shape: 40 limbs of 28 bits = 1120 bits of operand width
     with pytest.raises(ddshe.DDSError) as ei:
-        eng.modmul_fold(N, [1 << 1100, 3])
+        eng.modmul_fold(N, [1 << 1500, 3])
     assert ei.value.status == ddshe.DDS_E_RANGE
 
 
