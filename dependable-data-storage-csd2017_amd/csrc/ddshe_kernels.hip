@@ -120,7 +120,7 @@ __global__ void k_ingest_be(const uint8_t* __restrict__ in, size_t width, size_t
       ++l;
     }
   }
-  while (l < S + 1) {
+  while (l < S || bitbuf != 0) {  // flush: zero-pad to S limbs, any leftover bit beyond S overflows
     uint32_t limb = (uint32_t)bitbuf & kMask;
     bitbuf >>= W;
     if (l < S) {
