@@ -63,6 +63,7 @@ struct DevBuf {
 
 struct Worker {
   hipStream_t stream = nullptr;
+  bool timed_fold = false;  // ev[0]/ev[1] bracket a first-level fold launch not yet accounted
   DevBuf in, in2, x, x2, p0, p1, out, flags, y, misc, misc2;
   hipEvent_t ev[4] = {};
   ~Worker() {
@@ -72,29 +73,48 @@ struct Worker {
   }
 };
 
+// Per-modulus constants for the two kernel shapes: the throughput shape (S limbs, TPI
+// lanes) of the first fold level, and the latency shape (S2 limbs, 16 lanes) of the
+// reduction tree and finalize. Both use radix 2^W, so R = 2^(W*S) and R2 = 2^(W*S2)
+// differ only by a power of two: every partial is tracked as prod * 2^E (E signed).
 struct ModConsts {
-  int S = 0, TPI = 0, W = 0;
+  int S = 0, TPI = 0, W = 0, S2 = 0;
   size_t bits = 0, bytes = 0;
   uint32_t n0 = 0;
-  bn::Limbs N, Rmod;
-  std::vector<uint32_t> host;  // kConstCount * S
-  uint32_t* d = nullptr;       // device copy
+  bn::Limbs N, Rmod, half;       // half = (N+1)/2 = 2^-1 mod N
+  std::vector<uint32_t> host;    // kConstCount * S  (throughput shape)
+  std::vector<uint32_t> host2;   // kConstCount * S2 (tail shape)
+  uint32_t* d = nullptr;         // device copies
+  uint32_t* d2 = nullptr;
   std::mutex ymu;
-  std::map<uint64_t, std::vector<uint32_t>> ycache;  // k -> R^k mod N (rW)
+  std::map<int64_t, std::vector<uint32_t>> ycache;  // E -> 2^(W*S2 - E) mod N, tail limbs
   ~ModConsts() {
     if (d) (void)hipFree(d);
+    if (d2) (void)hipFree(d2);
   }
   std::vector<uint32_t> rw(const bn::Limbs& v) const { return bn::to_rw(v, S, W); }
   bn::Limbs value(const uint32_t* limbs) const { return bn::from_rw(limbs, S, W); }
-  const std::vector<uint32_t>& y_for(uint64_t k) {
+  bn::Limbs value2(const uint32_t* limbs) const { return bn::from_rw(limbs, S2, W); }
+  // 2^e mod N for a signed e
+  bn::Limbs pow2(int64_t e) const {
+    return e >= 0 ? bn::powmod_u64(bn::Limbs{2}, (uint64_t)e, N) : bn::powmod_u64(half, (uint64_t)(-e), N);
+  }
+  // finalize multiplier for a tail-shape partial holding prod * 2^E
+  const std::vector<uint32_t>& y_for(int64_t E) {
     std::lock_guard<std::mutex> lk(ymu);
-    auto it = ycache.find(k);
+    auto it = ycache.find(E);
     if (it != ycache.end()) return it->second;
     if (ycache.size() > 64) ycache.clear();
-    bn::Limbs y = bn::powmod_u64(Rmod, k, N);
-    return ycache.emplace(k, rw(y)).first->second;
+    bn::Limbs y = pow2((int64_t)W * S2 - E);
+    return ycache.emplace(E, bn::to_rw(y, S2, W)).first->second;
   }
+  // bits of 2 contributed by one Montgomery product of the main / tail shape
+  int64_t wS() const { return (int64_t)W * S; }
+  int64_t wS2() const { return (int64_t)W * S2; }
 };
+
+// partial exchanged between GPUs: S2 tail limbs + signed exponent E (two words)
+size_t partial_words_for(const ModConsts& mc) { return (size_t)mc.S2 + 2; }
 
 }  // namespace
 
@@ -176,31 +196,41 @@ int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_p
   mc->bytes = (mc->bits + 7) / 8;
   const Shape sh = pick_shape(mc->bits);
   if (!sh.S) return fail(DDS_E_UNSUPPORTED, "modulus too large");
+  const Shape tail = tail_shape(sh);
   mc->S = sh.S;
   mc->TPI = sh.TPI;
   mc->W = sh.W;
+  mc->S2 = tail.S;
   const int S = mc->S;
   mc->N = N;
+  mc->half = bn::sub(bn::add(N, bn::Limbs{1}), bn::Limbs{});
+  (void)bn::divmod_small(mc->half, 2);
   mc->n0 = bn::mont_n0(N[0], mc->W);
   mc->Rmod = bn::mod(bn::pow2((size_t)mc->W * S), N);
   bn::Limbs R2 = bn::mod(bn::mul(mc->Rmod, mc->Rmod), N);
   bn::Limbs N2 = bn::add(N, N);
-  mc->host.assign((size_t)kConstCount * S, 0);
-  auto put = [&](int slot, const bn::Limbs& v) {
-    auto r = mc->rw(v);
-    std::copy(r.begin(), r.end(), mc->host.begin() + (size_t)slot * S);
+  auto fill = [&](std::vector<uint32_t>& dst, int s, const bn::Limbs& rmod, const bn::Limbs& r2) {
+    dst.assign((size_t)kConstCount * s + 1, 0);  // +1: ingest reads 2N limb s (always 0 by choice of s)
+    auto put = [&](int slot, const bn::Limbs& v) {
+      auto r = bn::to_rw(v, s, mc->W);
+      std::copy(r.begin(), r.end(), dst.begin() + (size_t)slot * s);
+    };
+    put(kConstN, N);
+    put(kConstRmod, rmod);
+    put(kConstR2, r2);
+    put(kConstOne, bn::Limbs{1});
+    put(kConstN2x, N2);
   };
-  put(kConstN, N);
-  put(kConstRmod, mc->Rmod);
-  put(kConstR2, R2);
-  put(kConstOne, bn::Limbs{1});
-  put(kConstN2x, N2);
+  fill(mc->host, S, mc->Rmod, R2);
+  {
+    bn::Limbs rm2 = bn::mod(bn::pow2((size_t)mc->W * mc->S2), N);
+    fill(mc->host2, mc->S2, rm2, bn::mod(bn::mul(rm2, rm2), N));
+  }
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(DDS_E_HIP, "hipSetDevice");
-  if (hipMalloc(&mc->d, (mc->host.size() + 1) * 4) != hipSuccess) return fail(DDS_E_NOMEM, "const alloc");
-  std::vector<uint32_t> up(mc->host);
-  up.push_back(0);  // ingest reads 2N limb S (always 0 by construction of S)
-  // 2N lives in the last slot; the extra zero word follows it
-  if (hipMemcpy(mc->d, up.data(), up.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+  if (hipMalloc(&mc->d, mc->host.size() * 4) != hipSuccess || hipMalloc(&mc->d2, mc->host2.size() * 4) != hipSuccess)
+    return fail(DDS_E_NOMEM, "const alloc");
+  if (hipMemcpy(mc->d, mc->host.data(), mc->host.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(mc->d2, mc->host2.data(), mc->host2.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
     return fail(DDS_E_HIP, "const upload");
   std::lock_guard<std::mutex> lk(ctx->mu);
   auto it = ctx->mods.find(N);
@@ -233,18 +263,22 @@ size_t max_fold_groups(dds_ctx* ctx, int S) {
   return (size_t)ctx->cus * bpc * (256 / pick_tpi(S));
 }
 
-// Fold `count` rows of an rW column into one un-finalised partial (in `*part`, stride pstride, row 0).
+// Fold `count` rows of an rW column into one un-finalised partial: tail-shape limbs
+// (row 0 of `*part`, stride `*part_stride`) holding prod(rows) * 2^(*E).
+//   level 1 (throughput shape, G groups): group g holds prod_g * R^(1 - c_g)
+//   tree (tail shape, G-1 products):      multiplies by R2^-(G-1)
 int fold_partial_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
-                        size_t count, const uint32_t** part, size_t* part_stride) {
-  const int S = mc.S;
+                        size_t count, const uint32_t** part, size_t* part_stride, int64_t* E) {
+  const int S = mc.S, S2 = mc.S2;
   size_t G = std::min(max_fold_groups(ctx, S), std::max<size_t>(1, count / 2));
   size_t ps = round_up(G, 64);
-  HIP_TRY(w->p0.ensure((size_t)S * ps * 4));
-  HIP_TRY(w->p1.ensure((size_t)S * round_up((G + 1) / 2, 64) * 4));
+  HIP_TRY(w->p0.ensure((size_t)S2 * ps * 4));
+  HIP_TRY(w->p1.ensure((size_t)S2 * round_up((G + 1) / 2, 64) * 4));
   record_time(ctx, w, st, true, 0);
-  HIP_TRY(launch_fold(S, X, xstride, count, mc.d, mc.n0, w->p0.as<uint32_t>(), ps, G, st));
+  HIP_TRY(launch_fold(S, X, xstride, count, mc.d, mc.n0, w->p0.as<uint32_t>(), ps, G, S2, st));
   record_time(ctx, w, st, false, 0);
   if (ctx->timing.load()) {
+    w->timed_fold = true;
     // Montgomery products issued by this launch: every row but each group's first
     std::lock_guard<std::mutex> lk(ctx->tmu);
     ctx->pending_modmuls = count > G ? count - G : 0;
@@ -254,36 +288,43 @@ int fold_partial_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, 
   size_t n = G, cs = ps;
   while (n > 1) {
     size_t ng = (n + 1) / 2, ns = round_up(ng, 64);
-    HIP_TRY(launch_fold(S, cur, cs, n, mc.d, mc.n0, nxt, ns, ng, st));
+    HIP_TRY(launch_fold_tail(S2, cur, cs, n, mc.d2, mc.n0, nxt, ns, ng, st));
     std::swap(cur, nxt);
     n = ng;
     cs = ns;
   }
   *part = cur;
   *part_stride = cs;
+  *E = mc.wS() * ((int64_t)G - (int64_t)count) - mc.wS2() * ((int64_t)G - 1);
   return DDS_OK;
 }
 
-int finalize_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* part, size_t pstride,
-                    uint64_t k, std::vector<uint32_t>* result_rw) {
-  const int S = mc.S;
-  const std::vector<uint32_t>& y = mc.y_for(k);
-  HIP_TRY(w->y.ensure((size_t)S * 4));
-  HIP_TRY(w->out.ensure((size_t)S * 4));
-  HIP_TRY(hipMemcpyAsync(w->y.p, y.data(), (size_t)S * 4, hipMemcpyHostToDevice, st));
-  HIP_TRY(launch_finalize(S, part, pstride, mc.d, w->y.as<uint32_t>(), mc.n0, w->out.as<uint32_t>(), st));
-  result_rw->assign(S, 0);
-  HIP_TRY(hipMemcpyAsync(result_rw->data(), w->out.p, (size_t)S * 4, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  if (ctx->timing.load()) {
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, w->ev[0], w->ev[1]) == hipSuccess) {
-      std::lock_guard<std::mutex> lk(ctx->tmu);
-      ctx->fold_ms += ms;
-      ctx->fold_launches += 1;
-      ctx->fold_modmuls += ctx->pending_modmuls;
-    }
+// after the stream has synchronised: account the timed first-level fold launch, if any
+void account_fold(dds_ctx* ctx, Worker* w) {
+  if (!w->timed_fold) return;
+  w->timed_fold = false;
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, w->ev[0], w->ev[1]) == hipSuccess) {
+    std::lock_guard<std::mutex> lk(ctx->tmu);
+    ctx->fold_ms += ms;
+    ctx->fold_launches += 1;
+    ctx->fold_modmuls += ctx->pending_modmuls;
   }
+}
+
+// canonical prod from a tail-shape partial holding prod * 2^E
+int finalize_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* part, size_t pstride,
+                    int64_t E, std::vector<uint32_t>* result_rw) {
+  const int S2 = mc.S2;
+  const std::vector<uint32_t>& y = mc.y_for(E);
+  HIP_TRY(w->y.ensure((size_t)S2 * 4));
+  HIP_TRY(w->out.ensure((size_t)S2 * 4));
+  HIP_TRY(hipMemcpyAsync(w->y.p, y.data(), (size_t)S2 * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(launch_finalize_tail(S2, part, pstride, mc.d2, w->y.as<uint32_t>(), mc.n0, w->out.as<uint32_t>(), st));
+  result_rw->assign(S2, 0);
+  HIP_TRY(hipMemcpyAsync(result_rw->data(), w->out.p, (size_t)S2 * 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  account_fold(ctx, w);
   return DDS_OK;
 }
 
@@ -428,10 +469,11 @@ int dds_modmul_fold(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const
     if ((rc = ingest(ctx, w, wl.st, *mc, ops, width, count, w->in, w->x.as<uint32_t>(), stride))) return rc;
     const uint32_t* part;
     size_t ps;
-    if ((rc = fold_partial_device(ctx, w, wl.st, *mc, w->x.as<uint32_t>(), stride, count, &part, &ps))) return rc;
+    int64_t E;
+    if ((rc = fold_partial_device(ctx, w, wl.st, *mc, w->x.as<uint32_t>(), stride, count, &part, &ps, &E))) return rc;
     std::vector<uint32_t> res;
-    if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, count, &res))) return rc;
-    return emit_be(mc->value(res.data()), mod_bytes, out, out_cap, out_len);
+    if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, E, &res))) return rc;
+    return emit_be(mc->value2(res.data()), mod_bytes, out, out_cap, out_len);
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");
   } catch (...) {
@@ -566,7 +608,7 @@ int dds_col_destroy(dds_col* col) {
 
 size_t dds_col_count(const dds_col* col) { return col ? col->count : 0; }
 
-size_t dds_col_partial_words(const dds_col* col) { return col ? (size_t)col->mc->S : 0; }
+size_t dds_col_partial_words(const dds_col* col) { return col ? partial_words_for(*col->mc) : 0; }
 
 int dds_col_append(dds_col* col, const uint8_t* ops, size_t width, size_t count) {
   try {
@@ -611,31 +653,26 @@ int dds_col_read(dds_col* col, size_t first, size_t count, uint8_t* out) {
 int dds_col_fold_partial(dds_col* col, size_t first, size_t count, uint32_t* partial, uint64_t* rows) {
   try {
     if (!col || !partial || first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
-    WorkerLease wl(col->ctx);
-    int rc;
-    if ((rc = wl.acquire())) return rc;
     ModConsts& mc = *col->mc;
-    if (count == 0) {  // empty partial = R mod N (identity of the partial algebra)
-      std::copy(mc.host.begin() + (size_t)kConstRmod * mc.S, mc.host.begin() + (size_t)(kConstRmod + 1) * mc.S,
-                partial);
-      if (rows) *rows = 0;
-      return DDS_OK;
+    const size_t S2 = (size_t)mc.S2;
+    int64_t E = 0;
+    if (count == 0) {  // empty partial: prod = 1, E = 0
+      std::fill(partial, partial + S2, 0u);
+      partial[0] = 1;
+    } else {
+      WorkerLease wl(col->ctx);
+      int rc;
+      if ((rc = wl.acquire())) return rc;
+      const uint32_t* part;
+      size_t ps;
+      if ((rc = fold_partial_device(col->ctx, wl.w, wl.st, mc, col->d + first, col->stride, count, &part, &ps, &E)))
+        return rc;
+      HIP_TRY(hipMemcpy2DAsync(partial, 4, part, ps * 4, 4, S2, hipMemcpyDeviceToHost, wl.st));
+      HIP_TRY(hipStreamSynchronize(wl.st));
+      account_fold(col->ctx, wl.w);
     }
-    const uint32_t* part;
-    size_t ps;
-    if ((rc = fold_partial_device(col->ctx, wl.w, wl.st, mc, col->d + first, col->stride, count, &part, &ps)))
-      return rc;
-    HIP_TRY(hipMemcpy2DAsync(partial, 4, part, ps * 4, 4, (size_t)mc.S, hipMemcpyDeviceToHost, wl.st));
-    HIP_TRY(hipStreamSynchronize(wl.st));
-    if (col->ctx->timing.load()) {
-      float ms = 0;
-      if (hipEventElapsedTime(&ms, wl.w->ev[0], wl.w->ev[1]) == hipSuccess) {
-        std::lock_guard<std::mutex> lk(col->ctx->tmu);
-        col->ctx->fold_ms += ms;
-        col->ctx->fold_launches += 1;
-        col->ctx->fold_modmuls += col->ctx->pending_modmuls;
-      }
-    }
+    partial[S2] = (uint32_t)(uint64_t)E;
+    partial[S2 + 1] = (uint32_t)((uint64_t)E >> 32);
     if (rows) *rows = count;
     return DDS_OK;
   } catch (const std::bad_alloc&) {
@@ -662,11 +699,12 @@ int dds_col_fold(dds_col* col, size_t first, size_t count, uint8_t* out, size_t 
     if ((rc = wl.acquire())) return rc;
     const uint32_t* part;
     size_t ps;
-    if ((rc = fold_partial_device(col->ctx, wl.w, wl.st, mc, col->d + first, col->stride, count, &part, &ps)))
+    int64_t E;
+    if ((rc = fold_partial_device(col->ctx, wl.w, wl.st, mc, col->d + first, col->stride, count, &part, &ps, &E)))
       return rc;
     std::vector<uint32_t> res;
-    if ((rc = finalize_device(col->ctx, wl.w, wl.st, mc, part, ps, count, &res))) return rc;
-    return emit_be(mc.value(res.data()), mc.bytes, out, out_cap, out_len);
+    if ((rc = finalize_device(col->ctx, wl.w, wl.st, mc, part, ps, E, &res))) return rc;
+    return emit_be(mc.value2(res.data()), mc.bytes, out, out_cap, out_len);
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");
   }
@@ -682,23 +720,37 @@ int dds_combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, 
     uint64_t k = 0;
     for (size_t i = 0; i < nparts; ++i) k += rows[i];
     if (k == 0) return fail(DDS_E_EMPTY, "no operand");
-    const int S = mc->S;
+    const size_t S2 = (size_t)mc->S2, pw = partial_words_for(*mc);
     WorkerLease wl(ctx);
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
+    // the tree below multiplies by R2^-(n-1); each partial carries its own 2^E_i
+    int64_t E = -mc->wS2() * ((int64_t)nparts - 1);
     const size_t stride = round_up(nparts, 64);
-    std::vector<uint32_t> h((size_t)S * stride, 0);
-    for (size_t i = 0; i < nparts; ++i)
-      for (int l = 0; l < S; ++l) h[(size_t)l * stride + i] = partials[i * S + l];
+    std::vector<uint32_t> h(S2 * stride, 0);
+    for (size_t i = 0; i < nparts; ++i) {
+      for (size_t l = 0; l < S2; ++l) h[l * stride + i] = partials[i * pw + l];
+      E += (int64_t)((uint64_t)partials[i * pw + S2] | ((uint64_t)partials[i * pw + S2 + 1] << 32));
+    }
     HIP_TRY(w->x.ensure(h.size() * 4));
+    HIP_TRY(w->p0.ensure(h.size() * 4));
+    HIP_TRY(w->p1.ensure(h.size() * 4));
     HIP_TRY(hipMemcpyAsync(w->x.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, wl.st));
-    const uint32_t* part;
-    size_t ps;
-    if ((rc = fold_partial_device(ctx, w, wl.st, *mc, w->x.as<uint32_t>(), stride, nparts, &part, &ps))) return rc;
-    // partials are already "prod * R^(1-c)": folding n of them gives prod * R^(1-k) as for rows
+    const uint32_t* cur = w->x.as<uint32_t>();
+    size_t n = nparts, cs = stride;
+    uint32_t* bufs[2] = {w->p0.as<uint32_t>(), w->p1.as<uint32_t>()};
+    int flip = 0;
+    while (n > 1) {
+      size_t ng = (n + 1) / 2, ns = round_up(ng, 64);
+      HIP_TRY(launch_fold_tail(mc->S2, cur, cs, n, mc->d2, mc->n0, bufs[flip], ns, ng, wl.st));
+      cur = bufs[flip];
+      flip ^= 1;
+      n = ng;
+      cs = ns;
+    }
     std::vector<uint32_t> res;
-    if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, k, &res))) return rc;
-    return emit_be(mc->value(res.data()), mod_bytes, out, out_cap, out_len);
+    if ((rc = finalize_device(ctx, w, wl.st, *mc, cur, cs, E, &res))) return rc;
+    return emit_be(mc->value2(res.data()), mod_bytes, out, out_cap, out_len);
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");
   }
@@ -720,8 +772,8 @@ int encrypt_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const
   HIP_TRY(hipMemcpyAsync(w->y.p, gr27.data(), gr27.size() * 4, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(w->y.as<uint32_t>() + gr27.size(), nbits_words.data(), nbits_words.size() * 4,
                          hipMemcpyHostToDevice, st));
-  HIP_TRY(launch_paillier_encrypt(S, d_rcol, rstride, d_m, count, mc.d, w->y.as<uint32_t>(),
-                                  w->y.as<uint32_t>() + gr27.size(), nbits, mc.n0, d_out, st));
+  HIP_TRY(launch_modexp(S, d_rcol, rstride, d_m, count, mc.d, w->y.as<uint32_t>(), w->y.as<uint32_t>() + gr27.size(),
+                        nbits, mc.n0, d_out, st));
   HIP_TRY(hipStreamSynchronize(st));  // host vectors above must outlive the async copies
   return DDS_OK;
 }
@@ -761,6 +813,44 @@ int dds_paillier_encrypt_batch(dds_ctx* ctx, const uint8_t* n_be, size_t n_bytes
     for (size_t i = 0; i < count; ++i) {
       for (int l = 0; l < S; ++l) limbs[l] = h[(size_t)l * stride + i];
       if (!bn::to_be(mc->value(limbs.data()), out + i * nsq_bytes, nsq_bytes))
+        return fail(DDS_E_RANGE, "result does not fit");
+    }
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_modexp_batch(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint8_t* exp_be, size_t exp_bytes,
+                     const uint8_t* bases_be, size_t width, size_t count, uint8_t* out) {
+  try {
+    if (!ctx || !exp_be || width == 0 || (count && (!bases_be || !out))) return fail(DDS_E_ARG, "bad arguments");
+    if (count == 0) return DDS_OK;
+    std::shared_ptr<ModConsts> mc;
+    int rc = get_mod(ctx, mod_be, mod_bytes, &mc);
+    if (rc) return rc;
+    bn::Limbs e = bn::from_be(exp_be, exp_bytes);
+    WorkerLease wl(ctx);
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    const int S = mc->S;
+    const size_t stride = round_up(count, 64);
+    HIP_TRY(w->x.ensure((size_t)S * stride * 4));
+    HIP_TRY(w->x2.ensure((size_t)S * stride * 4));
+    if ((rc = ingest(ctx, w, wl.st, *mc, bases_be, width, count, w->in, w->x.as<uint32_t>(), stride))) return rc;
+    std::vector<uint32_t> ew(e.begin(), e.end());
+    if (ew.empty()) ew.push_back(0);
+    HIP_TRY(w->y.ensure(ew.size() * 4));
+    HIP_TRY(hipMemcpyAsync(w->y.p, ew.data(), ew.size() * 4, hipMemcpyHostToDevice, wl.st));
+    HIP_TRY(launch_modexp(S, w->x.as<uint32_t>(), stride, nullptr, count, mc->d, nullptr, w->y.as<uint32_t>(),
+                          (int)bn::bit_length(e), mc->n0, w->x2.as<uint32_t>(), wl.st));
+    std::vector<uint32_t> h((size_t)S * stride);
+    HIP_TRY(hipMemcpyAsync(h.data(), w->x2.p, h.size() * 4, hipMemcpyDeviceToHost, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    std::vector<uint32_t> limbs(S);
+    for (size_t i = 0; i < count; ++i) {
+      for (int l = 0; l < S; ++l) limbs[l] = h[(size_t)l * stride + i];
+      if (!bn::to_be(mc->value(limbs.data()), out + i * mod_bytes, mod_bytes))
         return fail(DDS_E_RANGE, "result does not fit");
     }
     return DDS_OK;

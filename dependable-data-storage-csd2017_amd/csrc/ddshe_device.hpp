@@ -39,8 +39,8 @@ __device__ __forceinline__ uint32_t grp_bcast0(uint32_t x) {
   if constexpr (TPI == 1) return x;
   else if constexpr (TPI == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xA0, 0xF, 0xF, false);  // quad_perm [0,0,2,2]
   else if constexpr (TPI == 4) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x00, 0xF, 0xF, false);  // quad_perm [0,0,0,0]
-  else if constexpr (TPI == 8) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x18);                      // and_mask 0b11000
-  else { static_assert(TPI == 16, "TPI"); return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x10); }
+  else if constexpr (TPI == 8) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x18);  // and_mask 0b11000
+  else { static_assert(TPI == 16, "TPI"); return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150, 0xF, 0xF, false); }  // row_newbcast:0
 }
 // value of lane r+1 (caller masks the group's top lane)
 template <int TPI>
@@ -74,10 +74,19 @@ struct Mont {
   // One CIOS step with multiplier limb b: t = (t + a·b + m·N) / 2^W.
   __device__ __forceinline__ static void step(uint64_t (&t)[L], const uint32_t (&a)[L], const uint32_t (&n)[L],
                                               uint32_t b, uint32_t n0, bool top) {
-    // pass 1: t += a*b, in place (no 64-bit temporaries live across the pass)
+    // pass 1: t += a*b, in place (no 64-bit temporaries live across the pass). The
+    // quotient m depends only on limb 0, so it is issued first and its latency
+    // (mul_lo -> and -> DPP) hides under the remaining L-1 mads.
+#ifndef DDSHE_AB_M_LATE
+    t[0] = (uint64_t)a[0] * b + t[0];
+    const uint32_t m = grp_bcast0<TPI>(((uint32_t)t[0] * n0) & kMask);
+#pragma unroll
+    for (int l = 1; l < L; ++l) t[l] = (uint64_t)a[l] * b + t[l];
+#else
 #pragma unroll
     for (int l = 0; l < L; ++l) t[l] = (uint64_t)a[l] * b + t[l];
     const uint32_t m = grp_bcast0<TPI>(((uint32_t)t[0] * n0) & kMask);
+#endif
     // pass 2: t = (t + m*N) / 2^W, shifting down one limb in place
     const uint64_t u0 = (uint64_t)m * n[0] + t[0];
     const uint32_t lo0 = (uint32_t)u0 & kMask;  // == 0 on the group's lane 0
@@ -94,7 +103,9 @@ struct Mont {
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       const uint64_t v = t[l] + c;
-      a[l] = (uint32_t)v & kMask;
+      // early-clobber output: a[l] must not inherit the low half of the 64-bit pair v,
+      // otherwise a[] ends up on even registers only and wastes ~L VGPRs
+      asm volatile("v_and_b32 %0, %1, %2" : "=&v"(a[l]) : "v"((uint32_t)v), "v"(kMask));
       c = v >> kW;
     }
     uint32_t clo = grp_from_prev<TPI>((uint32_t)c & kMask);
@@ -110,6 +121,23 @@ struct Mont {
 #pragma unroll
     for (int l = 0; l < L; ++l) asm volatile("" : "+v"(t[l]));
   }
+  // opaque redefinition of the 32-bit operands once per Montgomery product: stops LICM
+  // from hoisting zext(a[l]) / zext(n[l]) out of the step loop as 64-bit values, which
+  // would pin every operand to an even register and waste ~2L VGPRs
+  __device__ __forceinline__ static void fence_ops(uint32_t (&a)[L], const uint32_t (&n)[L]) {
+#ifdef DDSHE_AB_NO_FENCE_OPS
+    return;
+#endif
+#pragma unroll
+    for (int l = 0; l < L; ++l) asm volatile("" : "+v"(a[l]));
+    if constexpr (TPI == 1) {  // N is wave-uniform: keep it in SGPRs (one SGPR operand per mad)
+#pragma unroll
+      for (int l = 0; l < L; ++l) asm volatile("" : "+s"(const_cast<uint32_t&>(n[l])));
+    } else {
+#pragma unroll
+      for (int l = 0; l < L; ++l) asm volatile("" : "+v"(const_cast<uint32_t&>(n[l])));
+    }
+  }
 
   // a <- MonPro(a, B), B = column `row` of the limb-transposed matrix X (limb i at
   // X[i*stride + row]; fully normalised, value < 2N). X and stride are wave-uniform:
@@ -122,7 +150,11 @@ struct Mont {
     uint64_t t[L];
 #pragma unroll
     for (int l = 0; l < L; ++l) t[l] = 0;
+#ifdef DDSHE_AB_PF
+    constexpr int PF = DDSHE_AB_PF;
+#else
     constexpr int PF = (S % 4 == 0) ? 4 : 2;  // limbs per unrolled block = loads in flight
+#endif
     static_assert(S % PF == 0, "S % PF");
     const uint32_t voff = row * 4u;
     const uint32_t sstride = (uint32_t)stride * 4u;  // host guarantees PF*stride*4 < 2^32
@@ -138,6 +170,7 @@ struct Mont {
     }
 #pragma unroll 1
     for (int i = 0; i < S - PF; i += PF) {
+      fence_ops(a, n);
       const auto rs = block_rsrc(i + PF);
       uint32_t bn[PF];
 #pragma unroll
@@ -158,19 +191,35 @@ struct Mont {
     settle(t, a, bottom);
   }
 
-  // a <- MonPro(a, B) with B held by the group in registers (same layout as a).
-  __device__ __forceinline__ static void mul_reg(uint32_t (&a)[L], const uint32_t (&bv)[L], const uint32_t (&n)[L],
-                                                 uint32_t n0, int r, bool top, bool bottom) {
+  // a <- MonPro(a, B), B in LDS (limb i at lb[i], fully normalised, value < 2N). The TPI
+  // lanes of a group read the same address (broadcast); group arrays sit S dwords apart.
+  __device__ __forceinline__ static void mul_lds(uint32_t (&a)[L], const uint32_t (&n)[L], const uint32_t* lb,
+                                                 uint32_t n0, bool top, bool bottom) {
     uint64_t t[L];
 #pragma unroll
     for (int l = 0; l < L; ++l) t[l] = 0;
-    for (int src = 0; src < TPI; ++src) {
+    constexpr int PF = (S % 4 == 0) ? 4 : 2;
+    uint32_t bq[PF];
 #pragma unroll
-      for (int l = 0; l < L; ++l) {
-        // limb src*L + l of B lives in lane `src` of the group
-        const uint32_t b = group_read(bv[l], src, r);
-        step(t, a, n, b, n0, top);
+    for (int q = 0; q < PF; ++q) bq[q] = lb[q];
+#pragma unroll 1
+    for (int i = 0; i < S - PF; i += PF) {
+      fence_ops(a, n);
+      uint32_t bn[PF];
+#pragma unroll
+      for (int q = 0; q < PF; ++q) bn[q] = lb[i + PF + q];
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        step(t, a, n, bq[q], n0, top);
+        fence_t(t);
       }
+#pragma unroll
+      for (int q = 0; q < PF; ++q) bq[q] = bn[q];
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      step(t, a, n, bq[q], n0, top);
+      fence_t(t);
     }
     settle(t, a, bottom);
   }

@@ -9,7 +9,7 @@
 //   MultAll fold  dds/http/DDSRestServer.scala:491-539  -> k_fold + k_finalize
 //   Sum / Mult    dds/http/DDSRestServer.scala:355-395, 447-490 -> k_pairs
 //   Search{Gt,GtEq,Lt,LtEq} DDSRestServer.scala:682-830 -> k_ope_count / k_ope_scatter
-//   HomoAdd.encrypt  utils/SJHomoLibProvider.scala:58 -> k_paillier_encrypt
+//   HomoAdd.encrypt  utils/SJHomoLibProvider.scala:58 -> k_modexp (also HomoMult.encrypt, :59)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -140,7 +140,7 @@ __global__ void k_ingest_be(const uint8_t* __restrict__ in, size_t width, size_t
 
 // rows >= 2N: x <- MonPro(MonPro(x, R^2 mod N), 1) = x mod N
 template <int S, int TPI, int W>
-__global__ void __launch_bounds__(256) k_reduce_rows(uint32_t* __restrict__ X, size_t stride, size_t count,
+__global__ void __launch_bounds__(256, 2) k_reduce_rows(uint32_t* __restrict__ X, size_t stride, size_t count,
                                                      const uint32_t* __restrict__ consts, uint32_t n0) {
   using G = Grp<S, TPI, W>;
   using M = Mont<S, TPI, W>;
@@ -169,9 +169,9 @@ __global__ void __launch_bounds__(256) k_reduce_rows(uint32_t* __restrict__ X, s
 // A group that folded c rows holds prod * R^(1-c); an empty group holds R mod N.
 // ------------------------------------------------------------------------------
 template <int S, int TPI, int W>
-__global__ void __launch_bounds__(256) k_fold(const uint32_t* __restrict__ X, size_t xstride, size_t count,
+__global__ void __launch_bounds__(256, 2) k_fold(const uint32_t* __restrict__ X, size_t xstride, size_t count,
                                               const uint32_t* __restrict__ consts, uint32_t n0,
-                                              uint32_t* __restrict__ P, size_t pstride, size_t ngroups) {
+                                              uint32_t* __restrict__ P, size_t pstride, size_t ngroups, int s_out) {
   using G = Grp<S, TPI, W>;
   using M = Mont<S, TPI, W>;
   constexpr int L = G::L;
@@ -190,6 +190,8 @@ __global__ void __launch_bounds__(256) k_fold(const uint32_t* __restrict__ X, si
   for (; row < count; row += ngroups) M::mul_col(a, n, X, xstride, (uint32_t)row, n0, g.top, g.bottom);
   M::normalize(a, g.bottom);
   g.store_col(a, P, pstride, grp);
+  // zero-extend to the tail shape's limb count (value < 2N never reaches these limbs)
+  for (int j = S + g.r; j < s_out; j += TPI) P[(size_t)j * pstride + grp] = 0u;
 }
 
 // result = canon(MonPro(P[0], Y)), Y = R^k mod N; writes S rW limbs to out
@@ -213,7 +215,7 @@ __global__ void __launch_bounds__(64) k_finalize(const uint32_t* __restrict__ P,
 
 // out[i] = A[i]*B[i] mod N (canonical), rW columns in and out
 template <int S, int TPI, int W>
-__global__ void __launch_bounds__(256) k_pairs(const uint32_t* __restrict__ A, const uint32_t* __restrict__ B,
+__global__ void __launch_bounds__(256, 2) k_pairs(const uint32_t* __restrict__ A, const uint32_t* __restrict__ B,
                                                size_t stride, size_t count, const uint32_t* __restrict__ consts,
                                                uint32_t n0, uint32_t* __restrict__ O) {
   using G = Grp<S, TPI, W>;
@@ -232,71 +234,71 @@ __global__ void __launch_bounds__(256) k_pairs(const uint32_t* __restrict__ A, c
 }
 
 // ------------------------------------------------------------------------------
-// Montgomery exponentiation helpers (register operands via ds_bpermute)
+// batched modular exponentiation: c_i = g^m_i * r_i^E mod N
+//   Paillier encrypt (HomoAdd.encrypt, SJHomoLibProvider.scala:58): N = n^2, E = n
+//   RSA encrypt / generic x^E (HomoMult.encrypt, :59): g^m term disabled (m == nullptr)
+// Left-to-right binary ladder over the uniform exponent E; every operand of a
+// Montgomery product is staged in the group's LDS slot (2 x S dwords), so the
+// registers hold only acc, N and the 64-bit accumulators (no spills).
+// consts: N, Rmod (=1 in Montgomery form), R2, One; gR = g*R mod N (uniform, global).
 // ------------------------------------------------------------------------------
-// acc <- acc^e * acc_in... : left-to-right binary over the bits of a uniform exponent
-template <int S, int TPI, int W, int L>
-__device__ __forceinline__ void mont_pow_uniform(uint32_t (&acc)[L], const uint32_t (&x)[L], const uint32_t (&n)[L],
-                                                 uint32_t n0, const uint32_t* __restrict__ ebits, int nbits,
-                                                 const Grp<S, TPI, W>& g) {
-  using M = Mont<S, TPI, W>;
-  for (int i = nbits - 1; i >= 0; --i) {
-    M::normalize(acc, g.bottom);
-    uint32_t sq[M::L];
+template <int S, int TPI, int W>
+__device__ __forceinline__ void store_lds(uint32_t* dst, const uint32_t (&a)[S / TPI], int r) {
 #pragma unroll
-    for (int l = 0; l < M::L; ++l) sq[l] = acc[l];
-    M::mul_reg(acc, sq, n, n0, g.r, g.top, g.bottom);
-    if ((ebits[i >> 5] >> (i & 31)) & 1u) M::mul_reg(acc, x, n, n0, g.r, g.top, g.bottom);
-  }
+  for (int l = 0; l < S / TPI; ++l) dst[r * (S / TPI) + l] = a[l];
 }
 
-// c_i = g^m_i * r_i^n mod N (N = n^2). Inputs r in rW column (values < N), m per row.
-// consts: N, gR (g*R mod N, Montgomery form), Rmod (1 in Montgomery form), R2, One
 template <int S, int TPI, int W>
-__global__ void __launch_bounds__(256) k_paillier_encrypt(const uint32_t* __restrict__ Rcol, size_t stride,
-                                                          const uint32_t* __restrict__ m, size_t count,
-                                                          const uint32_t* __restrict__ consts,
-                                                          const uint32_t* __restrict__ gR,
-                                                          const uint32_t* __restrict__ nbits_words, int nbits,
-                                                          uint32_t n0, uint32_t* __restrict__ O) {
+__global__ void __launch_bounds__(256, 2) k_modexp(const uint32_t* __restrict__ Rcol, size_t stride,
+                                                const uint32_t* __restrict__ m, size_t count,
+                                                const uint32_t* __restrict__ consts, const uint32_t* __restrict__ gR,
+                                                const uint32_t* __restrict__ ebits, int nbits, uint32_t n0,
+                                                uint32_t* __restrict__ O) {
   using G = Grp<S, TPI, W>;
   using M = Mont<S, TPI, W>;
   constexpr int L = G::L;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   G g;
   const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
   if (grp >= count) return;
-  uint32_t n[L], x[L], acc[L], gx[L], acc2[L];
+  uint32_t* sq = lds + (size_t)(threadIdx.x / TPI) * 2 * S;  // group-private operand slot
+  uint32_t* xs = sq + S;
+  uint32_t n[L], acc[L];
   g.load_vec(n, consts + kConstN * S);
-  g.load_col(x, Rcol, stride, grp);
-  M::mul_col(x, n, consts + kConstR2 * S, 1, 0, n0, g.top, g.bottom);  // r*R
-  M::normalize(x, g.bottom);
-  g.load_vec(acc, consts + kConstRmod * S);                         // 1*R
-  mont_pow_uniform<S, TPI, W, L>(acc, x, n, n0, nbits_words, nbits, g);   // r^n * R
-  // g^m with a per-row exponent: multiply-always with a select to stay uniform
-  g.load_vec(gx, gR);
-  g.load_vec(acc2, consts + kConstRmod * S);
-  const uint32_t mi = m[grp];
-  const uint32_t mbits = mi ? 32u - (uint32_t)__builtin_clz(mi) : 0u;
-  // wave-uniform trip count (max over the wave's groups)
-  uint32_t wb = mbits;
-  for (int off = 32; off >= 1; off >>= 1) wb = max(wb, (uint32_t)__shfl_xor((int)wb, off));
-  uint32_t one[L];
-  g.load_vec(one, consts + kConstRmod * S);
-  for (int i = (int)wb - 1; i >= 0; --i) {
-    M::normalize(acc2, g.bottom);
-    uint32_t sq[L];
-#pragma unroll
-    for (int l = 0; l < L; ++l) sq[l] = acc2[l];
-    M::mul_reg(acc2, sq, n, n0, g.r, g.top, g.bottom);
-    uint32_t sel[L];
-    const bool bit = (mi >> i) & 1u;
-#pragma unroll
-    for (int l = 0; l < L; ++l) sel[l] = bit ? gx[l] : one[l];
-    M::mul_reg(acc2, sel, n, n0, g.r, g.top, g.bottom);
+  // x = r*R (Montgomery form), kept in LDS for the ladder's multiplies
+  g.load_col(acc, Rcol, stride, grp);
+  M::mul_col(acc, n, consts + kConstR2 * S, 1, 0, n0, g.top, g.bottom);
+  M::normalize(acc, g.bottom);
+  store_lds<S, TPI, W>(xs, acc, g.r);
+  g.load_vec(acc, consts + kConstRmod * S);  // 1*R
+  for (int i = nbits - 1; i >= 0; --i) {
+    M::normalize(acc, g.bottom);
+    store_lds<S, TPI, W>(sq, acc, g.r);
+    M::mul_lds(acc, n, sq, n0, g.top, g.bottom);  // square
+    if ((ebits[i >> 5] >> (i & 31)) & 1u) M::mul_lds(acc, n, xs, n0, g.top, g.bottom);
   }
-  M::normalize(acc2, g.bottom);
-  M::mul_reg(acc, acc2, n, n0, g.r, g.top, g.bottom);               // g^m r^n R
-  M::mul_col(acc, n, consts + kConstOne * S, 1, 0, n0, g.top, g.bottom);  // g^m r^n
+  if (m != nullptr) {
+    // g^m_i: per-row exponent; the ladder length is the wave's max bit length so the
+    // branch stays uniform, the multiplier is g*R or 1*R selected per group
+    const uint32_t mi = m[grp];
+    uint32_t wb = mi ? 32u - (uint32_t)__builtin_clz(mi) : 0u;
+    for (int off = 32; off >= 1; off >>= 1) wb = max(wb, (uint32_t)__shfl_xor((int)wb, off));
+    M::normalize(acc, g.bottom);
+    store_lds<S, TPI, W>(xs, acc, g.r);  // park r^E*R in xs; acc is reused for g^m
+    g.load_vec(acc, consts + kConstRmod * S);
+    for (int i = (int)wb - 1; i >= 0; --i) {
+      M::normalize(acc, g.bottom);
+      store_lds<S, TPI, W>(sq, acc, g.r);
+      M::mul_lds(acc, n, sq, n0, g.top, g.bottom);
+      const uint32_t* sel = ((mi >> i) & 1u) ? gR : consts + kConstRmod * S;
+#pragma unroll
+      for (int l = 0; l < L; ++l) sq[g.r * L + l] = sel[g.r * L + l];
+      M::mul_lds(acc, n, sq, n0, g.top, g.bottom);
+    }
+    // acc = (g^m R) * (r^E R) * R^-1
+    M::mul_lds(acc, n, xs, n0, g.top, g.bottom);
+  }
+  M::mul_col(acc, n, consts + kConstOne * S, 1, 0, n0, g.top, g.bottom);  // leave Montgomery form
   g.canon(acc, n);
   g.store_col(acc, O, stride, grp);
 }
@@ -314,7 +316,7 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 }
 
 template <int S, int TPI, int W>
-__global__ void __launch_bounds__(256) k_synth_rows(const uint32_t* __restrict__ T, size_t tstride, uint32_t tcount,
+__global__ void __launch_bounds__(256, 2) k_synth_rows(const uint32_t* __restrict__ T, size_t tstride, uint32_t tcount,
                                                     const uint32_t* __restrict__ P, size_t pstride, uint32_t pcount,
                                                     uint64_t seed, uint64_t row0, size_t count,
                                                     const uint32_t* __restrict__ consts, uint32_t n0,
@@ -484,18 +486,35 @@ __global__ void __launch_bounds__(256) k_plain_sum_reduce(const uint64_t* __rest
 
 #define DDSHE_SWITCH(S_RT, ...)                      \
   switch (S_RT) {                                    \
-    DDSHE_DISPATCH(40, 1, 28, __VA_ARGS__)           \
+    DDSHE_DISPATCH(40, 2, 28, __VA_ARGS__)           \
     DDSHE_DISPATCH(74, 2, 28, __VA_ARGS__)           \
     DDSHE_DISPATCH(148, 4, 28, __VA_ARGS__)          \
     DDSHE_DISPATCH(232, 8, 27, __VA_ARGS__)          \
     default: return hipErrorInvalidValue;            \
   }
 
-static const Shape kShapes[] = {{40, 1, 28}, {74, 2, 28}, {148, 4, 28}, {232, 8, 27}};
+static const Shape kShapes[] = {{40, 2, 28}, {74, 2, 28}, {148, 4, 28}, {232, 8, 27}};
+// latency-oriented shapes for the reduction tree / finalize: 16 lanes per bignum
+static const Shape kTail[] = {{48, 16, 28}, {80, 16, 28}, {160, 16, 28}, {240, 16, 27}};
+
+#define DDSHE_TAIL_SWITCH(S_RT, ...)                 \
+  switch (S_RT) {                                    \
+    DDSHE_DISPATCH(48, 16, 28, __VA_ARGS__)          \
+    DDSHE_DISPATCH(80, 16, 28, __VA_ARGS__)          \
+    DDSHE_DISPATCH(160, 16, 28, __VA_ARGS__)         \
+    DDSHE_DISPATCH(240, 16, 27, __VA_ARGS__)         \
+    default: return hipErrorInvalidValue;            \
+  }
 
 Shape pick_shape(size_t mod_bits) {
   for (const Shape& s : kShapes)
     if ((size_t)s.W * s.S >= mod_bits + 2) return s;
+  return Shape{0, 0, 0};
+}
+
+Shape tail_shape(const Shape& main) {
+  for (int i = 0; i < 4; ++i)
+    if (kShapes[i].S == main.S) return kTail[i];
   return Shape{0, 0, 0};
 }
 
@@ -520,17 +539,27 @@ hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, c
 }
 
 hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts, uint32_t n0,
-                       uint32_t* P, size_t pstride, size_t ngroups, hipStream_t st) {
+                       uint32_t* P, size_t pstride, size_t ngroups, int s_out, hipStream_t st) {
   DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X, xstride,
-                                     count, consts, n0, P, pstride, ngroups));
+                                     count, consts, n0, P, pstride, ngroups, s_out < S ? S : s_out));
   return hipGetLastError();
 }
 
-hipError_t launch_finalize(int S, const uint32_t* P, size_t pstride, const uint32_t* consts, const uint32_t* Y,
-                           uint32_t n0, uint32_t* out, hipStream_t st) {
-  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_finalize<S, TPI, W>), dim3(1), dim3(64), 0, st, P, pstride, consts, Y, n0, out));
+hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
+                            uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups, hipStream_t st) {
+  DDSHE_TAIL_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X,
+                                          xstride, count, consts, n0, P, pstride, ngroups, S));
   return hipGetLastError();
 }
+
+hipError_t launch_finalize_tail(int S, const uint32_t* P, size_t pstride, const uint32_t* consts, const uint32_t* Y,
+                                uint32_t n0, uint32_t* out, hipStream_t st) {
+  DDSHE_TAIL_SWITCH(S, hipLaunchKernelGGL((k_finalize<S, TPI, W>), dim3(1), dim3(64), 0, st, P, pstride, consts, Y, n0,
+                                          out));
+  return hipGetLastError();
+}
+
+int tail_tpi() { return 16; }
 
 hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stride, size_t count,
                         const uint32_t* consts, uint32_t n0, uint32_t* O, hipStream_t st) {
@@ -540,12 +569,13 @@ hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stri
   return hipGetLastError();
 }
 
-hipError_t launch_paillier_encrypt(int S, const uint32_t* Rcol, size_t stride, const uint32_t* m, size_t count,
-                                   const uint32_t* consts, const uint32_t* gR, const uint32_t* nbits_words, int nbits,
-                                   uint32_t n0, uint32_t* O, hipStream_t st) {
+hipError_t launch_modexp(int S, const uint32_t* Rcol, size_t stride, const uint32_t* m, size_t count,
+                         const uint32_t* consts, const uint32_t* gR, const uint32_t* ebits, int nbits, uint32_t n0,
+                         uint32_t* O, hipStream_t st) {
   if (count == 0) return hipSuccess;
-  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_paillier_encrypt<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), 0, st,
-                                     Rcol, stride, m, count, consts, gR, nbits_words, nbits, n0, O));
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_modexp<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256),
+                                     (256 / TPI) * 2 * S * 4, st, Rcol, stride, m, count, consts, gR, ebits, nbits,
+                                     n0, O));
   return hipGetLastError();
 }
 

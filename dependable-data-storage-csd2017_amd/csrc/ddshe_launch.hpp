@@ -15,21 +15,27 @@ struct Shape {
   int W;    // radix bits
 };
 Shape pick_shape(size_t mod_bits);  // S == 0: unsupported
+Shape tail_shape(const Shape& main);  // TPI = 16 shape (more limbs, same W) for tree levels + finalize
 size_t max_modulus_bits();
 
 hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, int W, const uint32_t* n2x,
                             uint32_t* X, size_t stride, uint32_t* flags, hipStream_t st);
 hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, const uint32_t* consts, uint32_t n0,
                               hipStream_t st);
+// main fold level (throughput shape); partial rows are zero-extended to s_out limbs
 hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts, uint32_t n0,
-                       uint32_t* P, size_t pstride, size_t ngroups, hipStream_t st);
-hipError_t launch_finalize(int S, const uint32_t* P, size_t pstride, const uint32_t* consts, const uint32_t* Y,
-                           uint32_t n0, uint32_t* out, hipStream_t st);
+                       uint32_t* P, size_t pstride, size_t ngroups, int s_out, hipStream_t st);
+// tree levels / finalize in the tail shape (S = tail limb count, consts of the tail shape)
+hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
+                            uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups, hipStream_t st);
+hipError_t launch_finalize_tail(int S, const uint32_t* P, size_t pstride, const uint32_t* consts, const uint32_t* Y,
+                                uint32_t n0, uint32_t* out, hipStream_t st);
 hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stride, size_t count,
                         const uint32_t* consts, uint32_t n0, uint32_t* O, hipStream_t st);
-hipError_t launch_paillier_encrypt(int S, const uint32_t* Rcol, size_t stride, const uint32_t* m, size_t count,
-                                   const uint32_t* consts, const uint32_t* gR, const uint32_t* nbits_words, int nbits,
-                                   uint32_t n0, uint32_t* O, hipStream_t st);
+// c_i = g^m_i * r_i^E mod N (m == nullptr: r_i^E); gR = g*R mod N in rW limbs
+hipError_t launch_modexp(int S, const uint32_t* Rcol, size_t stride, const uint32_t* m, size_t count,
+                         const uint32_t* consts, const uint32_t* gR, const uint32_t* ebits, int nbits, uint32_t n0,
+                         uint32_t* O, hipStream_t st);
 hipError_t launch_synth_rows(int S, const uint32_t* T, size_t tstride, uint32_t tcount, const uint32_t* P,
                              size_t pstride, uint32_t pcount, uint64_t seed, uint64_t row0, size_t count,
                              const uint32_t* consts, uint32_t n0, uint32_t* X, size_t xstride, hipStream_t st);

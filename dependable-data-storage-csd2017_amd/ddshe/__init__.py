@@ -34,7 +34,8 @@ EXPORTS = [
     "dds_modmul_fold", "dds_paillier_sum", "dds_rsa_product", "dds_modmul_pairs", "dds_bigint_sum",
     "dds_col_create", "dds_col_destroy", "dds_col_append", "dds_col_count", "dds_col_read", "dds_col_fold",
     "dds_col_fold_partial", "dds_col_partial_words", "dds_combine_partials", "dds_col_fill_paillier_synth",
-    "dds_ope_filter", "dds_ope_filter_device", "dds_paillier_encrypt_batch", "dds_sum_all_dec", "dds_mult_all_dec",
+    "dds_ope_filter", "dds_ope_filter_device", "dds_paillier_encrypt_batch", "dds_modexp_batch", "dds_sum_all_dec",
+    "dds_mult_all_dec",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -79,6 +80,7 @@ _sig("dds_ope_filter", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int
 _sig("dds_ope_filter_device", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int64, C.c_int, C.c_void_p, _szp)
 _sig("dds_paillier_encrypt_batch", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, C.POINTER(C.c_uint32),
      C.c_char_p, _sz, _sz, _u8p, _sz)
+_sig("dds_modexp_batch", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, C.c_char_p, _sz, _sz, _u8p)
 for _n in ("dds_sum_all_dec", "dds_mult_all_dec"):
     _sig(_n, C.c_int, C.c_void_p, C.POINTER(C.c_char_p), _sz, C.c_char_p, C.c_char_p, _sz, _szp)
 
@@ -235,6 +237,18 @@ class Engine:
                                                ints_to_be(rs, rw), rw, len(rs), out, nb), "dds_paillier_encrypt_batch")
         raw = bytes(out)
         return [int.from_bytes(raw[i * nb:(i + 1) * nb], "big") for i in range(len(rs))]
+
+    def modexp_batch(self, modulus: int, exponent: int, bases) -> list[int]:
+        """out[i] = bases[i]^exponent mod modulus (HomoMult.encrypt for an RSA key)."""
+        bases = [int(x) for x in bases]
+        mb = nbytes(modulus)
+        width = max([mb] + [nbytes(x) for x in bases])
+        out = (C.c_uint8 * (mb * max(1, len(bases))))()
+        _check(_lib.dds_modexp_batch(self._h, int_to_be(modulus, mb), mb, int_to_be(exponent, nbytes(exponent)),
+                                     nbytes(exponent), ints_to_be(bases, width), width, len(bases), out),
+               "dds_modexp_batch")
+        raw = bytes(out)
+        return [int.from_bytes(raw[i * mb:(i + 1) * mb], "big") for i in range(len(bases))]
 
     def column(self, modulus: int, capacity: int) -> "Column":
         return Column(self, modulus, capacity)

@@ -143,6 +143,12 @@ int dds_paillier_encrypt_batch(dds_ctx* ctx, const uint8_t* n_be, size_t n_bytes
                                const uint32_t* m, const uint8_t* r_be, size_t r_width, size_t count, uint8_t* out,
                                size_t nsq_bytes);
 
+/* Batched modular exponentiation out[i] = base[i]^exp mod modulus (mod_bytes each):
+ * HomoMult.encrypt(pk, m) = m^e mod n (SJHomoLibProvider.scala:59) and decrypt-side
+ * checks. Bases are validated like fold operands. */
+int dds_modexp_batch(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint8_t* exp_be, size_t exp_bytes,
+                     const uint8_t* bases_be, size_t width, size_t count, uint8_t* out);
+
 /* ---- route-level entry points on decimal strings (what the Scala route holds) ----
  * values: count NUL-terminated decimal strings (contents(position) of the rows that
  * passed the guard). modulus_dec NULL selects the plain add / multiply branch.

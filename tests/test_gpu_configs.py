@@ -1,0 +1,81 @@
+"""GPU parity for the BASELINE.json configurations (the non-headline ones are parity
+cases, not bench lines). Each check is bit-exact against the oracle or a
+size-independent property (decrypt of the fold)."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import homo
+
+pytestmark = pytest.mark.gpu
+
+
+def test_config1_paillier1024_10k_vs_c_restatement(eng, keys):
+    """Config 1: Paillier HomoAdd sum over 10k encrypted ints, 1024-bit key; the reference
+    BigInteger path restated in C (oracle/csrc/fold_ref.c) is the comparison."""
+    from oracle import cref
+    k = keys["paillier1024_seed1"]
+    count = 10_000
+    col = eng.column(k["nsquare"], count)
+    col.fill_paillier_synth(k["n"], k["g"], seed=1, row0=0, count=count, pool=128)
+    cs = col.read(0, count)
+    got = eng.paillier_sum(k["nsquare"], cs)          # host-buffer path (ingest + fold)
+    assert got == cref.fold(k["nsquare"], cs)
+    assert col.fold() == got                           # device-resident path
+    import ddshe
+    assert homo.paillier_decrypt(got, k) == int(ddshe.synth_plaintexts(1, 0, count).astype(np.int64).sum()) % k["n"]
+
+
+def test_config3_rsa2048_product_and_ope_filter(eng, keys):
+    """Config 3: RSA HomoMult product + OPE range filter, 2048-bit key (scaled to 200k rows
+    for the product; the filter runs at the full 10M rows)."""
+    k = keys["rsa2048_seed3"]
+    n = k["n"]
+    rng = np.random.default_rng(3)
+    count = 200_000
+    ms = rng.integers(1, 10_000, size=count)
+    cs = eng.modexp_batch(n, k["e"], ms.tolist())      # HomoMult.encrypt on the GPU
+    for i in (0, 1, count - 1):
+        assert cs[i] == homo.rsa_encrypt(int(ms[i]), k)
+    col = eng.column(n, count)
+    col.append(cs)
+    prod = col.fold()
+    exp = 1
+    for m in ms.tolist():
+        exp = exp * m % n
+    assert homo.rsa_decrypt(prod, k) == exp
+    assert col.fold(0, 5000) == homo.modmul_fold(cs[:5000], n)
+    # OPE: seeded strictly increasing map of m (order preserving), bound at the median
+    rows = 10_000_000
+    m_all = rng.integers(0, 10_000, size=rows)
+    ope_map = np.cumsum(rng.integers(1, 1 << 40, size=10_000)).astype(np.int64) - (1 << 50)
+    col64 = ope_map[m_all]
+    valid = np.ones(rows, dtype=np.uint8)
+    bound = int(np.sort(col64)[rows // 2])
+    for op, f in (("gt", np.greater), ("ge", np.greater_equal), ("lt", np.less), ("le", np.less_equal)):
+        got = eng.ope_filter(col64, valid, bound, op)
+        assert np.array_equal(got, np.nonzero(f(col64, bound))[0].astype(np.uint32)), op
+
+
+def test_config4_paillier3072_encrypt_then_sum(eng, keys):
+    """Config 4: batched Paillier encrypt (g^m r^n mod n^2) + sum, 3072-bit key (6144-bit n^2),
+    scaled to 512 rows per test run; caller-supplied r for bit-exactness."""
+    k = keys["paillier3072_seed4"]
+    rng = random.Random(4)
+    ms = [rng.randrange(10_000) for _ in range(512)]
+    rs = [rng.randrange(1, k["n"]) for _ in ms]
+    cs = eng.paillier_encrypt_batch(k["n"], k["g"], ms, rs)
+    for i in (0, 255, 511):
+        assert cs[i] == homo.paillier_encrypt(ms[i], rs[i], k)
+    s = eng.paillier_sum(k["nsquare"], cs)
+    assert s == homo.modmul_fold(cs, k["nsquare"])
+    assert homo.paillier_decrypt(s, k) == sum(ms) % k["n"]
+
+
+def test_modexp_edge_exponents(eng, keys):
+    n = keys["rsa1024_committed"]["n"]
+    xs = [0, 1, 2, n - 1, 12345]
+    assert eng.modexp_batch(n, 0, xs) == [1 % n] * len(xs)
+    assert eng.modexp_batch(n, 1, xs) == [x % n for x in xs]
+    assert eng.modexp_batch(n, 65537, xs) == [pow(x, 65537, n) for x in xs]

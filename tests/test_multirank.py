@@ -1,7 +1,9 @@
 """World-size-2 gloo test (CPU) of the multi-GPU fold orchestration: row sharding,
 the all-gather of per-rank partials and the partial algebra used by
-dds_combine_partials. Each rank's partial is computed with the oracle's Montgomery
-restatement (radix 2^27, R = 2^(27*S)), exactly the value dds_col_fold_partial returns."""
+dds_combine_partials. Each rank's partial is restated from the engine's definition
+(dds_col_fold_partial): S2 = 160 radix-2^28 limbs holding prod * 2^E plus the signed
+exponent E in two words, where a fold with G first-level groups gives
+E = 28*148*(G - rows) - 28*160*(G - 1)."""
 import os
 import random
 
@@ -10,24 +12,47 @@ import torch.multiprocessing as mp
 
 from oracle import homo
 
-S = 152  # r27 limbs of a 4096-bit modulus
-R = 1 << (27 * S)
+W, S, S2 = 28, 148, 160  # throughput / tail limb counts for a 4095-bit modulus
+WS, WS2 = W * S, W * S2
 
 
-def r27(x):
-    return [(x >> (27 * i)) & ((1 << 27) - 1) for i in range(S)]
+def limbs(x):
+    return [(x >> (W * i)) & ((1 << W) - 1) for i in range(S2)]
 
 
-def from_r27(ws):
-    return sum(int(w) << (27 * i) for i, w in enumerate(ws))
+def from_limbs(ws):
+    return sum(int(w) << (W * i) for i, w in enumerate(ws[:S2]))
 
 
-def partial(xs, N):
-    Rinv = pow(R, -1, N)
-    v = R % N
+def pow2(e, N):
+    return pow(2, e, N) if e >= 0 else pow((N + 1) // 2, -e, N)
+
+
+def partial(xs, N, G):
+    """What dds_col_fold_partial returns for rows xs folded by G first-level groups."""
+    import numpy as np
+    E = WS * (G - len(xs)) - WS2 * (G - 1)
+    prod = 1
     for x in xs:
-        v = v * x * Rinv % N
-    return v
+        prod = prod * x % N
+    v = prod * pow2(E, N) % N
+    words = limbs(v) + [E & 0xFFFFFFFF, (E >> 32) & 0xFFFFFFFF]
+    return np.array(words, dtype=np.uint32)
+
+
+def combine(parts, N):
+    """dds_combine_partials: tail-shape tree over the partials, then finalize."""
+    n = len(parts)
+    E = -WS2 * (n - 1)
+    acc = None
+    for p in parts:
+        e = int(p[S2]) | (int(p[S2 + 1]) << 32)
+        if e >= 1 << 63:
+            e -= 1 << 64
+        E += e
+        v = from_limbs(p)
+        acc = v if acc is None else acc * v * pow2(-WS2, N) % N
+    return acc * pow2(WS2 - E, N) * pow2(-WS2, N) % N
 
 
 def _worker(rank, world, port, N, xs, out_q):
@@ -38,16 +63,10 @@ def _worker(rank, world, port, N, xs, out_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import ddshe.dist as dd
     row0, cnt = dd.shard_range(len(xs), world, rank)
-    v = partial(xs[row0:row0 + cnt], N)
-    parts, rows = dd.gather_partials(np.array(r27(v), dtype=np.uint32), cnt)
+    part = partial(xs[row0:row0 + cnt], N, G=max(1, cnt // 2) if rank == 0 else 3)
+    parts, rows = dd.gather_partials(part, cnt)
     if rank == 0:
-        # dds_combine_partials: fold the partials like rows, then multiply by R^k
-        Rinv = pow(R, -1, N)
-        acc = from_r27(parts[0])
-        for p in parts[1:]:
-            acc = acc * from_r27(p) * Rinv % N
-        k = int(rows.sum())
-        out_q.put((acc * pow(R, k, N) * Rinv % N, k))
+        out_q.put((combine(list(parts), N), int(rows.sum())))
     dist.barrier()
     dist.destroy_process_group()
 
