@@ -577,6 +577,64 @@ int dds_bigint_sum(dds_ctx* ctx, const uint8_t* ops, size_t width, size_t count,
   }
 }
 
+int dds_bigint_product(dds_ctx* ctx, const uint8_t* ops, size_t width, size_t count, uint8_t* out, size_t out_cap,
+                       size_t* out_len) {
+  try {
+    if (!ctx || width == 0 || (count && !ops)) return fail(DDS_E_ARG, "bad arguments");
+    if (count == 0) return fail(DDS_E_EMPTY, "no operand");
+    WorkerLease wl(ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    // boundary format: big-endian bytes -> radix-2^16 limbs (one per u32 word), row-major
+    size_t len = (width + 1) / 2;
+    std::vector<uint32_t> h(count * len, 0);
+    for (size_t r = 0; r < count; ++r)
+      for (size_t i = 0; i < width; ++i) {
+        const size_t bit = 8 * (width - 1 - i);
+        h[r * len + bit / 16] |= (uint32_t)ops[r * width + i] << (bit % 16);
+      }
+    HIP_TRY(w->x.ensure(h.size() * 4));
+    HIP_TRY(hipMemcpyAsync(w->x.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, wl.st));
+    HIP_TRY(w->flags.ensure(16));
+    uint32_t* cur = w->x.as<uint32_t>();
+    size_t n = count;
+    while (n > 1) {  // one tree level: n rows of len limbs -> ceil(n/2) rows of 2 len limbs
+      const size_t pairs = (n + 1) / 2, outlen = 2 * len;
+      HIP_TRY(w->misc.ensure(pairs * outlen * 8));
+      HIP_TRY(w->x2.ensure(pairs * outlen * 4));
+      HIP_TRY(w->p0.ensure(pairs * outlen * 4));
+      HIP_TRY(launch_bigmul_level(cur, n, len, w->misc.as<uint64_t>(), w->x2.as<uint32_t>(), wl.st));
+      uint32_t* v = w->x2.as<uint32_t>();
+      uint32_t* u = w->p0.as<uint32_t>();
+      for (;;) {  // carry passes until every limb is < 2^16 (ripples are rare and short)
+        HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, wl.st));
+        HIP_TRY(launch_bigmul_carry(v, pairs, outlen, u, w->flags.as<uint32_t>(), wl.st));
+        uint32_t flag = 0;
+        HIP_TRY(hipMemcpyAsync(&flag, w->flags.p, 4, hipMemcpyDeviceToHost, wl.st));
+        HIP_TRY(hipStreamSynchronize(wl.st));
+        std::swap(u, v);
+        if (!flag) break;
+      }
+      // v holds the normalised level; move it to the level buffer
+      HIP_TRY(w->x.ensure(pairs * outlen * 4));
+      HIP_TRY(hipMemcpyAsync(w->x.p, v, pairs * outlen * 4, hipMemcpyDeviceToDevice, wl.st));
+      cur = w->x.as<uint32_t>();
+      n = pairs;
+      len = outlen;
+    }
+    std::vector<uint32_t> res(len);
+    HIP_TRY(hipMemcpyAsync(res.data(), cur, len * 4, hipMemcpyDeviceToHost, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    bn::Limbs v((len + 1) / 2, 0);
+    for (size_t i = 0; i < len; ++i) v[i / 2] |= res[i] << (16 * (i % 2));
+    bn::trim(v);
+    return emit_be(v, std::max<size_t>(1, bn::byte_length(v)), out, out_cap, out_len);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
 // ---- device columns -----------------------------------------------------------
 int dds_col_create(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, size_t capacity, dds_col** out) {
   try {
@@ -1029,8 +1087,22 @@ int fold_dec(dds_ctx* ctx, const char* const* values, size_t count, const char* 
   int rc = parse_values(values, count, &mags, &negs);
   if (rc) return rc;
   if (count == 1) return write_dec(bn::to_dec(mags[0], negs[0]), out, out_cap, out_len);  // unreduced (:416-417)
+  if (!mod_dec && !additive) {  // unbounded product (DDSRestServer.scala:520) on the GPU product tree
+    size_t width = 1;
+    bool neg = false;
+    for (size_t i = 0; i < count; ++i) {
+      width = std::max(width, bn::byte_length(mags[i]));
+      neg ^= (bool)negs[i];
+    }
+    std::vector<uint8_t> ops(count * width);
+    for (size_t i = 0; i < count; ++i) bn::to_be(mags[i], ops.data() + i * width, width);
+    std::vector<uint8_t> buf(count * width + 8);
+    size_t len = 0;
+    if ((rc = dds_bigint_product(ctx, ops.data(), width, count, buf.data(), buf.size(), &len))) return rc;
+    bn::Limbs r = bn::from_be(buf.data(), len);
+    return write_dec(bn::to_dec(r, neg && !r.empty()), out, out_cap, out_len);
+  }
   if (!mod_dec) {
-    if (!additive) return fail(DDS_E_UNSUPPORTED, "unbounded product (MultAll without pubkey) not implemented");
     // plain sum: positives and negatives summed separately on the GPU
     size_t width = 1;
     for (auto& m : mags) width = std::max(width, bn::byte_length(m));

@@ -474,6 +474,57 @@ __global__ void __launch_bounds__(256) k_plain_sum_reduce(const uint64_t* __rest
 }
 
 // ------------------------------------------------------------------------------
+// unbounded big-integer product tree: MultAll without pubkey (DDSRestServer.scala:520,
+// `mult.get.multiply(operand)`). Radix 2^16 limbs in 32-bit words; one tree level
+// multiplies rows (2p, 2p+1) of a [count][len] matrix into row p of [count/2][2 len].
+// ------------------------------------------------------------------------------
+// column sums: S[p][k] = sum_{i+j=k} A[2p][i] * A[2p+1][j]  (< len * 2^32, 64-bit)
+__global__ void __launch_bounds__(256) k_bigmul_cols(const uint32_t* __restrict__ A, size_t count, size_t len,
+                                                     uint64_t* __restrict__ Sk) {
+  const size_t outlen = 2 * len;
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t p = blockIdx.y;
+  if (k >= outlen) return;
+  const uint32_t* a = A + (2 * p) * len;
+  uint64_t acc = 0;
+  if (2 * p + 1 < count) {
+    const uint32_t* b = a + len;
+    const size_t i0 = k >= len ? k - len + 1 : 0;
+    const size_t i1 = k < len ? k : len - 1;
+    for (size_t i = i0; i <= i1; ++i) acc += (uint64_t)(a[i] * b[k - i]);  // 16x16 -> 32 bits
+  } else {
+    acc = k < len ? a[k] : 0;  // odd row passes through
+  }
+  Sk[p * outlen + k] = acc;
+}
+
+// spread each 64-bit column sum over four 16-bit limbs: v_k = sum_d piece_d(S_{k-d}) (< 2^18)
+__global__ void __launch_bounds__(256) k_bigmul_spread(const uint64_t* __restrict__ Sk, size_t outlen,
+                                                       uint32_t* __restrict__ V) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t p = blockIdx.y;
+  if (k >= outlen) return;
+  const uint64_t* s = Sk + p * outlen;
+  uint32_t v = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+    if (k >= (size_t)d) v += (uint32_t)((s[k - d] >> (16 * d)) & 0xFFFFu);
+  V[p * outlen + k] = v;
+}
+
+// one carry pass: w_k = (v_k & 0xFFFF) + (v_{k-1} >> 16); flags[0] = 1 if some w_k > 0xFFFF
+__global__ void __launch_bounds__(256) k_bigmul_carry(const uint32_t* __restrict__ V, size_t outlen,
+                                                      uint32_t* __restrict__ Wout, uint32_t* __restrict__ flag) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t p = blockIdx.y;
+  if (k >= outlen) return;
+  const uint32_t* v = V + p * outlen;
+  const uint32_t w = (v[k] & 0xFFFFu) + (k ? v[k - 1] >> 16 : 0u);
+  Wout[p * outlen + k] = w;
+  if (w > 0xFFFFu) atomicOr(flag, 1u);
+}
+
+// ------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------
 // Instantiated shapes (S limbs of W bits on TPI lanes); a modulus uses the first that holds
@@ -605,6 +656,21 @@ hipError_t launch_plain_sum(const uint32_t* X, size_t stride, size_t count, int 
                             uint64_t* out, hipStream_t st) {
   hipLaunchKernelGGL(k_plain_sum, dim3(grid_for(nthreads)), dim3(256), 0, st, X, stride, count, S, nthreads, part);
   hipLaunchKernelGGL(k_plain_sum_reduce, dim3(S), dim3(256), 0, st, part, nthreads, S, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_bigmul_level(const uint32_t* A, size_t count, size_t len, uint64_t* Sk, uint32_t* V, hipStream_t st) {
+  const size_t pairs = (count + 1) / 2, outlen = 2 * len;
+  dim3 grid((unsigned)((outlen + 255) / 256), (unsigned)pairs);
+  hipLaunchKernelGGL(k_bigmul_cols, grid, dim3(256), 0, st, A, count, len, Sk);
+  hipLaunchKernelGGL(k_bigmul_spread, grid, dim3(256), 0, st, Sk, outlen, V);
+  return hipGetLastError();
+}
+
+hipError_t launch_bigmul_carry(const uint32_t* V, size_t pairs, size_t outlen, uint32_t* Wout, uint32_t* flag,
+                               hipStream_t st) {
+  dim3 grid((unsigned)((outlen + 255) / 256), (unsigned)pairs);
+  hipLaunchKernelGGL(k_bigmul_carry, grid, dim3(256), 0, st, V, outlen, Wout, flag);
   return hipGetLastError();
 }
 

@@ -44,6 +44,11 @@ hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n,
                              uint32_t* block_counts, uint64_t* total, uint32_t* out, hipStream_t st);
 hipError_t launch_plain_sum(const uint32_t* X, size_t stride, size_t count, int S, size_t nthreads, uint64_t* part,
                             uint64_t* out, hipStream_t st);
+// unbounded product tree level: rows (2p, 2p+1) of A[count][len] (radix 2^16 in u32)
+// -> V[pairs][2 len] (limbs < 2^18, carries resolved by launch_bigmul_carry passes)
+hipError_t launch_bigmul_level(const uint32_t* A, size_t count, size_t len, uint64_t* Sk, uint32_t* V, hipStream_t st);
+hipError_t launch_bigmul_carry(const uint32_t* V, size_t pairs, size_t outlen, uint32_t* Wout, uint32_t* flag,
+                               hipStream_t st);
 hipError_t fold_occupancy(int S, int* blocks_per_cu);
 
 }  // namespace ddshe

@@ -32,6 +32,7 @@ EXPORTS = [
     "dds_ctx_create", "dds_ctx_destroy", "dds_strerror", "dds_last_error", "dds_max_modulus_bits",
     "dds_ctx_set_stream", "dds_ctx_set_timing", "dds_ctx_get_timing", "dds_ctx_reset_timing", "dds_ctx_get_fold_work",
     "dds_modmul_fold", "dds_paillier_sum", "dds_rsa_product", "dds_modmul_pairs", "dds_bigint_sum",
+    "dds_bigint_product",
     "dds_col_create", "dds_col_destroy", "dds_col_append", "dds_col_count", "dds_col_read", "dds_col_fold",
     "dds_col_fold_partial", "dds_col_partial_words", "dds_combine_partials", "dds_col_fill_paillier_synth",
     "dds_ope_filter", "dds_ope_filter_device", "dds_paillier_encrypt_batch", "dds_modexp_batch", "dds_sum_all_dec",
@@ -64,6 +65,7 @@ for _n in ("dds_modmul_fold", "dds_paillier_sum", "dds_rsa_product"):
     _sig(_n, C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, _sz, _u8p, _sz, _szp)
 _sig("dds_modmul_pairs", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, C.c_char_p, _sz, _sz, _u8p)
 _sig("dds_bigint_sum", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz, _u8p, _sz, _szp)
+_sig("dds_bigint_product", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz, _u8p, _sz, _szp)
 _sig("dds_col_create", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz, C.POINTER(C.c_void_p))
 _sig("dds_col_destroy", C.c_int, C.c_void_p)
 _sig("dds_col_append", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz)
@@ -191,6 +193,16 @@ class Engine:
         olen = C.c_size_t()
         _check(_lib.dds_bigint_sum(self._h, ints_to_be(ops, width), width, len(ops), out, len(out), C.byref(olen)),
                "dds_bigint_sum")
+        return int.from_bytes(bytes(out[: olen.value]), "big")
+
+    def bigint_product(self, ops) -> int:
+        """Unbounded product (MultAll without pubkey, DDSRestServer.scala:520)."""
+        ops = [int(x) for x in ops]
+        width = max([1] + [nbytes(x) for x in ops])
+        out = (C.c_uint8 * (width * max(1, len(ops)) + 8))()
+        olen = C.c_size_t()
+        _check(_lib.dds_bigint_product(self._h, ints_to_be(ops, width), width, len(ops), out, len(out),
+                                       C.byref(olen)), "dds_bigint_product")
         return int.from_bytes(bytes(out[: olen.value]), "big")
 
     # ---- decimal route entry points ----

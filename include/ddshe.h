@@ -98,6 +98,12 @@ int dds_modmul_pairs(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, cons
 int dds_bigint_sum(dds_ctx* ctx, const uint8_t* operands_be, size_t width, size_t count, uint8_t* out,
                    size_t out_cap, size_t* out_len);
 
+/* MultAll without pubkey (unbounded BigInteger multiply, DDSRestServer.scala:520):
+ * product of count operands on a GPU product tree; result big-endian, minimal length
+ * (*out_len), at most count*width bytes. */
+int dds_bigint_product(dds_ctx* ctx, const uint8_t* operands_be, size_t width, size_t count, uint8_t* out,
+                       size_t out_cap, size_t* out_len);
+
 /* ---- device-resident columns (ciphertexts stay in HBM across requests) ----
  * A column holds `count` residues of one modulus in the engine's resident
  * format (limb-transposed radix-2^27). */

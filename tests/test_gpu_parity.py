@@ -69,8 +69,6 @@ def test_routes_golden(eng, vectors):
             else:
                 assert routes.sum_all(eng, rows, c["position"], c["nsqr"]) == c["result"]
         elif c["route"] == "MultAll":
-            if c["n"] is None:
-                continue  # unbounded product: DDS_E_UNSUPPORTED this round
             assert routes.mult_all(eng, rows, c["position"], c["n"]) == c["result"]
         else:
             assert sorted(routes.search(eng, c["route"], keyed, c["position"], c["value"])) == c["result"]
@@ -137,6 +135,19 @@ def test_bigint_sum(eng):
     xs = [rng.getrandbits(4096) for _ in range(5000)]
     assert eng.bigint_sum(xs) == sum(xs)
     assert eng.bigint_sum([5]) == 5
+
+
+@pytest.mark.parametrize("count,bits", [(2, 64), (3, 2048), (17, 4096), (1000, 2048), (257, 31)])
+def test_bigint_product_tree(eng, count, bits):
+    rng = random.Random(count * bits)
+    xs = [rng.getrandbits(bits) for _ in range(count)]
+    exp = 1
+    for x in xs:
+        exp *= x
+    assert eng.bigint_product(xs) == exp
+    assert eng.bigint_product(xs[:1] + [0] + xs[1:]) == 0
+    assert eng.mult_all_dec(["-3", "5", "-7"], None) == "105"
+    assert eng.mult_all_dec(["-3", "5"], None) == "-15"
 
 
 def test_decimal_routes_signs_and_formats(eng, keys):
