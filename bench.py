@@ -129,12 +129,17 @@ def main():
         avg_launch_s = fold_ms / max(1, fold_launches) / 1e3
         per_launch_mac = fold_modmuls / max(1, fold_launches) * MAC_PER_MODMUL
         achieved = per_launch_mac / avg_launch_s / 1e12 if fold_launches else None
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+        if os.path.exists(tf):  # HBM bytes per launch from the committed rocprofv3 PMC passes, per row
+            pm = json.load(open(tf))
+            traffic = pm["hbm_bytes_per_launch"] / pm["rows_per_launch"] * mine  # the launch reads every row once
         roofline = {
             "bound": "valu-int",
             "kernel": "k_fold<152,4> (first fold level over the rows)",
             "achieved": achieved, "peak": PEAK_TMAC, "unit": "TMAC/s",
             "frac": (achieved / PEAK_TMAC) if achieved else None,
-            "traffic": None,
+            "traffic": traffic, "traffic_unit": "bytes/launch (PMC, profiles/r01_pmc_traffic.json)",
             "avg_launch_ms": avg_launch_s * 1e3,
             "modmuls_per_launch": fold_modmuls / max(1, fold_launches),
             "mac_per_modmul": MAC_PER_MODMUL,

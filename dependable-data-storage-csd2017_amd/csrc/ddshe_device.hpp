@@ -118,6 +118,9 @@ struct Mont {
   // opaque register barrier: stops LLVM re-associating the u64 sums of consecutive
   // unrolled steps into mad(x,y,0)+add trees (extra registers and 64-bit adds)
   __device__ __forceinline__ static void fence_t(uint64_t (&t)[L]) {
+#ifdef DDSHE_AB_NO_FENCE_T
+    return;
+#endif
 #pragma unroll
     for (int l = 0; l < L; ++l) asm volatile("" : "+v"(t[l]));
   }
@@ -155,13 +158,53 @@ struct Mont {
 #else
     constexpr int PF = (S % 4 == 0) ? 4 : 2;  // limbs per unrolled block = loads in flight
 #endif
-    static_assert(S % PF == 0, "S % PF");
+    static_assert(S % PF == 0 && S >= 2 * PF, "S % PF");
     const uint32_t voff = row * 4u;
     const uint32_t sstride = (uint32_t)stride * 4u;  // host guarantees PF*stride*4 < 2^32
     auto block_rsrc = [&](int i) {
       return __builtin_amdgcn_make_buffer_rsrc((void*)(X + (size_t)i * stride), (short)0, (int)(PF * sstride),
                                                0x00020000);
     };
+#ifndef DDSHE_AB_SHALLOW_PF
+    // two blocks in flight: limbs of block i+2 are requested while block i is computed
+    // (one block = PF steps ~ 1.4k cycles per wave is short of an HBM miss under load)
+    uint32_t bq[PF], bm[PF];
+    {
+      const auto rs0 = block_rsrc(0), rs1 = block_rsrc(PF);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) bq[q] = __builtin_amdgcn_raw_buffer_load_b32(rs0, voff, q * sstride, 0);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) bm[q] = __builtin_amdgcn_raw_buffer_load_b32(rs1, voff, q * sstride, 0);
+    }
+#pragma unroll 1
+    for (int i = 0; i < S - 2 * PF; i += PF) {
+      fence_ops(a, n);
+      const auto rs = block_rsrc(i + 2 * PF);
+      uint32_t bn[PF];
+#pragma unroll
+      for (int q = 0; q < PF; ++q) bn[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, q * sstride, 0);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        step(t, a, n, bq[q], n0, top);
+        fence_t(t);
+      }
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        bq[q] = bm[q];
+        bm[q] = bn[q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      step(t, a, n, bq[q], n0, top);
+      fence_t(t);
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      step(t, a, n, bm[q], n0, top);
+      fence_t(t);
+    }
+#else
     uint32_t bq[PF];
     {
       const auto rs = block_rsrc(0);
@@ -188,6 +231,7 @@ struct Mont {
       step(t, a, n, bq[q], n0, top);
       fence_t(t);
     }
+#endif
     settle(t, a, bottom);
   }
 
