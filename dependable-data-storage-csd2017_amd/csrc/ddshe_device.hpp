@@ -147,6 +147,10 @@ struct Mont {
   // each block of PF limbs is read through a buffer descriptor whose base is
   // X + i*stride (SGPRs), voffset = 4*row, soffset = 4*q*stride — no per-lane 64-bit
   // address arithmetic in the loop.
+  // FenceOps: see fence_ops. The single-product fold loop runs faster without it (the
+  // operand redefinitions also pin the schedule; measured -6 % time at 2-block prefetch),
+  // kernels with several products in sequence need it to stay spill-free.
+  template <bool FenceOps = true>
   __device__ __forceinline__ static void mul_col(uint32_t (&a)[L], const uint32_t (&n)[L],
                                                  const uint32_t* __restrict__ X, size_t stride, uint32_t row,
                                                  uint32_t n0, bool top, bool bottom) {
@@ -178,7 +182,7 @@ struct Mont {
     }
 #pragma unroll 1
     for (int i = 0; i < S - 2 * PF; i += PF) {
-      fence_ops(a, n);
+      if constexpr (FenceOps) fence_ops(a, n);
       const auto rs = block_rsrc(i + 2 * PF);
       uint32_t bn[PF];
 #pragma unroll
@@ -213,7 +217,7 @@ struct Mont {
     }
 #pragma unroll 1
     for (int i = 0; i < S - PF; i += PF) {
-      fence_ops(a, n);
+      if constexpr (FenceOps) fence_ops(a, n);
       const auto rs = block_rsrc(i + PF);
       uint32_t bn[PF];
 #pragma unroll

@@ -15,19 +15,19 @@ int main(int argc, char** argv) {
   int nvar = argc > 3 ? atoi(argv[3]) : 4;
   launch_t fns[4] = {k_ab0_launch, k_ab1_launch, k_ab2_launch, k_ab3_launch};
   size_t stride = (count + 63) / 64 * 64;
-  std::vector<uint32_t> h((size_t)S * stride), hn(S);
+  std::vector<uint32_t> h((size_t)S * stride), hn((size_t)S * 5, 0);  // constant block (kConstCount*S)
   srand(1);
-  for (int l = 0; l < S; ++l) hn[l] = (uint32_t)rand() & ((1u << W) - 1);
+  for (int l = 0; l < S; ++l) hn[l] = (uint32_t)rand() & ((1u << W) - 1);  // kConstN
   hn[0] |= 1; hn[S - 1] = (1u << 10) | 5;   // ~4095-bit odd modulus (top limb small)
   for (int l = 0; l < S; ++l) for (size_t i = 0; i < count; ++i) h[(size_t)l * stride + i] = (uint32_t)rand() & ((1u << W) - 1);
   for (size_t i = 0; i < count; ++i) h[(size_t)(S - 1) * stride + i] = 3;  // value < N
   uint32_t inv = hn[0]; for (int i = 0; i < 5; ++i) inv *= 2u - hn[0] * inv;
   uint32_t n0 = (0u - inv) & ((1u << W) - 1);
   uint32_t *dX, *dN, *dP;
-  hipMalloc(&dX, h.size() * 4); hipMalloc(&dN, S * 4);
+  hipMalloc(&dX, h.size() * 4); hipMalloc(&dN, hn.size() * 4);
   size_t G = 32768, ps = G;
-  hipMalloc(&dP, (size_t)S * ps * 4);
-  hipMemcpy(dX, h.data(), h.size() * 4, hipMemcpyHostToDevice); hipMemcpy(dN, hn.data(), S * 4, hipMemcpyHostToDevice);
+  hipMalloc(&dP, (size_t)160 * ps * 4);  // production kernel zero-fills to s_out=160
+  hipMemcpy(dX, h.data(), h.size() * 4, hipMemcpyHostToDevice); hipMemcpy(dN, hn.data(), hn.size() * 4, hipMemcpyHostToDevice);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   std::vector<std::vector<float>> t(nvar);
   for (int v = 0; v < nvar; ++v) fns[v](dX, stride, count, dN, n0, dP, ps, G);  // warm

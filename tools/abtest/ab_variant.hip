@@ -1,7 +1,24 @@
 // One fold-kernel variant per translation unit (A/B timing tool, not product).
-// Compiled with -DVARIANT=<n> -DKNAME=<kernel name>; variant switches live in ddshe_device.hpp
-// behind DDSHE_AB_* macros.
+// -DKNAME=<name> names the variant; switches live in ddshe_device.hpp behind DDSHE_AB_* macros.
+// -DPROD times the production kernel (ddshe_fold.hpp's k_fold) compiled inside namespace KNAME,
+// so several builds of it (different macros) can share one process.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#define CAT2(a, b) a##b
+#define CAT(a, b) CAT2(a, b)
+#ifdef PROD
+namespace KNAME {
+#include "ddshe_fold.hpp"
+}
+extern "C" hipError_t CAT(KNAME, _launch)(const uint32_t* X, size_t xstride, size_t count, const uint32_t* C, uint32_t n0,
+                                          uint32_t* P, size_t pstride, size_t ngroups) {
+  // C: kConstCount*S constant block (only kConstN / kConstRmod are read by k_fold)
+  hipLaunchKernelGGL((KNAME::ddshe::k_fold<148, 4, 28>), dim3((unsigned)((ngroups * 4 + 255) / 256)), dim3(256), 0, 0,
+                     X, xstride, count, C, n0, P, pstride, ngroups, 160);
+  return hipGetLastError();
+}
+#else
 #include "ddshe_device.hpp"
 using namespace ddshe;
 template <int S, int TPI, int W>
@@ -23,11 +40,10 @@ __global__ void __launch_bounds__(256, 2) KNAME(const uint32_t* __restrict__ X, 
   M::normalize(a, bottom);
   for (int l = 0; l < L; ++l) P[(size_t)(r * L + l) * pstride + grp] = a[l];
 }
-#define CAT2(a, b) a##b
-#define CAT(a, b) CAT2(a, b)
 extern "C" hipError_t CAT(KNAME, _launch)(const uint32_t* X, size_t xstride, size_t count, const uint32_t* N, uint32_t n0,
-                                   uint32_t* P, size_t pstride, size_t ngroups) {
+                                          uint32_t* P, size_t pstride, size_t ngroups) {
   hipLaunchKernelGGL((KNAME<148, 4, 28>), dim3((unsigned)((ngroups * 4 + 255) / 256)), dim3(256), 0, 0, X, xstride,
                      count, N, n0, P, pstride, ngroups);
   return hipGetLastError();
 }
+#endif
