@@ -61,13 +61,39 @@ struct DevBuf {
   }
 };
 
+struct HostBuf {  // pinned staging (truly asynchronous H2D)
+  void* p = nullptr;
+  size_t cap = 0;
+  ~HostBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) {
+      (void)hipHostFree(p);
+      p = nullptr;
+      cap = 0;
+    }
+    hipError_t e = hipHostMalloc(&p, bytes, 0);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+};
+
 struct Worker {
   hipStream_t stream = nullptr;
   bool timed_fold = false;  // ev[0]/ev[1] bracket a first-level fold launch not yet accounted
   DevBuf in, in2, x, x2, p0, p1, out, flags, y, misc, misc2;
   hipEvent_t ev[4] = {};
+  // decimal codec: double-buffered pinned chunks (chars, offsets), their device copies,
+  // per-row status bytes, and the event after each slot's last use
+  HostBuf hch[2], hoff[2];
+  DevBuf dch[2], doff[2], rflags;
+  hipEvent_t ev_dec[2] = {};
   ~Worker() {
     for (auto e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto e : ev_dec)
       if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -88,9 +114,15 @@ struct ModConsts {
   uint32_t* d2 = nullptr;
   std::mutex ymu;
   std::map<int64_t, std::vector<uint32_t>> ycache;  // E -> 2^(W*S2 - E) mod N, tail limbs
+  // decimal codec table (k_dec_parse), built on first use: Pt[l*jpad + j] = limb l of 10^(8j)
+  // for the jfit powers below 2^(W*S), then jst[i] (first power reaching limb TPI*i, rounded down to 4)
+  std::mutex decmu;
+  uint32_t* dtab = nullptr;
+  int jfit = 0, jpad = 0;
   ~ModConsts() {
     if (d) (void)hipFree(d);
     if (d2) (void)hipFree(d2);
+    if (dtab) (void)hipFree(dtab);
   }
   std::vector<uint32_t> rw(const bn::Limbs& v) const { return bn::to_rw(v, S, W); }
   bn::Limbs value(const uint32_t* limbs) const { return bn::from_rw(limbs, S, W); }
@@ -162,6 +194,8 @@ struct WorkerLease {
         return fail(DDS_E_HIP, "hipStreamCreate");
       for (auto& e : nw->ev)
         if (hipEventCreate(&e) != hipSuccess) return fail(DDS_E_HIP, "hipEventCreate");
+      for (auto& e : nw->ev_dec)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(DDS_E_HIP, "hipEventCreate");
       w = nw.get();
       ctx->workers.push_back(std::move(nw));
     }
@@ -351,6 +385,124 @@ int ingest(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint8_t
   HIP_TRY(hipStreamSynchronize(st));
   if (flags & 2u) return fail(DDS_E_RANGE, "operand wider than the modulus limb width");
   if (flags & 1u) HIP_TRY(launch_reduce_rows(mc.S, X, stride, count, mc.d, mc.n0, st));
+  return DDS_OK;
+}
+
+// ---- decimal codec (BigInteger.toString rows) ---------------------------------------------
+// The rows arrive either Arrow-style (chars + offsets[count+1]) or as NUL-terminated strings
+// (the JNA String[] of the route bodies, DDSRestServer.scala:417,419,422,513).
+struct DecRows {
+  const char* chars = nullptr;
+  const uint64_t* offs = nullptr;
+  const char* const* strs = nullptr;
+  size_t len(size_t i) const { return strs ? strlen(strs[i]) : (size_t)(offs[i + 1] - offs[i]); }
+  const char* row(size_t i) const { return strs ? strs[i] : chars + offs[i]; }
+};
+
+constexpr size_t kDecChunkBytes = (size_t)64 << 20;  // chars per pinned chunk
+constexpr size_t kDecChunkRows = (size_t)1 << 18;
+
+int dec_table(ModConsts& mc) {
+  std::lock_guard<std::mutex> lk(mc.decmu);
+  if (mc.dtab) return DDS_OK;
+  const size_t cap = (size_t)mc.W * mc.S;
+  std::vector<bn::Limbs> pw;
+  bn::Limbs P{1};
+  while (bn::bit_length(P) <= cap) {
+    pw.push_back(P);
+    P = bn::mul_small_add(P, 100000000u, 0);
+  }
+  const int jfit = (int)pw.size(), jpad = (jfit + 3) & ~3, L = mc.S / mc.TPI;
+  // 64-bit lazy accumulation: jfit * (10^8 - 1) * (2^W - 1) < 2^64
+  if ((double)jfit * 1e8 * (double)(1u << mc.W) >= 18446744073709551616.0)
+    return fail(DDS_E_UNSUPPORTED, "decimal table bound");
+  std::vector<uint32_t> tab((size_t)mc.S * jpad + ((L + 3) & ~3), 0);
+  for (int j = 0; j < jfit; ++j) {
+    std::vector<uint32_t> rw = mc.rw(pw[j]);
+    for (int l = 0; l < mc.S; ++l) tab[(size_t)l * jpad + j] = rw[l];
+  }
+  for (int i = 0; i < L; ++i) {
+    const size_t lbits = (size_t)mc.W * mc.TPI * i;
+    int j = 0;
+    while (j < jfit && bn::bit_length(pw[j]) <= lbits) ++j;
+    tab[(size_t)mc.S * jpad + i] = (uint32_t)(j & ~3);
+  }
+  uint32_t* d = nullptr;
+  HIP_TRY(hipMalloc(&d, tab.size() * 4));
+  if (hipMemcpy(d, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    return fail(DDS_E_HIP, "decimal table upload");
+  }
+  mc.dtab = d;
+  mc.jfit = jfit;
+  mc.jpad = jpad;
+  return DDS_OK;
+}
+
+// Parse rows [0, count) into X (stride) on the GPU: chunks are packed into pinned buffers
+// (host, overlapping the previous chunk's copy + parse), copied, parsed by k_dec_parse, then
+// negative / >= 2N rows are fixed by k_dec_fix. *orflags = OR of the row status bits
+// (kDecFormat / kDecWide rows hold zeros); w->rflags keeps the per-row bytes. Rows longer than a
+// chunk are parsed as "0" and listed in *long_rows for the caller.
+int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, size_t count, uint32_t* X,
+               size_t stride, uint32_t* orflags, std::vector<size_t>* long_rows) {
+  *orflags = 0;
+  if (count == 0) return DDS_OK;
+  int rc = dec_table(mc);
+  if (rc) return rc;
+  HIP_TRY(w->rflags.ensure(count));
+  HIP_TRY(w->flags.ensure(16));
+  HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, st));
+  bool used[2] = {false, false};
+  int slot = 0;
+  for (size_t b = 0; b < count;) {
+    if (used[slot]) HIP_TRY(hipEventSynchronize(w->ev_dec[slot]));
+    HIP_TRY(w->hch[slot].ensure(kDecChunkBytes + 64));
+    HIP_TRY(w->hoff[slot].ensure((kDecChunkRows + 1) * 8));
+    char* dst = (char*)w->hch[slot].p + 16;
+    uint64_t* o = (uint64_t*)w->hoff[slot].p;
+    size_t pos = 0, e = b;
+    o[0] = 0;
+    while (e < count && e - b < kDecChunkRows) {
+      size_t n = src.len(e);
+      const bool longrow = n > kDecChunkBytes - 64;
+      if (longrow) n = 1;
+      if (pos + n > kDecChunkBytes) break;
+      if (longrow) long_rows->push_back(e);
+      memcpy(dst + pos, longrow ? "0" : src.row(e), n);
+      pos += n;
+      o[++e - b] = pos;
+    }
+    const size_t nrows = e - b, bytes = (16 + pos + 16 + 3) & ~(size_t)3;
+    memset(dst + pos, 0, bytes - 16 - pos);
+    HIP_TRY(w->dch[slot].ensure(bytes));
+    HIP_TRY(w->doff[slot].ensure((nrows + 1) * 8));
+    HIP_TRY(hipMemcpyAsync(w->dch[slot].p, w->hch[slot].p, bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(w->doff[slot].p, o, (nrows + 1) * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_dec_parse(mc.S, w->dch[slot].as<uint32_t>(), w->doff[slot].as<uint64_t>(), 0, nrows, mc.dtab,
+                             mc.jfit, mc.jpad, mc.d, X + b, stride, w->rflags.as<uint8_t>() + b,
+                             w->flags.as<uint32_t>(), st));
+    HIP_TRY(hipEventRecord(w->ev_dec[slot], st));
+    used[slot] = true;
+    slot ^= 1;
+    b = e;
+  }
+  uint32_t fl = 0;
+  HIP_TRY(hipMemcpyAsync(&fl, w->flags.p, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (fl & (kDecNeg | kDecReduce))
+    HIP_TRY(launch_dec_fix(mc.S, X, stride, count, w->rflags.as<uint8_t>(), mc.d, mc.n0, st));
+  *orflags = fl;
+  return DDS_OK;
+}
+
+// indices of rows whose status has any bit of `mask` (after ingest_dec)
+int dec_rows_with(Worker* w, hipStream_t st, size_t count, uint32_t mask, std::vector<size_t>* rows) {
+  std::vector<uint8_t> f(count);
+  HIP_TRY(hipMemcpyAsync(f.data(), w->rflags.p, count, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  for (size_t i = 0; i < count; ++i)
+    if (f[i] & mask) rows->push_back(i);
   return DDS_OK;
 }
 
@@ -688,6 +840,39 @@ int dds_col_append(dds_col* col, const uint8_t* ops, size_t width, size_t count)
   }
 }
 
+int dds_col_append_dec(dds_col* col, const char* chars, const uint64_t* offsets, size_t count) {
+  try {
+    if (!col || (count && (!chars || !offsets))) return fail(DDS_E_ARG, "bad arguments");
+    std::lock_guard<std::mutex> lk(col->mu);
+    if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
+    if (count == 0) return DDS_OK;
+    for (size_t i = 0; i < count; ++i)
+      if (offsets[i + 1] < offsets[i]) return fail(DDS_E_ARG, "offsets must be non-decreasing");
+    WorkerLease wl(col->ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    DecRows src;
+    src.chars = chars;
+    src.offs = offsets;
+    uint32_t fl = 0;
+    std::vector<size_t> longr;
+    if ((rc = ingest_dec(wl.w, wl.st, *col->mc, src, count, col->d + col->count, col->stride, &fl, &longr)))
+      return rc;
+    if (fl & (kDecFormat | kDecWide)) {
+      std::vector<size_t> bad;
+      if ((rc = dec_rows_with(wl.w, wl.st, count, kDecFormat, &bad))) return rc;
+      if (!bad.empty()) return fail(DDS_E_FORMAT, "row " + std::to_string(bad[0]) + ": NumberFormatException");
+      return fail(DDS_E_RANGE, "decimal row wider than the column limb capacity");
+    }
+    if (!longr.empty()) return fail(DDS_E_RANGE, "decimal row wider than the column limb capacity");
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    col->count += count;
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
 int dds_col_read(dds_col* col, size_t first, size_t count, uint8_t* out) {
   try {
     if (!col || (count && !out) || first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
@@ -699,7 +884,9 @@ int dds_col_read(dds_col* col, size_t first, size_t count, uint8_t* out) {
     std::vector<uint32_t> limbs(S);
     for (size_t i = 0; i < count; ++i) {
       for (int l = 0; l < S; ++l) limbs[l] = h[(size_t)l * count + i];
-      if (!bn::to_be(col->mc->value(limbs.data()), out + i * col->mc->bytes, col->mc->bytes))
+      bn::Limbs v = col->mc->value(limbs.data());
+      if (bn::cmp(v, col->mc->N) >= 0) v = bn::mod(v, col->mc->N);  // rows are kept < 2N
+      if (!bn::to_be(v, out + i * col->mc->bytes, col->mc->bytes))
         return fail(DDS_E_RANGE, "row does not fit");
     }
     return DDS_OK;
@@ -1078,10 +1265,72 @@ int write_dec(const std::string& s, char* out, size_t out_cap, size_t* out_len) 
 }
 
 // shared by SumAll (nsqr) and MultAll (pubkey modulus): acc = prod mod M over decimal operands
+// Modular SumAll / MultAll over decimal rows (DDSRestServer.scala:412-430, 506-524): rows are
+// parsed on the GPU (ingest_dec) straight into a device column, then folded. Rows the column
+// cannot hold (|x| >= 2^(W*S): never a well-formed ciphertext) are reduced exactly on the host
+// at the boundary so the result keeps BigInteger semantics.
+int fold_dec_mod(dds_ctx* ctx, const char* const* values, size_t count, const char* mod_dec, char* out,
+                 size_t out_cap, size_t* out_len) {
+  bn::Limbs M;
+  bool mneg = false;
+  if (!bn::from_dec(mod_dec, strlen(mod_dec), M, &mneg) || mneg || M.empty())
+    return fail(DDS_E_FORMAT, "modulus: NumberFormatException / non-positive");
+  const size_t mb = bn::byte_length(M);
+  std::vector<uint8_t> mbe(mb);
+  bn::to_be(M, mbe.data(), mb);
+  std::shared_ptr<ModConsts> mc;
+  int rc = get_mod(ctx, mbe.data(), mb, &mc);
+  if (rc) return rc;
+  WorkerLease wl(ctx);
+  if ((rc = wl.acquire())) return rc;
+  Worker* w = wl.w;
+  const size_t stride = round_up(count, 64);
+  HIP_TRY(w->x.ensure((size_t)mc->S * stride * 4));
+  uint32_t* X = w->x.as<uint32_t>();
+  DecRows src;
+  src.strs = values;
+  uint32_t fl = 0;
+  std::vector<size_t> host_rows;
+  if ((rc = ingest_dec(w, wl.st, *mc, src, count, X, stride, &fl, &host_rows))) return rc;
+  if (fl & kDecFormat) {
+    std::vector<size_t> bad;
+    if ((rc = dec_rows_with(w, wl.st, count, kDecFormat, &bad))) return rc;
+    return fail(DDS_E_FORMAT, std::string("NumberFormatException: row ") + std::to_string(bad.empty() ? 0 : bad[0]));
+  }
+  if (fl & kDecWide)
+    if ((rc = dec_rows_with(w, wl.st, count, kDecWide, &host_rows))) return rc;
+  std::vector<uint32_t> fixed;  // limbs of the host-reduced rows; alive until the copies complete
+  fixed.reserve(host_rows.size() * mc->S);
+  for (size_t i : host_rows) {
+    bn::Limbs x;
+    bool neg = false;
+    if (!bn::from_dec(values[i], strlen(values[i]), x, &neg))
+      return fail(DDS_E_FORMAT, std::string("NumberFormatException: row ") + std::to_string(i));
+    x = bn::mod(x, M);
+    if (neg && !x.empty()) x = bn::sub(M, x);
+    std::vector<uint32_t> rw = mc->rw(x);
+    fixed.insert(fixed.end(), rw.begin(), rw.end());
+  }
+  for (size_t k = 0; k < host_rows.size(); ++k)
+    HIP_TRY(hipMemcpy2DAsync(X + host_rows[k], stride * 4, fixed.data() + k * mc->S, 4, 4, (size_t)mc->S,
+                             hipMemcpyHostToDevice, wl.st));
+  if (!host_rows.empty()) HIP_TRY(hipStreamSynchronize(wl.st));
+  const uint32_t* part;
+  size_t ps;
+  int64_t E;
+  if ((rc = fold_partial_device(ctx, w, wl.st, *mc, X, stride, count, &part, &ps, &E))) return rc;
+  std::vector<uint32_t> res;
+  if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, E, &res))) return rc;
+  return write_dec(bn::to_dec(mc->value2(res.data())), out, out_cap, out_len);
+}
+
 int fold_dec(dds_ctx* ctx, const char* const* values, size_t count, const char* mod_dec, bool additive, char* out,
              size_t out_cap, size_t* out_len) {
   if (!ctx || (count && !values)) return fail(DDS_E_ARG, "bad arguments");
   if (count == 0) return fail(DDS_E_EMPTY, "no operand");
+  for (size_t i = 0; i < count; ++i)
+    if (!values[i]) return fail(DDS_E_ARG, "NULL operand");
+  if (mod_dec && count > 1) return fold_dec_mod(ctx, values, count, mod_dec, out, out_cap, out_len);
   std::vector<bn::Limbs> mags;
   std::vector<bool> negs;
   int rc = parse_values(values, count, &mags, &negs);
@@ -1130,30 +1379,7 @@ int fold_dec(dds_ctx* ctx, const char* const* values, size_t count, const char* 
     bn::Limbs r = rneg ? bn::sub(sn, sp) : bn::sub(sp, sn);
     return write_dec(bn::to_dec(r, rneg), out, out_cap, out_len);
   }
-  bn::Limbs M;
-  bool mneg = false;
-  if (!bn::from_dec(mod_dec, strlen(mod_dec), M, &mneg) || mneg || M.empty())
-    return fail(DDS_E_FORMAT, "modulus: NumberFormatException / non-positive");
-  const size_t mb = bn::byte_length(M);
-  // operands to residues in [0, M): negatives are mapped to M - (|x| mod M) (Java BigInteger.mod)
-  // operands wider than the modulus (garbage rows) are reduced here so that the
-  // result still matches BigInteger semantics; well-formed ciphertexts are < M.
-  const size_t width = mb;
-  for (size_t i = 0; i < count; ++i) {
-    if (negs[i]) {
-      bn::Limbs r = bn::mod(mags[i], M);
-      mags[i] = r.empty() ? r : bn::sub(M, r);
-    } else if (bn::byte_length(mags[i]) > mb) {
-      mags[i] = bn::mod(mags[i], M);
-    }
-  }
-  std::vector<uint8_t> ops(count * width), mbe(mb), res(mb);
-  for (size_t i = 0; i < count; ++i) bn::to_be(mags[i], ops.data() + i * width, width);
-  bn::to_be(M, mbe.data(), mb);
-  size_t len = 0;
-  rc = dds_modmul_fold(ctx, mbe.data(), mb, ops.data(), width, count, res.data(), res.size(), &len);
-  if (rc) return rc;
-  return write_dec(bn::to_dec(bn::from_be(res.data(), len)), out, out_cap, out_len);
+  return fold_dec_mod(ctx, values, count, mod_dec, out, out_cap, out_len);
 }
 }  // namespace
 

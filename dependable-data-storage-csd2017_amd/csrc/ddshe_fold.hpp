@@ -81,12 +81,13 @@ struct Grp {
 
 // ------------------------------------------------------------------------------
 // fold: each group folds rows g, g+G, g+2G, ... with Montgomery products.
-// A group that folded c rows holds prod * R^(1-c); an empty group holds R mod N.
+// A group that folded c rows holds prod * R^(1-c). Requires 1 <= ngroups <= count (no empty
+// group: the launcher checks), which keeps the kernel body to load, MonPro loop, store.
 // ------------------------------------------------------------------------------
 template <int S, int TPI, int W>
 __global__ void __launch_bounds__(256, 2) k_fold(const uint32_t* __restrict__ X, size_t xstride, size_t count,
                                               const uint32_t* __restrict__ consts, uint32_t n0,
-                                              uint32_t* __restrict__ P, size_t pstride, size_t ngroups, int s_out) {
+                                              uint32_t* __restrict__ P, size_t pstride, size_t ngroups) {
   using G = Grp<S, TPI, W>;
   using M = Mont<S, TPI, W>;
   constexpr int L = G::L;
@@ -95,19 +96,11 @@ __global__ void __launch_bounds__(256, 2) k_fold(const uint32_t* __restrict__ X,
   if (grp >= ngroups) return;
   uint32_t n[L], a[L];
   g.load_vec(n, consts + kConstN * S);
-  size_t row = grp;
-  if (row < count) {
-    g.load_col(a, X, xstride, row);
-    row += ngroups;
-  } else {
-    g.load_vec(a, consts + kConstRmod * S);
-  }
-  for (; row < count; row += ngroups)
+  g.load_col(a, X, xstride, grp);
+  for (size_t row = grp + ngroups; row < count; row += ngroups)
     M::template mul_col<false>(a, n, X, xstride, (uint32_t)row, n0, g.top, g.bottom);
   M::normalize(a, g.bottom);
   g.store_col(a, P, pstride, grp);
-  // zero-extend to the tail shape's limb count (value < 2N never reaches these limbs)
-  for (int j = S + g.r; j < s_out; j += TPI) P[(size_t)j * pstride + grp] = 0u;
 }
 
 // result = canon(MonPro(P[0], Y)), Y = R^k mod N; writes S rW limbs to out

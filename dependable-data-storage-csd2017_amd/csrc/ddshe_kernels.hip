@@ -16,6 +16,7 @@
 #include "ddshe_device.hpp"
 #include "ddshe_fold.hpp"
 #include "ddshe_launch.hpp"
+#include "ddshe_shapes.hpp"
 
 namespace ddshe {
 
@@ -409,36 +410,6 @@ __global__ void __launch_bounds__(256) k_bigmul_carry(const uint32_t* __restrict
 // ------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------
-// Instantiated shapes (S limbs of W bits on TPI lanes); a modulus uses the first that holds
-// bits+2 bits. Keep in sync with kShapes below.
-#define DDSHE_DISPATCH(S_, TPI_, W_, ...)            \
-  case S_: {                                         \
-    constexpr int S = S_, TPI = TPI_, W = W_;        \
-    __VA_ARGS__;                                     \
-  } break;
-
-#define DDSHE_SWITCH(S_RT, ...)                      \
-  switch (S_RT) {                                    \
-    DDSHE_DISPATCH(40, 2, 28, __VA_ARGS__)           \
-    DDSHE_DISPATCH(74, 2, 28, __VA_ARGS__)           \
-    DDSHE_DISPATCH(148, 4, 28, __VA_ARGS__)          \
-    DDSHE_DISPATCH(232, 8, 27, __VA_ARGS__)          \
-    default: return hipErrorInvalidValue;            \
-  }
-
-static const Shape kShapes[] = {{40, 2, 28}, {74, 2, 28}, {148, 4, 28}, {232, 8, 27}};
-// latency-oriented shapes for the reduction tree / finalize: 16 lanes per bignum
-static const Shape kTail[] = {{48, 16, 28}, {80, 16, 28}, {160, 16, 28}, {240, 16, 27}};
-
-#define DDSHE_TAIL_SWITCH(S_RT, ...)                 \
-  switch (S_RT) {                                    \
-    DDSHE_DISPATCH(48, 16, 28, __VA_ARGS__)          \
-    DDSHE_DISPATCH(80, 16, 28, __VA_ARGS__)          \
-    DDSHE_DISPATCH(160, 16, 28, __VA_ARGS__)         \
-    DDSHE_DISPATCH(240, 16, 27, __VA_ARGS__)         \
-    default: return hipErrorInvalidValue;            \
-  }
-
 Shape pick_shape(size_t mod_bits) {
   for (const Shape& s : kShapes)
     if ((size_t)s.W * s.S >= mod_bits + 2) return s;
@@ -452,8 +423,6 @@ Shape tail_shape(const Shape& main) {
 }
 
 size_t max_modulus_bits() { return (size_t)kShapes[3].W * kShapes[3].S - 2; }
-
-static inline unsigned grid_for(size_t threads) { return (unsigned)((threads + 255) / 256); }
 
 hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, int W, const uint32_t* n2x,
                             uint32_t* X, size_t stride, uint32_t* flags, hipStream_t st) {
@@ -473,15 +442,22 @@ hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, c
 
 hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts, uint32_t n0,
                        uint32_t* P, size_t pstride, size_t ngroups, int s_out, hipStream_t st) {
+  if (ngroups == 0 || ngroups > count) return hipErrorInvalidValue;
+  // limbs S..s_out of the partials (tail shape is wider): zero, contiguous in the limb-major layout
+  if (s_out > S) {
+    hipError_t e = hipMemsetAsync(P + (size_t)S * pstride, 0, (size_t)(s_out - S) * pstride * 4, st);
+    if (e != hipSuccess) return e;
+  }
   DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X, xstride,
-                                     count, consts, n0, P, pstride, ngroups, s_out < S ? S : s_out));
+                                     count, consts, n0, P, pstride, ngroups));
   return hipGetLastError();
 }
 
 hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
                             uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups, hipStream_t st) {
+  if (ngroups == 0 || ngroups > count) return hipErrorInvalidValue;
   DDSHE_TAIL_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X,
-                                          xstride, count, consts, n0, P, pstride, ngroups, S));
+                                          xstride, count, consts, n0, P, pstride, ngroups));
   return hipGetLastError();
 }
 

@@ -51,4 +51,14 @@ hipError_t launch_bigmul_carry(const uint32_t* V, size_t pairs, size_t outlen, u
                                hipStream_t st);
 hipError_t fold_occupancy(int S, int* blocks_per_cu);
 
+// decimal codec (ddshe_codec.hip): per-row status bits
+enum : uint32_t { kDecNeg = 1, kDecReduce = 2, kDecWide = 4, kDecFormat = 8 };
+// chars4: staged chars, 4-byte aligned, row bytes at [offs[i] - obase + 16, offs[i+1] - obase + 16) with
+// at least 16 readable bytes before and after; tab: per-modulus table (ModConsts::dec_table)
+hipError_t launch_dec_parse(int S, const uint32_t* chars4, const uint64_t* offs, uint64_t obase, size_t count,
+                            const uint32_t* tab, int jfit, int jpad, const uint32_t* consts, uint32_t* X,
+                            size_t stride, uint8_t* rowflags, uint32_t* flags, hipStream_t st);
+hipError_t launch_dec_fix(int S, uint32_t* X, size_t stride, size_t count, const uint8_t* rowflags,
+                          const uint32_t* consts, uint32_t n0, hipStream_t st);
+
 }  // namespace ddshe

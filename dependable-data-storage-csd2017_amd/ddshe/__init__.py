@@ -33,7 +33,7 @@ EXPORTS = [
     "dds_ctx_set_stream", "dds_ctx_set_timing", "dds_ctx_get_timing", "dds_ctx_reset_timing", "dds_ctx_get_fold_work",
     "dds_modmul_fold", "dds_paillier_sum", "dds_rsa_product", "dds_modmul_pairs", "dds_bigint_sum",
     "dds_bigint_product",
-    "dds_col_create", "dds_col_destroy", "dds_col_append", "dds_col_count", "dds_col_read", "dds_col_fold",
+    "dds_col_create", "dds_col_destroy", "dds_col_append", "dds_col_append_dec", "dds_col_count", "dds_col_read", "dds_col_fold",
     "dds_col_fold_partial", "dds_col_partial_words", "dds_combine_partials", "dds_col_fill_paillier_synth",
     "dds_ope_filter", "dds_ope_filter_device", "dds_paillier_encrypt_batch", "dds_modexp_batch", "dds_sum_all_dec",
     "dds_mult_all_dec",
@@ -69,6 +69,7 @@ _sig("dds_bigint_product", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz, _u8p, _sz,
 _sig("dds_col_create", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz, C.POINTER(C.c_void_p))
 _sig("dds_col_destroy", C.c_int, C.c_void_p)
 _sig("dds_col_append", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz)
+_sig("dds_col_append_dec", C.c_int, C.c_void_p, C.c_char_p, C.POINTER(C.c_uint64), _sz)
 _sig("dds_col_count", _sz, C.c_void_p)
 _sig("dds_col_read", C.c_int, C.c_void_p, _sz, _sz, _u8p)
 _sig("dds_col_fold", C.c_int, C.c_void_p, _sz, _sz, _u8p, _sz, _szp)
@@ -310,6 +311,22 @@ class Column:
         ops = [int(x) for x in ops]
         width = max([self.mb] + [nbytes(x) for x in ops])
         _check(_lib.dds_col_append(self._h, ints_to_be(ops, width), width, len(ops)), "dds_col_append")
+
+    def append_dec(self, rows):
+        """Append decimal rows (str / bytes, BigInteger.toString text), parsed on the GPU.
+        `rows` may also be a (chars: bytes, offsets: uint64 array of len+1) Arrow-style pair."""
+        if isinstance(rows, tuple):
+            chars, offs = rows
+            offs = np.ascontiguousarray(offs, dtype=np.uint64)
+            n = len(offs) - 1
+        else:
+            enc = [r.encode() if isinstance(r, str) else bytes(r) for r in rows]
+            chars = b"".join(enc)
+            offs = np.zeros(len(enc) + 1, dtype=np.uint64)
+            np.cumsum([len(e) for e in enc], out=offs[1:])
+            n = len(enc)
+        _check(_lib.dds_col_append_dec(self._h, chars, offs.ctypes.data_as(C.POINTER(C.c_uint64)), n),
+               "dds_col_append_dec")
 
     def read(self, first: int, count: int) -> list[int]:
         out = (C.c_uint8 * (self.mb * max(1, count)))()

@@ -106,15 +106,25 @@ int dds_bigint_product(dds_ctx* ctx, const uint8_t* operands_be, size_t width, s
 
 /* ---- device-resident columns (ciphertexts stay in HBM across requests) ----
  * A column holds `count` residues of one modulus in the engine's resident
- * format (limb-transposed radix-2^27). */
+ * format (limb-transposed radix-2^W, W = 28 or 27). */
 int dds_col_create(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, size_t capacity, dds_col** out);
 int dds_col_destroy(dds_col* col);
 /* append `count` big-endian operands (validated against the modulus) */
 int dds_col_append(dds_col* col, const uint8_t* operands_be, size_t width, size_t count);
+/* append `count` decimal rows (BigInteger.toString text, as stored in DDSSet contents) parsed on
+ * the GPU. Replaces the per-row new BigInteger(String) of the fold loops
+ * (DDSRestServer.scala:417,419,422,513). Rows are an Arrow-style string column: row i is
+ * chars[offsets[i] .. offsets[i+1]), offsets has count+1 non-decreasing entries. Syntax is
+ * BigInteger(String) radix 10 with ASCII digits: optional '+'/'-', then >= 1 digit.
+ * A negative row is stored as its residue (BigInteger.mod). Errors: DDS_E_FORMAT for a malformed
+ * row (NumberFormatException), DDS_E_RANGE for |row| >= 2^(W*S) (the column's limb capacity, a
+ * few bits above the modulus); the column is unchanged on error. */
+int dds_col_append_dec(dds_col* col, const char* chars, const uint64_t* offsets, size_t count);
 size_t dds_col_count(const dds_col* col);
-/* download rows [first, first+count) as big-endian, mod_bytes each */
+/* download rows [first, first+count) as canonical residues (x mod N), big-endian, mod_bytes each */
 int dds_col_read(dds_col* col, size_t first, size_t count, uint8_t* out);
-/* fold rows [first, first+count) (SumAll/MultAll semantics as dds_modmul_fold) */
+/* fold rows [first, first+count) (SumAll/MultAll semantics as dds_modmul_fold; a column holds
+ * residues, so a one-row fold returns that row's canonical residue) */
 int dds_col_fold(dds_col* col, size_t first, size_t count, uint8_t* out, size_t out_cap, size_t* out_len);
 /* fold rows to one un-finalised partial for multi-GPU combination:
  * partial_r27 receives limbs() words, *rows the row count it covers. */

@@ -15,7 +15,7 @@ extern "C" hipError_t CAT(KNAME, _launch)(const uint32_t* X, size_t xstride, siz
                                           uint32_t* P, size_t pstride, size_t ngroups) {
   // C: kConstCount*S constant block (only kConstN / kConstRmod are read by k_fold)
   hipLaunchKernelGGL((KNAME::ddshe::k_fold<148, 4, 28>), dim3((unsigned)((ngroups * 4 + 255) / 256)), dim3(256), 0, 0,
-                     X, xstride, count, C, n0, P, pstride, ngroups, 160);
+                     X, xstride, count, C, n0, P, pstride, ngroups);
   return hipGetLastError();
 }
 #else
