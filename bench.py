@@ -37,22 +37,58 @@ def load_key():
     return {k: int(v, 16) for k, v in raw["paillier2048_committed"].items()}
 
 
+def window_counts(e: int):
+    """(squarings, multiplies, table products) of the engine's sliding-window schedule for a
+    uniform exponent e (mirror of window_schedule in ddshe_capi.cpp)."""
+    nb = e.bit_length()
+    if nb == 0:
+        return 0, 0, 0
+    w = 1 if nb <= 24 else 3 if nb <= 80 else 4 if nb <= 240 else 5
+    i, sq, mul = nb - 1, 0, 0
+    first = True
+    while i >= 0:
+        if not (e >> i) & 1:
+            sq, i = sq + 1, i - 1
+            continue
+        j = max(i - w + 1, 0)
+        while not (e >> j) & 1:
+            j += 1
+        if not first:
+            sq, mul = sq + i - j + 1, mul + 1
+        first, i = False, j - 1
+    table = 1 + (1 if w > 1 else 0) + (2 ** (w - 1) - 1)  # x*R, x^2, odd powers
+    return sq, mul, table
+
+
+def binary_ladder_modmuls(e: int, m_bits: int = 14) -> int:
+    """SURVEY.md §8d work unit of one encryption: left-to-right binary modexp of r^n and g^m."""
+    return (e.bit_length() - 1) + (m_bits - 1) + (bin(e).count("1") - 1) + (m_bits // 2 - 1) + 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=10_000_000,
-                    help="ciphertexts per rank per step (weak scaling); whole job with --strong")
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--workload", choices=("sum", "product_filter", "encrypt_sum"), default="sum",
+                    help="sum: BASELINE.json config 2 (headline); product_filter: config 3; encrypt_sum: config 4")
+    ap.add_argument("--rows", type=int, default=None,
+                    help="rows per rank per step (weak scaling); whole job with --strong")
     ap.add_argument("--strong", action="store_true", help="split --rows over the ranks instead")
-    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--pool", type=int, default=1024)
+    ap.add_argument("--public", action="store_true", help="encrypt_sum: public-key path (no CRT)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verify", type=int, default=1, help="check Dec(result) == sum(m) on rank 0")
+    ap.add_argument("--verify", type=int, default=1, help="check the result on rank 0")
     args = ap.parse_args()
+    dflt = {"sum": (10_000_000, 20, 3, 2), "product_filter": (10_000_000, 10, 2, 3),
+            "encrypt_sum": (1_000_000, 2, 1, 4)}[args.workload]
+    args.rows = dflt[0] if args.rows is None else args.rows
+    args.steps = dflt[1] if args.steps is None else args.steps
+    args.warmup = dflt[2] if args.warmup is None else args.warmup
+    args.seed = dflt[3] if args.seed is None else args.seed
 
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -66,8 +102,6 @@ def main():
     import ddshe
     import ddshe.dist as ddist
 
-    key = load_key()
-    nsq = key["nsquare"]
     eng = ddshe.Engine(local)
     stream = torch.cuda.current_stream()
     eng.set_stream(stream.cuda_stream)
@@ -75,41 +109,30 @@ def main():
     # shard rows by contiguous key range; weak scaling: each rank owns --rows rows
     total = args.rows if args.strong else args.rows * world
     row0, mine = ddist.shard_range(total, world, rank)
-    per = (total + world - 1) // world
-    col = eng.column(nsq, max(1, mine))
+    ctx = dict(args=args, eng=eng, world=world, rank=rank, local=local, total=total, row0=row0, mine=mine,
+               per=(total + world - 1) // world, torch=torch, ddshe=ddshe, ddist=ddist)
+    wl = {"sum": SumWorkload, "product_filter": ProductFilterWorkload, "encrypt_sum": EncryptSumWorkload}[args.workload](ctx)
     t_fill = time.time()
-    if mine:
-        col.fill_paillier_synth(key["n"], key["g"], args.seed, row0, mine, args.pool)
+    wl.setup()
     torch.cuda.synchronize()
     t_fill = time.time() - t_fill
 
-    mb = (nsq.bit_length() + 7) // 8
-
-    def step():
-        if world == 1:
-            return col.fold()
-        part, rows = col.fold_partial()
-        parts, rows_all = ddist.gather_partials(part, rows, device=torch.device("cuda", local))
-        if rank != 0:
-            return None
-        return eng.combine_partials(nsq, parts, rows_all)
-
     for _ in range(args.warmup):
-        res = step()
+        res = wl.step()
     eng.set_timing(True)
     eng.reset_timing()
+    wl.reset_timers()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res = step()
+        res = wl.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     eng.set_timing(False)
-    fold_ms, fold_launches, _, fold_modmuls = eng.timing()
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -117,53 +140,302 @@ def main():
 
     out = None
     if rank == 0:
-        ok = None
-        if args.verify:
-            from oracle import homo  # checker only
-            ms = ddshe.synth_plaintexts(args.seed, 0, total)
-            ok = homo.paillier_decrypt(res, key) == int(ms.astype(np.int64).sum()) % key["n"]
-            if not ok:
-                print("VERIFY FAILED: Dec(fold) != sum(m)", file=sys.stderr)
-        adds = (total - 1) * args.steps
-        value = adds / elapsed
-        avg_launch_s = fold_ms / max(1, fold_launches) / 1e3
-        per_launch_mac = fold_modmuls / max(1, fold_launches) * MAC_PER_MODMUL
-        achieved = per_launch_mac / avg_launch_s / 1e12 if fold_launches else None
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-        if os.path.exists(tf):  # HBM bytes per launch from the committed rocprofv3 PMC passes, per row
-            pm = json.load(open(tf))
-            traffic = pm["hbm_bytes_per_launch"] / pm["rows_per_launch"] * mine  # the launch reads every row once
-        roofline = {
-            "bound": "valu-int",
-            "kernel": "k_fold<152,4> (first fold level over the rows)",
-            "achieved": achieved, "peak": PEAK_TMAC, "unit": "TMAC/s",
-            "frac": (achieved / PEAK_TMAC) if achieved else None,
-            "traffic": traffic, "traffic_unit": "bytes/launch (PMC, profiles/r01_pmc_traffic.json)",
-            "avg_launch_ms": avg_launch_s * 1e3,
-            "modmuls_per_launch": fold_modmuls / max(1, fold_launches),
-            "mac_per_modmul": MAC_PER_MODMUL,
-        }
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(col, nsq, mb, args.cpu_seconds)
-        out = {
-            "metric": "Paillier homomorphic adds/sec (2048-bit key, mod n^2)",
-            "value": value, "unit": "HomoAdd/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong" if args.strong else "weak",
-            "vs_baseline": None, "dtype": "u32", "data": "synthetic (seeded Paillier ciphertexts, committed key)",
-            "config": {"workload": "paillier_sumall_fold_10M_2048bit", "rows": total, "rows_per_gpu": per, "key_bits": key["n"].bit_length(),
-                       "modulus_bits": nsq.bit_length(), "parallelism": f"rows-sharded x{world}",
-                       "global_batch": total, "seq_len": None, "model": None},
-            "roofline": roofline, "cpu_baseline": cpu, "verified": ok, "fill_s": t_fill,
-        }
+        out = wl.report(res, elapsed)
+        out["fill_s"] = t_fill
         print(json.dumps(out))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    col.close()
+    wl.close()
     eng.close()
     return out
+
+
+class _Workload:
+    def __init__(self, ctx):
+        self.__dict__.update(ctx)
+
+    def reset_timers(self):
+        pass
+
+    def fold_or_combine(self, col, modulus):
+        """One SumAll/MultAll fold over this rank's rows; N > 1: partial, RCCL gather, combine on rank 0."""
+        if self.world == 1:
+            return col.fold()
+        part, rows = col.fold_partial()
+        parts, rows_all = self.ddist.gather_partials(part, rows, device=self.torch.device("cuda", self.local))
+        if self.rank != 0:
+            return None
+        return self.eng.combine_partials(modulus, parts, rows_all)
+
+    def fold_roofline(self, s32):
+        """Dominant kernel (first fold level) from HIP events on its launch stream."""
+        fold_ms, fold_launches, _, fold_modmuls = self.eng.timing()
+        mac = 2 * s32 * s32 + s32
+        avg_launch_s = fold_ms / max(1, fold_launches) / 1e3
+        per_launch_mac = fold_modmuls / max(1, fold_launches) * mac
+        achieved = per_launch_mac / avg_launch_s / 1e12 if fold_launches else None
+        return {"bound": "valu-int", "achieved": achieved, "peak": PEAK_TMAC, "unit": "TMAC/s",
+                "frac": (achieved / PEAK_TMAC) if achieved else None, "avg_launch_ms": avg_launch_s * 1e3,
+                "modmuls_per_launch": fold_modmuls / max(1, fold_launches), "mac_per_modmul": mac}
+
+    def common(self, metric, value, unit, elapsed, workload, extra_cfg):
+        a = self.args
+        return {
+            "metric": metric, "value": value, "unit": unit, "n_gpus": self.world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong" if a.strong else "weak", "vs_baseline": None, "dtype": "u32",
+            "config": dict({"workload": workload, "rows": self.total, "rows_per_gpu": self.per,
+                            "parallelism": f"rows-sharded x{self.world}", "global_batch": self.total,
+                            "seq_len": None, "model": None}, **extra_cfg),
+        }
+
+    def close(self):
+        pass
+
+
+class SumWorkload(_Workload):
+    """BASELINE.json config 2 (headline): SumAll HomoAdd fold over 10M ciphertexts, committed 2048-bit key."""
+
+    def setup(self):
+        self.key = load_key()
+        self.nsq = self.key["nsquare"]
+        self.col = self.eng.column(self.nsq, max(1, self.mine))
+        if self.mine:
+            self.col.fill_paillier_synth(self.key["n"], self.key["g"], self.args.seed, self.row0, self.mine,
+                                         self.args.pool)
+
+    def step(self):
+        return self.fold_or_combine(self.col, self.nsq)
+
+    def report(self, res, elapsed):
+        a, key, nsq = self.args, self.key, self.nsq
+        ok = None
+        if a.verify:
+            from oracle import homo  # checker only
+            ms = self.ddshe.synth_plaintexts(a.seed, 0, self.total)
+            ok = homo.paillier_decrypt(res, key) == int(ms.astype("int64").sum()) % key["n"]
+            if not ok:
+                print("VERIFY FAILED: Dec(fold) != sum(m)", file=sys.stderr)
+        roof = self.fold_roofline(S_32)
+        roof["kernel"] = "k_fold<148,4,28> (first fold level over the rows)"
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+        if os.path.exists(tf):  # HBM bytes per launch from the committed rocprofv3 PMC passes, per row
+            pm = json.load(open(tf))
+            traffic = pm["hbm_bytes_per_launch"] / pm["rows_per_launch"] * self.mine  # each row read once
+        roof.update(traffic=traffic, traffic_unit="bytes/launch (PMC, profiles/r01_pmc_traffic.json)")
+        cpu = None
+        if self.world == 1 and not a.no_cpu_baseline:
+            cpu = cpu_baseline(self.col, nsq, (nsq.bit_length() + 7) // 8, a.cpu_seconds)
+        out = self.common("Paillier homomorphic adds/sec (2048-bit key, mod n^2)",
+                          (self.total - 1) * a.steps / elapsed, "HomoAdd/s", elapsed,
+                          "paillier_sumall_fold_10M_2048bit",
+                          {"key_bits": key["n"].bit_length(), "modulus_bits": nsq.bit_length()})
+        out.update(data="synthetic (seeded Paillier ciphertexts, committed key)", roofline=roof, cpu_baseline=cpu,
+                   verified=ok)
+        return out
+
+    def close(self):
+        self.col.close()
+
+
+def load_keyset(name):
+    raw = json.load(open(os.path.join(ROOT, "tests", "golden", "keys.json")))
+    return {k: (int(v, 16) if k != "x509_hex" else v) for k, v in raw[name].items()}
+
+
+class ProductFilterWorkload(_Workload):
+    """BASELINE.json config 3: RSA HomoMult product (MultAll, DDSRestServer.scala:491-539) + OPE range
+    filter (SearchGt/GtEq/Lt/LtEq, :682-830) over 10M rows, synthetic 2048-bit RSA key (e = 65537).
+    Rows: c_i = (j_i+1)^e mod n with j_i = splitmix64(seed ^ splitmix64(i)) % 9999; OPE column =
+    a seeded strictly increasing int64 map of the same plaintexts; bound = the map at m = 5000."""
+
+    def setup(self):
+        import numpy as np
+        torch = self.torch
+        self.key = load_keyset("rsa2048_seed3")
+        n, e = self.key["n"], self.key["e"]
+        self.table = self.eng.modexp_batch(n, e, list(range(1, 10000)))  # HomoMult.encrypt on the GPU
+        self.col = self.eng.column(n, max(1, self.mine))
+        if self.mine:
+            self.col.fill_table_synth(self.table, self.args.seed, self.row0, self.mine)
+        rng = np.random.default_rng(self.args.seed)
+        self.ope_map = np.cumsum(rng.integers(1, 1 << 40, size=10001, dtype=np.int64)) - (1 << 52)
+        j = self.ddshe.synth_indices(self.args.seed, self.row0, self.mine, 9999)
+        self.ope_host = self.ope_map[j.astype(np.int64) + 1]
+        self.d_ope = torch.from_numpy(self.ope_host).to("cuda")
+        self.d_valid = torch.ones(max(1, self.mine), dtype=torch.uint8, device="cuda")
+        self.d_out = torch.empty(max(1, self.mine), dtype=torch.int32, device="cuda")
+        self.bound = int(self.ope_map[5000])
+        self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        self.fold_ms = self.filter_ms = 0.0
+
+    def reset_timers(self):
+        self.fold_ms = self.filter_ms = 0.0
+
+    def step(self):
+        self.ev[0].record()
+        res = self.fold_or_combine(self.col, self.key["n"])
+        self.ev[1].record()
+        counts = {op: self.eng.ope_filter_device(self.d_ope.data_ptr(), self.d_valid.data_ptr(), self.mine,
+                                                 self.bound, op, self.d_out.data_ptr())
+                  for op in ("gt", "ge", "lt", "le")}
+        self.ev[2].record()
+        self.ev[2].synchronize()
+        self.fold_ms += self.ev[0].elapsed_time(self.ev[1])
+        self.filter_ms += self.ev[1].elapsed_time(self.ev[2])
+        return res, counts
+
+    def report(self, res, elapsed):
+        import numpy as np
+        a, key = self.args, self.key
+        prod, counts = res
+        ok = None
+        if a.verify:
+            j = self.ddshe.synth_indices(a.seed, 0, self.total, 9999)
+            cnt = np.bincount(j, minlength=9999)
+            want = 1
+            for t, c in zip(self.table, cnt.tolist()):
+                if c:
+                    want = want * pow(t, c, key["n"]) % key["n"]
+            ok = prod == want
+            if self.world == 1:
+                for op, f in (("gt", np.greater), ("ge", np.greater_equal), ("lt", np.less), ("le", np.less_equal)):
+                    ok = ok and counts[op] == int(f(self.ope_host, self.bound).sum())
+            if not ok:
+                print("VERIFY FAILED", file=sys.stderr)
+        roof = self.fold_roofline(64)
+        roof["kernel"] = "k_fold<74,2,28> (first MultAll fold level, 2048-bit n)"
+        filt_s = self.filter_ms / 1e3 / (4 * a.steps)
+        matches = sum(counts.values()) / 4
+        filt_bytes = 9 * self.mine + 4 * matches  # int64 OPE value + valid byte per row, u32 id per match
+        filt = {"bound": "hbm", "achieved": filt_bytes / filt_s / 1e9, "peak": 8000.0, "unit": "GB/s",
+                "frac": filt_bytes / filt_s / 1e9 / 8000.0, "avg_filter_ms": filt_s * 1e3,
+                "algorithmic_bytes": filt_bytes, "traffic": None}
+        cpu = None
+        if self.world == 1 and not a.no_cpu_baseline:
+            n = key["n"]
+            mb = (n.bit_length() + 7) // 8
+            cpu = cpu_baseline(self.col, n, mb, a.cpu_seconds)
+            cpu["unit"] = "HomoMult/s"
+        out = self.common("RSA HomoMult product + OPE range filter rows/sec (2048-bit key)",
+                          self.total * a.steps / elapsed, "rows/s", elapsed, "rsa_multall_plus_ope_filter_10M_2048bit",
+                          {"key_bits": key["n"].bit_length(), "filters_per_step": 4})
+        out.update(data="synthetic (seeded RSA ciphertexts of U[1,10^4) plaintexts, seeded OPE map)",
+                   roofline=roof, filter_roofline=filt, cpu_baseline=cpu, verified=ok,
+                   fold_ms_per_step=self.fold_ms / a.steps, filter_ms_per_step=self.filter_ms / a.steps,
+                   homomult_per_s=(self.total - 1) * a.steps / elapsed, matches=counts)
+        return out
+
+    def close(self):
+        self.col.close()
+
+
+class EncryptSumWorkload(_Workload):
+    """BASELINE.json config 4: batched Paillier encryption (g^m r^n mod n^2, HomoAdd.encrypt,
+    SJHomoLibProvider.scala:58) + SumAll over the fresh ciphertexts, synthetic 3072-bit key
+    (n^2 6144-bit). Sub-batch: 1M rows per GPU per step (SURVEY.md §8d allows 1M). r_i from a
+    seeded device stream (dds_col_fill_random), m_i as in config 2. CRT halves unless --public."""
+
+    def setup(self):
+        torch = self.torch
+        self.key = load_keyset("paillier3072_seed4")
+        k = self.key
+        self.rcol = self.eng.column(k["nsquare"], max(1, self.mine))
+        self.out = self.eng.column(k["nsquare"], max(1, self.mine))
+        if self.mine:
+            self.rcol.fill_random(k["n"].bit_length() - 1, self.args.seed, self.row0, self.mine)
+        self.ms = self.ddshe.synth_plaintexts(self.args.seed, self.row0, self.mine)
+        self.d_m = torch.from_numpy(self.ms.astype("int32")).to("cuda")
+        self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        self.enc_ms = 0.0
+
+    def reset_timers(self):
+        self.enc_ms = 0.0
+
+    def step(self):
+        k = self.key
+        self.out.truncate(0)
+        self.ev[0].record()
+        pq = (None, None) if self.args.public else (k["p"], k["q"])
+        self.out.encrypt_paillier(self.rcol, 0, self.d_m.data_ptr(), self.mine, k["n"], k["g"], *pq)
+        self.ev[1].record()
+        res = self.fold_or_combine(self.out, k["nsquare"])
+        self.ev[1].synchronize()
+        self.enc_ms += self.ev[0].elapsed_time(self.ev[1])
+        return res
+
+    def report(self, res, elapsed):
+        a, k = self.args, self.key
+        ok = None
+        if a.verify:
+            from oracle import homo  # checker only
+            ms_all = self.ddshe.synth_plaintexts(a.seed, 0, self.total)
+            ok = homo.paillier_decrypt(res, k) == int(ms_all.astype("int64").sum()) % k["n"]
+            if self.world == 1:
+                idx = [0, self.mine // 2, self.mine - 1]
+                rs = self.rcol.read(0, self.mine) if self.mine <= 4096 else None
+                for i in idx:
+                    r = rs[i] if rs else self.rcol.read(i, 1)[0]
+                    ok = ok and self.out.read(i, 1)[0] == homo.paillier_encrypt(int(self.ms[i]), r, k)
+            if not ok:
+                print("VERIFY FAILED", file=sys.stderr)
+        enc_s = self.enc_ms / 1e3 / a.steps
+        # work actually issued per encryption: per CRT half (or the n^2 modulus with --public)
+        n = k["n"]
+        sq, mul, tab = window_counts(n)
+        m_ops = 2 * 14  # g^m_i ladder (<= 14 bits, both products issued per bit) + 1 merge
+        if a.public:
+            s32 = (k["nsquare"].bit_length() + 31) // 32
+            per_enc = [(sq + mul + tab + m_ops + 2, s32)]
+        else:
+            s32 = (k["p"].bit_length() * 2 + 31) // 32
+            per_enc = [(sq + mul + tab + m_ops + 3, s32)] * 2
+        mac_issued = sum(cnt * (2 * s * s + s) for cnt, s in per_enc)
+        achieved = mac_issued * self.mine / enc_s / 1e12
+        s_full = (k["nsquare"].bit_length() + 31) // 32
+        binary_mac = binary_ladder_modmuls(n) * (2 * s_full * s_full + s_full)
+        roof = {"bound": "valu-int", "kernel": "k_modexp_ladder (encrypt phase: pre + ladder + CRT kernels)",
+                "achieved": achieved, "peak": PEAK_TMAC, "unit": "TMAC/s", "frac": achieved / PEAK_TMAC,
+                "mac_per_encrypt_issued": mac_issued, "mac_per_encrypt_binary_ladder_n2": binary_mac,
+                "effective_vs_binary_ladder_n2": binary_mac * self.mine / enc_s / 1e12,
+                "avg_encrypt_ms": enc_s * 1e3, "traffic": None}
+        cpu = None
+        if self.world == 1 and not a.no_cpu_baseline:
+            cpu = cpu_encrypt_baseline(k, self.rcol, self.ms, a.cpu_seconds, self.out)
+        out = self.common("Paillier encryptions + HomoAdd sum /sec (3072-bit key, mod n^2)",
+                          self.total * a.steps / elapsed, "encrypt/s", elapsed,
+                          "paillier_encrypt_sum_3072bit_1M_per_gpu",
+                          {"key_bits": n.bit_length(), "modulus_bits": k["nsquare"].bit_length(),
+                           "path": "public (n, g)" if a.public else "CRT (p^2, q^2 halves)"})
+        out.update(data="synthetic (seeded r stream on device, m ~ U[0,10^4))", roofline=roof, cpu_baseline=cpu,
+                   verified=ok, encrypt_ms_per_step=self.enc_ms / a.steps)
+        return out
+
+    def close(self):
+        self.rcol.close()
+        self.out.close()
+
+
+def cpu_encrypt_baseline(k, rcol, ms, seconds, out_col=None):
+    """Paillier encryption restated on the host (oracle/homo.py: Python int pow, one thread) on
+    the first rows of the same r column; the GPU ciphertexts of those rows are compared."""
+    from oracle import homo
+    t = time.perf_counter()
+    done, i = 0, 0
+    rs = rcol.read(0, min(len(rcol), 256))
+    out = []
+    while time.perf_counter() - t < seconds and i < len(rs):
+        out.append(homo.paillier_encrypt(int(ms[i]), rs[i], k))
+        i += 1
+    dt = time.perf_counter() - t
+    done = i
+    res = {"value": done / dt, "unit": "encrypt/s", "cores": 1, "kind": "port",
+           "sample": f"first {done} rows, g^m r^n mod n^2 with Python int pow (public key), {dt:.1f}s"}
+    if out_col is not None:
+        res["gpu_matches_sample"] = out_col.read(0, done) == out
+    return res
 
 
 def cpu_baseline(col, nsq, mb, seconds):

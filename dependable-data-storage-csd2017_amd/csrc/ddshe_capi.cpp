@@ -83,7 +83,8 @@ struct HostBuf {  // pinned staging (truly asynchronous H2D)
 struct Worker {
   hipStream_t stream = nullptr;
   bool timed_fold = false;  // ev[0]/ev[1] bracket a first-level fold launch not yet accounted
-  DevBuf in, in2, x, x2, p0, p1, out, flags, y, misc, misc2;
+  DevBuf in, in2, x, x2, p0, p1, out, flags, y, misc, misc2, tab;
+  DevBuf crt[7];  // CRT encryption scratch (see encrypt_crt_device)
   hipEvent_t ev[4] = {};
   // decimal codec: double-buffered pinned chunks (chars, offsets), their device copies,
   // per-row status bytes, and the event after each slot's last use
@@ -150,6 +151,8 @@ size_t partial_words_for(const ModConsts& mc) { return (size_t)mc.S2 + 2; }
 
 }  // namespace
 
+struct CrtKey;  // CRT form of a Paillier key (encrypt_crt_device)
+
 struct dds_ctx {
   int device = 0;
   int cus = 0;
@@ -157,6 +160,7 @@ struct dds_ctx {
   std::vector<std::unique_ptr<Worker>> workers;
   std::vector<Worker*> idle;
   std::map<bn::Limbs, std::shared_ptr<ModConsts>> mods;
+  std::map<std::pair<bn::Limbs, bn::Limbs>, std::shared_ptr<CrtKey>> crt_keys;
   hipStream_t ext_stream = nullptr;
   std::atomic<bool> timing{false};
   std::mutex tmu;
@@ -818,6 +822,14 @@ int dds_col_destroy(dds_col* col) {
 
 size_t dds_col_count(const dds_col* col) { return col ? col->count : 0; }
 
+int dds_col_truncate(dds_col* col, size_t count) {
+  if (!col) return fail(DDS_E_ARG, "bad arguments");
+  std::lock_guard<std::mutex> lk(col->mu);
+  if (count > col->count) return fail(DDS_E_ARG, "truncate beyond the row count");
+  col->count = count;
+  return DDS_OK;
+}
+
 size_t dds_col_partial_words(const dds_col* col) { return col ? partial_words_for(*col->mc) : 0; }
 
 int dds_col_append(dds_col* col, const uint8_t* ops, size_t width, size_t count) {
@@ -1001,25 +1013,190 @@ int dds_combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, 
   }
 }
 
-// ---- Paillier encryption ---------------------------------------------------------
+// ---- modular exponentiation / Paillier encryption --------------------------------
 namespace {
-int encrypt_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const bn::Limbs& n, const bn::Limbs& g,
-                   const uint32_t* d_m, const uint32_t* d_rcol, size_t rstride, size_t count, uint32_t* d_out,
-                   bool use_n_exponent) {
-  (void)ctx;
+// Sliding-window schedule of a uniform exponent E (left to right): sched[0] = index of the
+// leading window's odd power, then (nsq << 16) | (idx + 1) per later window (idx + 1 == 0:
+// trailing squarings only). Returns the number of odd powers the table must hold.
+int window_schedule(const bn::Limbs& E, std::vector<uint32_t>* sched) {
+  sched->clear();
+  const int nb = (int)bn::bit_length(E);
+  if (nb == 0) return 1;
+  auto bit = [&](int i) { return (E[(size_t)i >> 5] >> (i & 31)) & 1u; };
+  // window width minimising table + multiplies (table of 2^(w-1) odd powers per row)
+  const int w = nb <= 24 ? 1 : nb <= 80 ? 3 : nb <= 240 ? 4 : 5;
+  int i = nb - 1;
+  uint32_t pending_sq = 0;
+  bool first = true;
+  while (i >= 0) {
+    if (!bit(i)) {
+      ++pending_sq;
+      --i;
+      continue;
+    }
+    int j = std::max(i - w + 1, 0);
+    while (!bit(j)) ++j;  // window [i..j] ends on a set bit
+    uint32_t v = 0;
+    for (int k = i; k >= j; --k) v = (v << 1) | bit(k);
+    const uint32_t idx = (v - 1) / 2;
+    if (first) {
+      sched->push_back(idx);
+      first = false;
+    } else {
+      pending_sq += (uint32_t)(i - j + 1);
+      sched->push_back((pending_sq << 16) | (idx + 1));
+    }
+    pending_sq = 0;
+    i = j - 1;
+  }
+  while (pending_sq > 0) {  // trailing zero bits: squarings only, <= 0xFFFF per entry
+    const uint32_t c = std::min<uint32_t>(pending_sq, 0xFFFF);
+    sched->push_back(c << 16);
+    pending_sq -= c;
+  }
+  return 1 << (w - 1);
+}
+
+// out[i] = g^m[i] * x[i]^E mod N on the device (d_m == nullptr: x[i]^E). x rows are rW,
+// fully normalised, < 2N. Processes the batch in chunks so the per-row window table
+// (nodd * S words per row) stays within ~2 GiB of HBM.
+int modexp_device(Worker* w, hipStream_t st, ModConsts& mc, const bn::Limbs& E, const bn::Limbs* g,
+                  const uint32_t* d_x, size_t xstride, const uint32_t* d_m, size_t count, uint32_t* d_out,
+                  size_t ostride) {
+  if (count == 0) return DDS_OK;
   const int S = mc.S;
-  bn::Limbs gR = bn::mod(bn::mul(bn::mod(g, mc.N), mc.Rmod), mc.N);
-  std::vector<uint32_t> gr27 = mc.rw(gR);
-  std::vector<uint32_t> nbits_words(n.begin(), n.end());
-  if (nbits_words.empty()) nbits_words.push_back(0);
-  const int nbits = use_n_exponent ? (int)bn::bit_length(n) : 0;
-  HIP_TRY(w->y.ensure((gr27.size() + nbits_words.size()) * 4));
-  HIP_TRY(hipMemcpyAsync(w->y.p, gr27.data(), gr27.size() * 4, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(w->y.as<uint32_t>() + gr27.size(), nbits_words.data(), nbits_words.size() * 4,
-                         hipMemcpyHostToDevice, st));
-  HIP_TRY(launch_modexp(S, d_rcol, rstride, d_m, count, mc.d, w->y.as<uint32_t>(), w->y.as<uint32_t>() + gr27.size(),
-                        nbits, mc.n0, d_out, st));
+  std::vector<uint32_t> sched;
+  const int nodd = window_schedule(E, &sched);
+  std::vector<uint32_t> gr;
+  if (d_m) gr = mc.rw(bn::mod(bn::mul(bn::mod(*g, mc.N), mc.Rmod), mc.N));
+  else gr.assign((size_t)S, 0);
+  const size_t sched_words = std::max<size_t>(sched.size(), 1);
+  HIP_TRY(w->y.ensure((gr.size() + sched_words) * 4));
+  uint32_t* d_gr = w->y.as<uint32_t>();
+  uint32_t* d_sched = d_gr + gr.size();
+  HIP_TRY(hipMemcpyAsync(d_gr, gr.data(), gr.size() * 4, hipMemcpyHostToDevice, st));
+  if (!sched.empty())
+    HIP_TRY(hipMemcpyAsync(d_sched, sched.data(), sched.size() * 4, hipMemcpyHostToDevice, st));
+  const size_t row_bytes = (size_t)nodd * S * 4;
+  const size_t chunk = std::min(round_up(count, 64), std::max<size_t>(64, ((size_t)2 << 30) / row_bytes / 64 * 64));
+  HIP_TRY(w->tab.ensure((size_t)nodd * S * chunk * 4));
+  for (size_t c0 = 0; c0 < count; c0 += chunk) {
+    const size_t cc = std::min(chunk, count - c0);
+    HIP_TRY(launch_modexp_pre(S, d_x + c0, xstride, cc, mc.d, mc.n0, nodd, w->tab.as<uint32_t>(), chunk, st));
+    HIP_TRY(launch_modexp_ladder(S, w->tab.as<uint32_t>(), chunk, d_m ? d_m + c0 : nullptr, cc, mc.d, d_gr, d_sched,
+                                 (int)sched.size(), mc.n0, d_out + c0, ostride, st));
+  }
   HIP_TRY(hipStreamSynchronize(st));  // host vectors above must outlive the async copies
+  return DDS_OK;
+}
+
+int encrypt_device(Worker* w, hipStream_t st, ModConsts& mc, const bn::Limbs& n, const bn::Limbs& g,
+                   const uint32_t* d_m, const uint32_t* d_rcol, size_t rstride, size_t count, uint32_t* d_out,
+                   size_t ostride, bool use_n_exponent) {
+  return modexp_device(w, st, mc, use_n_exponent ? n : bn::Limbs{}, &g, d_rcol, rstride, d_m, count, d_out, ostride);
+}
+}  // namespace
+
+// CRT form of a Paillier key (p, q): per-modulus constants of p^2, q^2, n^2 and the Garner
+// constants c1R = (q^2)^-1 R_p, c2R = -(q^2)^-1 R_p (mod p^2), q2R = q^2 R_n (mod n^2).
+struct CrtKey {
+  std::shared_ptr<ModConsts> mp, mq, mn;
+  bn::Limbs n;
+  uint32_t* d = nullptr;  // c1R | c2R (2 Sp limbs) | q2R (Sn limbs)
+  ~CrtKey() {
+    if (d) (void)hipFree(d);
+  }
+};
+
+namespace {
+int get_crt_key(dds_ctx* ctx, const bn::Limbs& p, const bn::Limbs& q, std::shared_ptr<CrtKey>* out) {
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    auto it = ctx->crt_keys.find({p, q});
+    if (it != ctx->crt_keys.end()) {
+      *out = it->second;
+      return DDS_OK;
+    }
+  }
+  if (p.empty() || q.empty() || !(p[0] & 1u) || !(q[0] & 1u) || bn::cmp(p, q) == 0 || bn::bit_length(p) < 2 ||
+      bn::bit_length(q) < 2)
+    return fail(DDS_E_ARG, "p, q must be distinct odd primes");
+  auto k = std::make_shared<CrtKey>();
+  k->n = bn::mul(p, q);
+  const bn::Limbs p2 = bn::mul(p, p), q2 = bn::mul(q, q), n2 = bn::mul(k->n, k->n);
+  auto be = [](const bn::Limbs& v) {
+    std::vector<uint8_t> b(bn::byte_length(v));
+    bn::to_be(v, b.data(), b.size());
+    return b;
+  };
+  int rc;
+  auto bp = be(p2), bq = be(q2), bn2 = be(n2);
+  if ((rc = get_mod(ctx, bp.data(), bp.size(), &k->mp)) || (rc = get_mod(ctx, bq.data(), bq.size(), &k->mq)) ||
+      (rc = get_mod(ctx, bn2.data(), bn2.size(), &k->mn)))
+    return rc;
+  // (q^2)^-1 mod p^2 = (q^2)^(p(p-1)-1) (Euler, p prime); verified below
+  const bn::Limbs phi = bn::mul(p, bn::sub(p, bn::Limbs{1}));
+  const bn::Limbs qinv = bn::powmod(bn::mod(q2, p2), bn::sub(phi, bn::Limbs{1}), p2);
+  if (bn::cmp(bn::mod(bn::mul(qinv, q2), p2), bn::Limbs{1}) != 0) return fail(DDS_E_ARG, "p, q must be distinct primes");
+  const ModConsts &mp = *k->mp, &mn = *k->mn;
+  std::vector<uint32_t> host;
+  auto put = [&](const std::vector<uint32_t>& v) { host.insert(host.end(), v.begin(), v.end()); };
+  put(mp.rw(bn::mulmod(qinv, mp.Rmod, p2)));
+  put(mp.rw(bn::mulmod(bn::sub(p2, qinv), mp.Rmod, p2)));
+  put(mn.rw(bn::mulmod(q2, mn.Rmod, n2)));
+  if (hipSetDevice(ctx->device) != hipSuccess || hipMalloc(&k->d, host.size() * 4) != hipSuccess)
+    return fail(DDS_E_NOMEM, "crt const alloc");
+  HIP_TRY(hipMemcpy(k->d, host.data(), host.size() * 4, hipMemcpyHostToDevice));
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  auto it = ctx->crt_keys.find({p, q});
+  if (it != ctx->crt_keys.end()) {
+    *out = it->second;
+    return DDS_OK;
+  }
+  if (ctx->crt_keys.size() > 16) ctx->crt_keys.clear();
+  ctx->crt_keys.emplace(std::make_pair(p, q), k);
+  *out = k;
+  return DDS_OK;
+}
+
+// The CRT halves need r < R_p, R_q (r fits the half-width limb layout) and y_q < R_p.
+bool crt_fits(const CrtKey& k) {
+  const size_t cap_p = (size_t)k.mp->S * k.mp->W - 2, cap_q = (size_t)k.mq->S * k.mq->W - 2;
+  const size_t nb = bn::bit_length(k.n);
+  return nb <= cap_p && nb <= cap_q && k.mq->bits <= cap_p;
+}
+
+// out = g^m r^n mod n^2 for rows of r (n^2 layout, values < 2^bits(n)) through the CRT halves
+int encrypt_crt_device(Worker* w, hipStream_t st, CrtKey& k, const bn::Limbs& g, const uint32_t* d_m,
+                       const uint32_t* d_r, size_t rstride, size_t count, uint32_t* d_out, size_t ostride) {
+  ModConsts &mp = *k.mp, &mq = *k.mq, &mn = *k.mn;
+  const size_t chunk = std::min<size_t>(round_up(count, 64), (size_t)1 << 20);
+  const size_t sp = (size_t)mp.S * chunk * 4, sq = (size_t)mq.S * chunk * 4, sn = (size_t)mn.S * chunk * 4;
+  const size_t sizes[7] = {sp, sq, sp, sq, sp, sn, sn};
+  for (int i = 0; i < 7; ++i) HIP_TRY(w->crt[i].ensure(sizes[i]));
+  HIP_TRY(w->flags.ensure(16));
+  HIP_TRY(hipMemsetAsync(w->flags.as<uint32_t>() + 1, 0, 4, st));
+  uint32_t* fl = w->flags.as<uint32_t>() + 1;
+  uint32_t *A = w->crt[0].as<uint32_t>(), *B = w->crt[1].as<uint32_t>(), *C = w->crt[2].as<uint32_t>(),
+           *D = w->crt[3].as<uint32_t>(), *E = w->crt[4].as<uint32_t>(), *F = w->crt[5].as<uint32_t>(),
+           *Gq = w->crt[6].as<uint32_t>();
+  int rc;
+  for (size_t c0 = 0; c0 < count; c0 += chunk) {
+    const size_t cc = std::min(chunk, count - c0);
+    HIP_TRY(launch_repack(d_r + c0, rstride, mn.S, mn.W, A, chunk, mp.S, mp.W, cc, fl, st));
+    HIP_TRY(launch_repack(d_r + c0, rstride, mn.S, mn.W, B, chunk, mq.S, mq.W, cc, fl, st));
+    if ((rc = modexp_device(w, st, mp, k.n, &g, A, chunk, d_m + c0, cc, C, chunk))) return rc;
+    if ((rc = modexp_device(w, st, mq, k.n, &g, B, chunk, d_m + c0, cc, D, chunk))) return rc;
+    HIP_TRY(launch_repack(D, chunk, mq.S, mq.W, E, chunk, mp.S, mp.W, cc, fl, st));
+    HIP_TRY(launch_crt_h(mp.S, C, E, chunk, cc, mp.d, k.d, mp.n0, A, st));
+    HIP_TRY(launch_repack(A, chunk, mp.S, mp.W, F, chunk, mn.S, mn.W, cc, fl, st));
+    HIP_TRY(launch_repack(D, chunk, mq.S, mq.W, Gq, chunk, mn.S, mn.W, cc, fl, st));
+    HIP_TRY(launch_crt_out(mn.S, F, Gq, chunk, cc, mn.d, k.d + 2 * (size_t)mp.S, mn.n0, d_out + c0, ostride, st));
+  }
+  uint32_t flags = 0;
+  HIP_TRY(hipMemcpyAsync(&flags, fl, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (flags) return fail(DDS_E_RANGE, "r does not fit below 2^bits(n)");
   return DDS_OK;
 }
 }  // namespace
@@ -1049,8 +1226,8 @@ int dds_paillier_encrypt_batch(dds_ctx* ctx, const uint8_t* n_be, size_t n_bytes
     HIP_TRY(w->misc.ensure(count * 4));
     if ((rc = ingest(ctx, w, wl.st, *mc, r_be, r_width, count, w->in, w->x.as<uint32_t>(), stride))) return rc;
     HIP_TRY(hipMemcpyAsync(w->misc.p, m, count * 4, hipMemcpyHostToDevice, wl.st));
-    if ((rc = encrypt_device(ctx, w, wl.st, *mc, n, g, w->misc.as<uint32_t>(), w->x.as<uint32_t>(), stride, count,
-                             w->x2.as<uint32_t>(), true)))
+    if ((rc = encrypt_device(w, wl.st, *mc, n, g, w->misc.as<uint32_t>(), w->x.as<uint32_t>(), stride, count,
+                             w->x2.as<uint32_t>(), stride, true)))
       return rc;
     std::vector<uint32_t> h((size_t)S * stride);
     HIP_TRY(hipMemcpy(h.data(), w->x2.p, h.size() * 4, hipMemcpyDeviceToHost));
@@ -1083,12 +1260,9 @@ int dds_modexp_batch(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, cons
     HIP_TRY(w->x.ensure((size_t)S * stride * 4));
     HIP_TRY(w->x2.ensure((size_t)S * stride * 4));
     if ((rc = ingest(ctx, w, wl.st, *mc, bases_be, width, count, w->in, w->x.as<uint32_t>(), stride))) return rc;
-    std::vector<uint32_t> ew(e.begin(), e.end());
-    if (ew.empty()) ew.push_back(0);
-    HIP_TRY(w->y.ensure(ew.size() * 4));
-    HIP_TRY(hipMemcpyAsync(w->y.p, ew.data(), ew.size() * 4, hipMemcpyHostToDevice, wl.st));
-    HIP_TRY(launch_modexp(S, w->x.as<uint32_t>(), stride, nullptr, count, mc->d, nullptr, w->y.as<uint32_t>(),
-                          (int)bn::bit_length(e), mc->n0, w->x2.as<uint32_t>(), wl.st));
+    if ((rc = modexp_device(w, wl.st, *mc, e, nullptr, w->x.as<uint32_t>(), stride, nullptr, count,
+                            w->x2.as<uint32_t>(), stride)))
+      return rc;
     std::vector<uint32_t> h((size_t)S * stride);
     HIP_TRY(hipMemcpyAsync(h.data(), w->x2.p, h.size() * 4, hipMemcpyDeviceToHost, wl.st));
     HIP_TRY(hipStreamSynchronize(wl.st));
@@ -1138,8 +1312,8 @@ int dds_col_fill_paillier_synth(dds_col* col, const uint8_t* n_be, size_t n_byte
     for (uint32_t i = 0; i < tcount; ++i) ms[i] = i;
     HIP_TRY(hipMemcpyAsync(w->x.p, ones.data(), ones.size() * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(w->in2.p, ms.data(), ms.size() * 4, hipMemcpyHostToDevice, st));
-    if ((rc = encrypt_device(col->ctx, w, st, mc, n, g, w->in2.as<uint32_t>(), w->x.as<uint32_t>(), ts, tcount,
-                             w->misc.as<uint32_t>(), false)))
+    if ((rc = encrypt_device(w, st, mc, n, g, w->in2.as<uint32_t>(), w->x.as<uint32_t>(), ts, tcount,
+                             w->misc.as<uint32_t>(), ts, false)))
       return rc;
     // pool P_j = r_j^n (encrypt with m = 0), r_j from seed
     std::vector<uint32_t> rcol((size_t)S * ps, 0), zeros(ps, 0);
@@ -1157,8 +1331,8 @@ int dds_col_fill_paillier_synth(dds_col* col, const uint8_t* n_be, size_t n_byte
     HIP_TRY(hipMemcpyAsync(w->in2.p, zeros.data(), zeros.size() * 4, hipMemcpyHostToDevice, st));
     uint32_t* pool_plain = w->misc2.as<uint32_t>();
     uint32_t* pool_mont = pool_plain + (size_t)S * ps;
-    if ((rc = encrypt_device(col->ctx, w, st, mc, n, g, w->in2.as<uint32_t>(), w->x.as<uint32_t>(), ps, pool_size,
-                             pool_plain, true)))
+    if ((rc = encrypt_device(w, st, mc, n, g, w->in2.as<uint32_t>(), w->x.as<uint32_t>(), ps, pool_size,
+                             pool_plain, ps, true)))
       return rc;
     // Montgomery form P*R mod N = pairs(P, R mod N)
     std::vector<uint32_t> rmod_col((size_t)S * ps, 0);
@@ -1170,6 +1344,135 @@ int dds_col_fill_paillier_synth(dds_col* col, const uint8_t* n_be, size_t n_byte
                               mc.n0, col->d + col->count, col->stride, st));
     HIP_TRY(hipStreamSynchronize(st));
     col->count += count;
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_paillier_encrypt_batch_crt(dds_ctx* ctx, const uint8_t* p_be, size_t p_bytes, const uint8_t* q_be,
+                                   size_t q_bytes, const uint8_t* g_be, size_t g_bytes, const uint32_t* m,
+                                   const uint8_t* r_be, size_t r_width, size_t count, uint8_t* out, size_t nsq_bytes) {
+  try {
+    if (!ctx || !p_be || !q_be || !g_be || r_width == 0 || (count && (!m || !r_be || !out)))
+      return fail(DDS_E_ARG, "bad args");
+    if (count == 0) return DDS_OK;
+    std::shared_ptr<CrtKey> k;
+    int rc = get_crt_key(ctx, bn::from_be(p_be, p_bytes), bn::from_be(q_be, q_bytes), &k);
+    if (rc) return rc;
+    ModConsts& mn = *k->mn;
+    if (nsq_bytes < mn.bytes) return fail(DDS_E_BUFSIZE, "nsq_bytes too small");
+    for (size_t i = 0; i < count; ++i) {  // r in [1, n): the CRT halves need r < 2^bits(n)
+      bn::Limbs r = bn::from_be(r_be + i * r_width, r_width);
+      if (r.empty() || bn::cmp(r, k->n) >= 0) return fail(DDS_E_RANGE, "r must be in [1, n)");
+    }
+    const bn::Limbs g = bn::from_be(g_be, g_bytes);
+    WorkerLease wl(ctx);
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    const int S = mn.S;
+    const size_t stride = round_up(count, 64);
+    HIP_TRY(w->x.ensure((size_t)S * stride * 4));
+    HIP_TRY(w->x2.ensure((size_t)S * stride * 4));
+    HIP_TRY(w->misc.ensure(count * 4));
+    if ((rc = ingest(ctx, w, wl.st, mn, r_be, r_width, count, w->in, w->x.as<uint32_t>(), stride))) return rc;
+    HIP_TRY(hipMemcpyAsync(w->misc.p, m, count * 4, hipMemcpyHostToDevice, wl.st));
+    if (crt_fits(*k))
+      rc = encrypt_crt_device(w, wl.st, *k, g, w->misc.as<uint32_t>(), w->x.as<uint32_t>(), stride, count,
+                              w->x2.as<uint32_t>(), stride);
+    else  // unbalanced factors: public-key path (same result)
+      rc = encrypt_device(w, wl.st, mn, k->n, g, w->misc.as<uint32_t>(), w->x.as<uint32_t>(), stride, count,
+                          w->x2.as<uint32_t>(), stride, true);
+    if (rc) return rc;
+    std::vector<uint32_t> h((size_t)S * stride);
+    HIP_TRY(hipMemcpy(h.data(), w->x2.p, h.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> limbs(S);
+    for (size_t i = 0; i < count; ++i) {
+      for (int l = 0; l < S; ++l) limbs[l] = h[(size_t)l * stride + i];
+      if (!bn::to_be(mn.value(limbs.data()), out + i * nsq_bytes, nsq_bytes))
+        return fail(DDS_E_RANGE, "result does not fit");
+    }
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_col_fill_table_synth(dds_col* col, const uint8_t* table_be, size_t width, size_t tcount, uint64_t seed,
+                             uint64_t row0, size_t count) {
+  try {
+    if (!col || !table_be || width == 0 || tcount == 0 || tcount > 0xFFFFFFFFu) return fail(DDS_E_ARG, "bad arguments");
+    std::lock_guard<std::mutex> lk(col->mu);
+    if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
+    WorkerLease wl(col->ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    ModConsts& mc = *col->mc;
+    const size_t ts = round_up(tcount, 64);
+    HIP_TRY(w->misc.ensure((size_t)mc.S * ts * 4));
+    if ((rc = ingest(col->ctx, w, wl.st, mc, table_be, width, tcount, w->in, w->misc.as<uint32_t>(), ts))) return rc;
+    HIP_TRY(launch_gather_rows(w->misc.as<uint32_t>(), ts, (uint32_t)tcount, mc.S, seed, row0, count,
+                               col->d + col->count, col->stride, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    col->count += count;
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_col_fill_random(dds_col* col, size_t bits, uint64_t seed, uint64_t row0, size_t count) {
+  try {
+    if (!col || bits == 0) return fail(DDS_E_ARG, "bad arguments");
+    std::lock_guard<std::mutex> lk(col->mu);
+    if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
+    if (bits >= col->mc->bits) return fail(DDS_E_RANGE, "random rows must stay below the modulus");
+    WorkerLease wl(col->ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    HIP_TRY(launch_fill_random(col->d + col->count, col->stride, col->mc->S, col->mc->W, seed, row0, count, (int)bits,
+                               wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    col->count += count;
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_col_encrypt_paillier(dds_col* out, dds_col* rcol, size_t r_first, const uint32_t* d_m, size_t count,
+                             const uint8_t* n_be, size_t n_bytes, const uint8_t* g_be, size_t g_bytes,
+                             const uint8_t* p_be, size_t p_bytes, const uint8_t* q_be, size_t q_bytes) {
+  try {
+    if (!out || !rcol || !n_be || !g_be || (count && !d_m) || (!p_be) != (!q_be)) return fail(DDS_E_ARG, "bad args");
+    if (count == 0) return DDS_OK;
+    if (r_first + count > rcol->count) return fail(DDS_E_ARG, "r rows out of range");
+    std::unique_lock<std::mutex> lk(out->mu, std::defer_lock);
+    std::unique_lock<std::mutex> lr(rcol->mu, std::defer_lock);
+    if (out == rcol) return fail(DDS_E_ARG, "out and r columns must differ");
+    std::lock(lk, lr);
+    if (out->count + count > out->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
+    const bn::Limbs n = bn::from_be(n_be, n_bytes), g = bn::from_be(g_be, g_bytes);
+    const bn::Limbs nsq = bn::mul(n, n);
+    if (bn::cmp(nsq, out->mc->N) != 0 || bn::cmp(nsq, rcol->mc->N) != 0)
+      return fail(DDS_E_ARG, "columns must be over n^2");
+    std::shared_ptr<CrtKey> k;
+    int rc;
+    if (p_be) {
+      if ((rc = get_crt_key(out->ctx, bn::from_be(p_be, p_bytes), bn::from_be(q_be, q_bytes), &k))) return rc;
+      if (bn::cmp(k->n, n) != 0) return fail(DDS_E_ARG, "p*q != n");
+    }
+    WorkerLease wl(out->ctx);
+    if ((rc = wl.acquire())) return rc;
+    uint32_t* dst = out->d + out->count;
+    const uint32_t* r = rcol->d + r_first;
+    if (k && crt_fits(*k))
+      rc = encrypt_crt_device(wl.w, wl.st, *k, g, d_m, r, rcol->stride, count, dst, out->stride);
+    else
+      rc = encrypt_device(wl.w, wl.st, *out->mc, n, g, d_m, r, rcol->stride, count, dst, out->stride, true);
+    if (rc) return rc;
+    out->count += count;
     return DDS_OK;
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");

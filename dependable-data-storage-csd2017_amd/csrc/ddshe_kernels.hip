@@ -9,7 +9,7 @@
 //   MultAll fold  dds/http/DDSRestServer.scala:491-539  -> k_fold + k_finalize
 //   Sum / Mult    dds/http/DDSRestServer.scala:355-395, 447-490 -> k_pairs
 //   Search{Gt,GtEq,Lt,LtEq} DDSRestServer.scala:682-830 -> k_ope_count / k_ope_scatter
-//   HomoAdd.encrypt  utils/SJHomoLibProvider.scala:58 -> k_modexp (also HomoMult.encrypt, :59)
+//   HomoAdd.encrypt  utils/SJHomoLibProvider.scala:58 -> k_modexp_pre + k_modexp_ladder (also HomoMult.encrypt, :59)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -117,13 +117,18 @@ __global__ void __launch_bounds__(256, 2) k_pairs(const uint32_t* __restrict__ A
 }
 
 // ------------------------------------------------------------------------------
-// batched modular exponentiation: c_i = g^m_i * r_i^E mod N
+// batched modular exponentiation: c_i = g^m_i * x_i^E mod N
 //   Paillier encrypt (HomoAdd.encrypt, SJHomoLibProvider.scala:58): N = n^2, E = n
 //   RSA encrypt / generic x^E (HomoMult.encrypt, :59): g^m term disabled (m == nullptr)
-// Left-to-right binary ladder over the uniform exponent E; every operand of a
-// Montgomery product is staged in the group's LDS slot (2 x S dwords), so the
-// registers hold only acc, N and the 64-bit accumulators (no spills).
-// consts: N, Rmod (=1 in Montgomery form), R2, One; gR = g*R mod N (uniform, global).
+// E is uniform over the batch, so the host turns it into a sliding-window schedule
+// (window w <= 5) that every group walks in lockstep — no divergence:
+//   k_modexp_pre:    Tab[j] = x^(2j+1)·R mod N, j < nodd (per row, limb-transposed in HBM)
+//   k_modexp_ladder: acc = Tab[sched[0]]; per entry: `nsq` squarings (operand staged in the
+//                    group's LDS slot, read by ds_read broadcast), then acc·Tab[idx] streamed
+//                    from HBM through the fold's buffer-descriptor path; then g^m_i (binary,
+//                    per-row exponent < 2^14), leave Montgomery form, canonicalise.
+// A 3072-bit E costs 3072 squarings + ~512 multiplies + 16 table products instead of
+// 3072 + ~1536 for the binary ladder (-22 % Montgomery products).
 // ------------------------------------------------------------------------------
 template <int S, int TPI, int W>
 __device__ __forceinline__ void store_lds(uint32_t* dst, const uint32_t (&a)[S / TPI], int r) {
@@ -132,11 +137,9 @@ __device__ __forceinline__ void store_lds(uint32_t* dst, const uint32_t (&a)[S /
 }
 
 template <int S, int TPI, int W>
-__global__ void __launch_bounds__(256, 2) k_modexp(const uint32_t* __restrict__ Rcol, size_t stride,
-                                                const uint32_t* __restrict__ m, size_t count,
-                                                const uint32_t* __restrict__ consts, const uint32_t* __restrict__ gR,
-                                                const uint32_t* __restrict__ ebits, int nbits, uint32_t n0,
-                                                uint32_t* __restrict__ O) {
+__global__ void __launch_bounds__(256, 2) k_modexp_pre(const uint32_t* __restrict__ Xcol, size_t xstride,
+                                                    size_t count, const uint32_t* __restrict__ consts, uint32_t n0,
+                                                    int nodd, uint32_t* __restrict__ Tab, size_t tstride) {
   using G = Grp<S, TPI, W>;
   using M = Mont<S, TPI, W>;
   constexpr int L = G::L;
@@ -144,21 +147,60 @@ __global__ void __launch_bounds__(256, 2) k_modexp(const uint32_t* __restrict__ 
   G g;
   const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
   if (grp >= count) return;
-  uint32_t* sq = lds + (size_t)(threadIdx.x / TPI) * 2 * S;  // group-private operand slot
+  uint32_t* x1 = lds + (size_t)(threadIdx.x / TPI) * 2 * S;  // group-private operand slots
+  uint32_t* x2 = x1 + S;
+  uint32_t n[L], acc[L];
+  g.load_vec(n, consts + kConstN * S);
+  g.load_col(acc, Xcol, xstride, grp);
+  M::mul_col(acc, n, consts + kConstR2 * S, 1, 0, n0, g.top, g.bottom);  // x*R
+  M::normalize(acc, g.bottom);
+  g.store_col(acc, Tab, tstride, grp);
+  if (nodd == 1) return;
+  store_lds<S, TPI, W>(x1, acc, g.r);
+  M::mul_lds(acc, n, x1, n0, g.top, g.bottom);  // x^2*R
+  M::normalize(acc, g.bottom);
+  store_lds<S, TPI, W>(x2, acc, g.r);
+#pragma unroll
+  for (int l = 0; l < L; ++l) acc[l] = x1[g.r * L + l];
+  for (int j = 1; j < nodd; ++j) {
+    M::mul_lds(acc, n, x2, n0, g.top, g.bottom);
+    M::normalize(acc, g.bottom);
+    g.store_col(acc, Tab + (size_t)j * S * tstride, tstride, grp);
+  }
+}
+
+// sched[0] = index of the leading window; sched[1..nsched) = (nsq << 16) | (idx + 1),
+// idx + 1 == 0: squarings only. nsched == 0: E == 0 (x^0 = 1).
+template <int S, int TPI, int W>
+__global__ void __launch_bounds__(256, 2) k_modexp_ladder(const uint32_t* __restrict__ Tab, size_t tstride,
+                                                       const uint32_t* __restrict__ m, size_t count,
+                                                       const uint32_t* __restrict__ consts,
+                                                       const uint32_t* __restrict__ gR,
+                                                       const uint32_t* __restrict__ sched, int nsched, uint32_t n0,
+                                                       uint32_t* __restrict__ O, size_t ostride) {
+  using G = Grp<S, TPI, W>;
+  using M = Mont<S, TPI, W>;
+  constexpr int L = G::L;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  G g;
+  const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
+  if (grp >= count) return;
+  uint32_t* sq = lds + (size_t)(threadIdx.x / TPI) * 2 * S;  // group-private operand slots
   uint32_t* xs = sq + S;
   uint32_t n[L], acc[L];
   g.load_vec(n, consts + kConstN * S);
-  // x = r*R (Montgomery form), kept in LDS for the ladder's multiplies
-  g.load_col(acc, Rcol, stride, grp);
-  M::mul_col(acc, n, consts + kConstR2 * S, 1, 0, n0, g.top, g.bottom);
-  M::normalize(acc, g.bottom);
-  store_lds<S, TPI, W>(xs, acc, g.r);
-  g.load_vec(acc, consts + kConstRmod * S);  // 1*R
-  for (int i = nbits - 1; i >= 0; --i) {
-    M::normalize(acc, g.bottom);
-    store_lds<S, TPI, W>(sq, acc, g.r);
-    M::mul_lds(acc, n, sq, n0, g.top, g.bottom);  // square
-    if ((ebits[i >> 5] >> (i & 31)) & 1u) M::mul_lds(acc, n, xs, n0, g.top, g.bottom);
+  if (nsched > 0) g.load_col(acc, Tab + (size_t)sched[0] * S * tstride, tstride, grp);
+  else g.load_vec(acc, consts + kConstRmod * S);  // 1*R
+  for (int k = 1; k < nsched; ++k) {
+    const uint32_t e = sched[k];
+    for (uint32_t s = e >> 16; s > 0; --s) {
+      M::normalize(acc, g.bottom);
+      store_lds<S, TPI, W>(sq, acc, g.r);
+      M::mul_lds(acc, n, sq, n0, g.top, g.bottom);
+    }
+    if (e & 0xFFFFu)
+      M::mul_col(acc, n, Tab + (size_t)((e & 0xFFFFu) - 1) * S * tstride, tstride, (uint32_t)grp, n0, g.top,
+                 g.bottom);
   }
   if (m != nullptr) {
     // g^m_i: per-row exponent; the ladder length is the wave's max bit length so the
@@ -167,7 +209,7 @@ __global__ void __launch_bounds__(256, 2) k_modexp(const uint32_t* __restrict__ 
     uint32_t wb = mi ? 32u - (uint32_t)__builtin_clz(mi) : 0u;
     for (int off = 32; off >= 1; off >>= 1) wb = max(wb, (uint32_t)__shfl_xor((int)wb, off));
     M::normalize(acc, g.bottom);
-    store_lds<S, TPI, W>(xs, acc, g.r);  // park r^E*R in xs; acc is reused for g^m
+    store_lds<S, TPI, W>(xs, acc, g.r);  // park x^E*R in xs; acc is reused for g^m
     g.load_vec(acc, consts + kConstRmod * S);
     for (int i = (int)wb - 1; i >= 0; --i) {
       M::normalize(acc, g.bottom);
@@ -178,12 +220,12 @@ __global__ void __launch_bounds__(256, 2) k_modexp(const uint32_t* __restrict__ 
       for (int l = 0; l < L; ++l) sq[g.r * L + l] = sel[g.r * L + l];
       M::mul_lds(acc, n, sq, n0, g.top, g.bottom);
     }
-    // acc = (g^m R) * (r^E R) * R^-1
+    // acc = (g^m R) * (x^E R) * R^-1
     M::mul_lds(acc, n, xs, n0, g.top, g.bottom);
   }
   M::mul_col(acc, n, consts + kConstOne * S, 1, 0, n0, g.top, g.bottom);  // leave Montgomery form
   g.canon(acc, n);
-  g.store_col(acc, O, stride, grp);
+  g.store_col(acc, O, ostride, grp);
 }
 
 // ------------------------------------------------------------------------------
@@ -222,6 +264,123 @@ __global__ void __launch_bounds__(256, 2) k_synth_rows(const uint32_t* __restric
   M::mul_col(a, n, P, pstride, bi, n0, g.top, g.bottom);
   g.canon(a, n);
   g.store_col(a, X, xstride, grp);
+}
+
+// ------------------------------------------------------------------------------
+// CRT Paillier encryption (HomoAdd.encrypt with the private factors, SJHomoLibProvider.scala:58;
+// the client holds the whole PaillierKey, :43-50): c = g^m r^n mod n^2 is computed as
+// y_p = g^m r^n mod p^2 and y_q mod q^2 (half-width moduli: 1/4 of the Montgomery work
+// each), then Garner: h = (y_p - y_q)·(q^2)^-1 mod p^2, c = y_q + q^2·h  (< n^2, exact).
+// ------------------------------------------------------------------------------
+// radix change between rW layouts, one row per thread: dst (Sd limbs of Wd bits) <- src
+// (Ss limbs of Ws bits). flags[0] |= 1 if the value does not fit in Sd limbs.
+__global__ void k_repack(const uint32_t* __restrict__ src, size_t sstride, int Ss, int Ws, uint32_t* __restrict__ dst,
+                         size_t dstride, int Sd, int Wd, size_t count, uint32_t* __restrict__ flags) {
+  const size_t row = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= count) return;
+  const uint32_t dmask = (1u << Wd) - 1u;
+  uint64_t buf = 0;
+  int nb = 0, l = 0;
+  bool over = false;
+  for (int i = 0; i < Ss; ++i) {
+    buf |= (uint64_t)src[(size_t)i * sstride + row] << nb;
+    nb += Ws;
+    while (nb >= Wd) {
+      const uint32_t v = (uint32_t)buf & dmask;
+      if (l < Sd) dst[(size_t)l * dstride + row] = v;
+      else over |= v != 0;
+      ++l;
+      buf >>= Wd;
+      nb -= Wd;
+    }
+  }
+  for (; l < Sd; ++l) {
+    dst[(size_t)l * dstride + row] = (uint32_t)buf & dmask;
+    buf >>= Wd;
+  }
+  if (over || buf != 0) atomicOr(flags, 1u);
+}
+
+// h = MonPro(y_p, c1R) + MonPro(y_q, c2R) with c1R = (q^2)^-1·R, c2R = -(q^2)^-1·R (mod p^2)
+//   == (y_p - y_q)·(q^2)^-1 (mod p^2); canonical h < p^2. The first term is parked in H
+//   (each lane re-reads only its own limbs) so one bignum is live at a time.
+template <int S, int TPI, int W>
+__global__ void __launch_bounds__(256, 2) k_crt_h(const uint32_t* __restrict__ Yp, const uint32_t* __restrict__ Yq,
+                                               size_t stride, size_t count, const uint32_t* __restrict__ consts,
+                                               const uint32_t* __restrict__ c12, uint32_t n0, uint32_t* H) {
+  using G = Grp<S, TPI, W>;
+  using M = Mont<S, TPI, W>;
+  constexpr int L = G::L;
+  G g;
+  const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
+  if (grp >= count) return;
+  uint32_t n[L], u[L];
+  g.load_vec(n, consts + kConstN * S);
+  g.load_col(u, Yp, stride, grp);
+  M::mul_col(u, n, c12, 1, 0, n0, g.top, g.bottom);
+  g.canon(u, n);
+  g.store_col(u, H, stride, grp);
+  g.load_col(u, Yq, stride, grp);
+  M::mul_col(u, n, c12 + S, 1, 0, n0, g.top, g.bottom);
+  g.canon(u, n);
+#pragma unroll
+  for (int l = 0; l < L; ++l) u[l] += H[(size_t)(g.r * L + l) * stride + grp];  // < 2 p^2, limbs < 2^(W+1)
+  g.canon(u, n);
+  g.store_col(u, H, stride, grp);
+}
+
+// c = canon(MonPro(h, q^2·R mod n^2)) + y_q   (h·q^2 + y_q < n^2: no reduction)
+template <int S, int TPI, int W>
+__global__ void __launch_bounds__(256, 2) k_crt_out(const uint32_t* __restrict__ Hn, const uint32_t* __restrict__ Yqn,
+                                                 size_t stride, size_t count, const uint32_t* __restrict__ consts,
+                                                 const uint32_t* __restrict__ q2R, uint32_t n0,
+                                                 uint32_t* __restrict__ O, size_t ostride) {
+  using G = Grp<S, TPI, W>;
+  using M = Mont<S, TPI, W>;
+  constexpr int L = G::L;
+  G g;
+  const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
+  if (grp >= count) return;
+  uint32_t n[L], a[L];
+  g.load_vec(n, consts + kConstN * S);
+  g.load_col(a, Hn, stride, grp);
+  M::mul_col(a, n, q2R, 1, 0, n0, g.top, g.bottom);
+  g.canon(a, n);
+  asm volatile("" ::: "memory");  // keep the y_q loads after the product (no extra live bignum)
+#pragma unroll
+  for (int l = 0; l < L; ++l) a[l] += Yqn[(size_t)(g.r * L + l) * stride + grp];
+  M::normalize(a, g.bottom);
+  g.store_col(a, O, ostride, grp);
+}
+
+// seeded r column (bench / tests): limb l of row i = splitmix64(splitmix64(seed ^ (row0+i)) + l),
+// truncated to `bits` bits (r < 2^bits), lowest bit forced to 1 (r != 0)
+__global__ void k_fill_random(uint32_t* __restrict__ X, size_t stride, int S, int W, uint64_t seed, uint64_t row0,
+                              size_t count, int bits) {
+  const size_t row = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= count) return;
+  const uint64_t h = splitmix64(seed ^ (row0 + row));
+  const uint32_t mask = (1u << W) - 1u;
+  for (int l = 0; l < S; ++l) {
+    const int lo = l * W;
+    uint32_t v = 0;
+    if (lo < bits) {
+      v = (uint32_t)splitmix64(h + (uint64_t)l) & mask;
+      if (bits - lo < W) v &= (1u << (bits - lo)) - 1u;
+      if (l == 0) v |= 1u;
+    }
+    X[(size_t)l * stride + row] = v;
+  }
+}
+
+// table-driven synthetic rows: X[row] = T[h % tcount], h = splitmix64(seed ^ splitmix64(row0+row))
+// (RSA config 3: T[j] = (j+1)^e mod n, DDSDataGenerator.scala:274 plaintexts)
+__global__ void k_gather_rows(const uint32_t* __restrict__ T, size_t tstride, uint32_t tcount, int S, uint64_t seed,
+                              uint64_t row0, size_t count, uint32_t* __restrict__ X, size_t xstride) {
+  const size_t row = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= count) return;
+  const uint32_t j = (uint32_t)(splitmix64(seed ^ splitmix64(row0 + row)) % tcount);
+  for (int l = 0; l < S; ++l) X[(size_t)l * xstride + row] = T[(size_t)l * tstride + j];
 }
 
 // ------------------------------------------------------------------------------
@@ -417,12 +576,16 @@ Shape pick_shape(size_t mod_bits) {
 }
 
 Shape tail_shape(const Shape& main) {
-  for (int i = 0; i < 4; ++i)
+  static_assert(sizeof(kShapes) == sizeof(kTail), "one tail shape per main shape");
+  for (size_t i = 0; i < sizeof(kShapes) / sizeof(kShapes[0]); ++i)
     if (kShapes[i].S == main.S) return kTail[i];
   return Shape{0, 0, 0};
 }
 
-size_t max_modulus_bits() { return (size_t)kShapes[3].W * kShapes[3].S - 2; }
+size_t max_modulus_bits() {
+  const Shape& s = kShapes[sizeof(kShapes) / sizeof(kShapes[0]) - 1];
+  return (size_t)s.W * s.S - 2;
+}
 
 hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, int W, const uint32_t* n2x,
                             uint32_t* X, size_t stride, uint32_t* flags, hipStream_t st) {
@@ -478,13 +641,21 @@ hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stri
   return hipGetLastError();
 }
 
-hipError_t launch_modexp(int S, const uint32_t* Rcol, size_t stride, const uint32_t* m, size_t count,
-                         const uint32_t* consts, const uint32_t* gR, const uint32_t* ebits, int nbits, uint32_t n0,
-                         uint32_t* O, hipStream_t st) {
+hipError_t launch_modexp_pre(int S, const uint32_t* Xcol, size_t xstride, size_t count, const uint32_t* consts,
+                             uint32_t n0, int nodd, uint32_t* Tab, size_t tstride, hipStream_t st) {
   if (count == 0) return hipSuccess;
-  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_modexp<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256),
-                                     (256 / TPI) * 2 * S * 4, st, Rcol, stride, m, count, consts, gR, ebits, nbits,
-                                     n0, O));
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_modexp_pre<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256),
+                                     (256 / TPI) * 2 * S * 4, st, Xcol, xstride, count, consts, n0, nodd, Tab, tstride));
+  return hipGetLastError();
+}
+
+hipError_t launch_modexp_ladder(int S, const uint32_t* Tab, size_t tstride, const uint32_t* m, size_t count,
+                                const uint32_t* consts, const uint32_t* gR, const uint32_t* sched, int nsched,
+                                uint32_t n0, uint32_t* O, size_t ostride, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_modexp_ladder<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256),
+                                     (256 / TPI) * 2 * S * 4, st, Tab, tstride, m, count, consts, gR, sched, nsched,
+                                     n0, O, ostride));
   return hipGetLastError();
 }
 
@@ -494,6 +665,46 @@ hipError_t launch_synth_rows(int S, const uint32_t* T, size_t tstride, uint32_t 
   if (count == 0) return hipSuccess;
   DDSHE_SWITCH(S, hipLaunchKernelGGL((k_synth_rows<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), 0, st, T, tstride,
                                      tcount, P, pstride, pcount, seed, row0, count, consts, n0, X, xstride));
+  return hipGetLastError();
+}
+
+hipError_t launch_repack(const uint32_t* src, size_t sstride, int Ss, int Ws, uint32_t* dst, size_t dstride, int Sd,
+                         int Wd, size_t count, uint32_t* flags, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_repack, dim3(grid_for(count)), dim3(256), 0, st, src, sstride, Ss, Ws, dst, dstride, Sd, Wd,
+                     count, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_crt_h(int S, const uint32_t* Yp, const uint32_t* Yq, size_t stride, size_t count,
+                        const uint32_t* consts, const uint32_t* c12, uint32_t n0, uint32_t* H, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_crt_h<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), 0, st, Yp, Yq,
+                                     stride, count, consts, c12, n0, H));
+  return hipGetLastError();
+}
+
+hipError_t launch_crt_out(int S, const uint32_t* Hn, const uint32_t* Yqn, size_t stride, size_t count,
+                          const uint32_t* consts, const uint32_t* q2R, uint32_t n0, uint32_t* O, size_t ostride,
+                          hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_crt_out<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), 0, st, Hn, Yqn,
+                                     stride, count, consts, q2R, n0, O, ostride));
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_random(uint32_t* X, size_t stride, int S, int W, uint64_t seed, uint64_t row0, size_t count,
+                              int bits, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fill_random, dim3(grid_for(count)), dim3(256), 0, st, X, stride, S, W, seed, row0, count, bits);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(const uint32_t* T, size_t tstride, uint32_t tcount, int S, uint64_t seed, uint64_t row0,
+                              size_t count, uint32_t* X, size_t xstride, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_rows, dim3(grid_for(count)), dim3(256), 0, st, T, tstride, tcount, S, seed, row0, count, X,
+                     xstride);
   return hipGetLastError();
 }
 

@@ -32,10 +32,27 @@ hipError_t launch_finalize_tail(int S, const uint32_t* P, size_t pstride, const 
                                 uint32_t n0, uint32_t* out, hipStream_t st);
 hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stride, size_t count,
                         const uint32_t* consts, uint32_t n0, uint32_t* O, hipStream_t st);
-// c_i = g^m_i * r_i^E mod N (m == nullptr: r_i^E); gR = g*R mod N in rW limbs
-hipError_t launch_modexp(int S, const uint32_t* Rcol, size_t stride, const uint32_t* m, size_t count,
-                         const uint32_t* consts, const uint32_t* gR, const uint32_t* ebits, int nbits, uint32_t n0,
-                         uint32_t* O, hipStream_t st);
+// modexp table: Tab[j] = x^(2j+1)*R mod N (j < nodd), entry j at Tab + j*S*tstride
+hipError_t launch_modexp_pre(int S, const uint32_t* Xcol, size_t xstride, size_t count, const uint32_t* consts,
+                             uint32_t n0, int nodd, uint32_t* Tab, size_t tstride, hipStream_t st);
+// O = g^m_i * x_i^E mod N (m == nullptr: x_i^E) from the table and the host-built window schedule;
+// gR = g*R mod N in rW limbs
+hipError_t launch_modexp_ladder(int S, const uint32_t* Tab, size_t tstride, const uint32_t* m, size_t count,
+                                const uint32_t* consts, const uint32_t* gR, const uint32_t* sched, int nsched,
+                                uint32_t n0, uint32_t* O, size_t ostride, hipStream_t st);
+// CRT encryption pieces (see ddshe_kernels.hip): radix change between rW layouts (flags[0] |= 1 on
+// overflow), h = (y_p - y_q)(q^2)^-1 mod p^2 (c12 = c1R | c2R, 2*S limbs), c = h*q^2 + y_q
+hipError_t launch_repack(const uint32_t* src, size_t sstride, int Ss, int Ws, uint32_t* dst, size_t dstride, int Sd,
+                         int Wd, size_t count, uint32_t* flags, hipStream_t st);
+hipError_t launch_crt_h(int S, const uint32_t* Yp, const uint32_t* Yq, size_t stride, size_t count,
+                        const uint32_t* consts, const uint32_t* c12, uint32_t n0, uint32_t* H, hipStream_t st);
+hipError_t launch_crt_out(int S, const uint32_t* Hn, const uint32_t* Yqn, size_t stride, size_t count,
+                          const uint32_t* consts, const uint32_t* q2R, uint32_t n0, uint32_t* O, size_t ostride,
+                          hipStream_t st);
+hipError_t launch_fill_random(uint32_t* X, size_t stride, int S, int W, uint64_t seed, uint64_t row0, size_t count,
+                              int bits, hipStream_t st);
+hipError_t launch_gather_rows(const uint32_t* T, size_t tstride, uint32_t tcount, int S, uint64_t seed, uint64_t row0,
+                              size_t count, uint32_t* X, size_t xstride, hipStream_t st);
 hipError_t launch_synth_rows(int S, const uint32_t* T, size_t tstride, uint32_t tcount, const uint32_t* P,
                              size_t pstride, uint32_t pcount, uint64_t seed, uint64_t row0, size_t count,
                              const uint32_t* consts, uint32_t n0, uint32_t* X, size_t xstride, hipStream_t st);

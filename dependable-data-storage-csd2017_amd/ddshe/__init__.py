@@ -36,7 +36,8 @@ EXPORTS = [
     "dds_col_create", "dds_col_destroy", "dds_col_append", "dds_col_append_dec", "dds_col_count", "dds_col_read", "dds_col_fold",
     "dds_col_fold_partial", "dds_col_partial_words", "dds_combine_partials", "dds_col_fill_paillier_synth",
     "dds_ope_filter", "dds_ope_filter_device", "dds_paillier_encrypt_batch", "dds_modexp_batch", "dds_sum_all_dec",
-    "dds_mult_all_dec",
+    "dds_mult_all_dec", "dds_paillier_encrypt_batch_crt", "dds_col_fill_random", "dds_col_encrypt_paillier",
+    "dds_col_fill_table_synth", "dds_col_truncate",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -71,6 +72,7 @@ _sig("dds_col_destroy", C.c_int, C.c_void_p)
 _sig("dds_col_append", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz)
 _sig("dds_col_append_dec", C.c_int, C.c_void_p, C.c_char_p, C.POINTER(C.c_uint64), _sz)
 _sig("dds_col_count", _sz, C.c_void_p)
+_sig("dds_col_truncate", C.c_int, C.c_void_p, _sz)
 _sig("dds_col_read", C.c_int, C.c_void_p, _sz, _sz, _u8p)
 _sig("dds_col_fold", C.c_int, C.c_void_p, _sz, _sz, _u8p, _sz, _szp)
 _sig("dds_col_fold_partial", C.c_int, C.c_void_p, _sz, _sz, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64))
@@ -83,6 +85,12 @@ _sig("dds_ope_filter", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int
 _sig("dds_ope_filter_device", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int64, C.c_int, C.c_void_p, _szp)
 _sig("dds_paillier_encrypt_batch", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, C.POINTER(C.c_uint32),
      C.c_char_p, _sz, _sz, _u8p, _sz)
+_sig("dds_paillier_encrypt_batch_crt", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, C.c_char_p, _sz,
+     C.POINTER(C.c_uint32), C.c_char_p, _sz, _sz, _u8p, _sz)
+_sig("dds_col_fill_table_synth", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz, C.c_uint64, C.c_uint64, _sz)
+_sig("dds_col_fill_random", C.c_int, C.c_void_p, _sz, C.c_uint64, C.c_uint64, _sz)
+_sig("dds_col_encrypt_paillier", C.c_int, C.c_void_p, C.c_void_p, _sz, C.c_void_p, _sz, C.c_char_p, _sz, C.c_char_p,
+     _sz, C.c_char_p, _sz, C.c_char_p, _sz)
 _sig("dds_modexp_batch", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, C.c_char_p, _sz, _sz, _u8p)
 for _n in ("dds_sum_all_dec", "dds_mult_all_dec"):
     _sig(_n, C.c_int, C.c_void_p, C.POINTER(C.c_char_p), _sz, C.c_char_p, C.c_char_p, _sz, _szp)
@@ -251,6 +259,19 @@ class Engine:
         raw = bytes(out)
         return [int.from_bytes(raw[i * nb:(i + 1) * nb], "big") for i in range(len(rs))]
 
+    def paillier_encrypt_batch_crt(self, p: int, q: int, g: int, ms, rs) -> list[int]:
+        """HomoAdd.encrypt(m, PaillierKey) with the private factors: same ciphertexts, CRT halves."""
+        ms = np.ascontiguousarray(ms, dtype=np.uint32)
+        rs = [int(r) for r in rs]
+        nb, rw = nbytes((p * q) ** 2), max([1] + [nbytes(r) for r in rs])
+        out = (C.c_uint8 * (nb * max(1, len(rs))))()
+        _check(_lib.dds_paillier_encrypt_batch_crt(self._h, int_to_be(p, nbytes(p)), nbytes(p), int_to_be(q, nbytes(q)),
+                                                   nbytes(q), int_to_be(g, nbytes(g)), nbytes(g),
+                                                   ms.ctypes.data_as(C.POINTER(C.c_uint32)), ints_to_be(rs, rw), rw,
+                                                   len(rs), out, nb), "dds_paillier_encrypt_batch_crt")
+        raw = bytes(out)
+        return [int.from_bytes(raw[i * nb:(i + 1) * nb], "big") for i in range(len(rs))]
+
     def modexp_batch(self, modulus: int, exponent: int, bases) -> list[int]:
         """out[i] = bases[i]^exponent mod modulus (HomoMult.encrypt for an RSA key)."""
         bases = [int(x) for x in bases]
@@ -354,6 +375,30 @@ class Column:
                                                 nbytes(g), seed, row0, count, pool), "dds_col_fill_paillier_synth")
 
 
+    def truncate(self, count: int = 0):
+        _check(_lib.dds_col_truncate(self._h, count), "dds_col_truncate")
+
+    def fill_table_synth(self, table, seed: int, row0: int, count: int):
+        """Append rows table[h_i % len(table)] (dds_col_fill_table_synth); see synth_indices."""
+        table = [int(x) for x in table]
+        _check(_lib.dds_col_fill_table_synth(self._h, ints_to_be(table, self.mb), self.mb, len(table), seed, row0,
+                                             count), "dds_col_fill_table_synth")
+
+    def fill_random(self, bits: int, seed: int, row0: int, count: int):
+        """Append seeded odd random rows < 2^bits (dds_col_fill_random)."""
+        _check(_lib.dds_col_fill_random(self._h, bits, seed, row0, count), "dds_col_fill_random")
+
+    def encrypt_paillier(self, rcol: "Column", r_first: int, d_m: int, count: int, n: int, g: int,
+                         p: int | None = None, q: int | None = None):
+        """Append Enc(m_i; r_i) for rows [r_first, r_first+count) of rcol; d_m: device uint32 pointer."""
+        pb = int_to_be(p, nbytes(p)) if p else None
+        qb = int_to_be(q, nbytes(q)) if q else None
+        _check(_lib.dds_col_encrypt_paillier(self._h, rcol._h, r_first, C.c_void_p(d_m), count,
+                                             int_to_be(n, nbytes(n)), nbytes(n), int_to_be(g, nbytes(g)), nbytes(g),
+                                             pb, nbytes(p) if p else 0, qb, nbytes(q) if q else 0),
+               "dds_col_encrypt_paillier")
+
+
 # ---- synthetic-row plaintexts (mirror of k_synth_rows' index derivation) ----
 _M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
 
@@ -366,11 +411,17 @@ def _splitmix64_np(x: np.ndarray) -> np.ndarray:
         return x ^ (x >> np.uint64(31))
 
 
-def synth_plaintexts(seed: int, row0: int, count: int, chunk: int = 1 << 22) -> np.ndarray:
-    """m_i of dds_col_fill_paillier_synth rows [row0, row0+count) (uint32)."""
+def synth_indices(seed: int, row0: int, count: int, modulo: int, chunk: int = 1 << 22) -> np.ndarray:
+    """splitmix64(seed ^ splitmix64(row)) % modulo for rows [row0, row0+count) (uint32): the index
+    derivation of k_synth_rows / k_gather_rows."""
     out = np.empty(count, dtype=np.uint32)
     for s in range(0, count, chunk):
         idx = np.arange(row0 + s, row0 + min(count, s + chunk), dtype=np.uint64)
         h = _splitmix64_np(np.uint64(seed) ^ _splitmix64_np(idx))
-        out[s:s + len(idx)] = (h % np.uint64(10000)).astype(np.uint32)
+        out[s:s + len(idx)] = (h % np.uint64(modulo)).astype(np.uint32)
     return out
+
+
+def synth_plaintexts(seed: int, row0: int, count: int, chunk: int = 1 << 22) -> np.ndarray:
+    """m_i of dds_col_fill_paillier_synth rows [row0, row0+count) (uint32)."""
+    return synth_indices(seed, row0, count, 10000, chunk)

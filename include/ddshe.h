@@ -121,6 +121,8 @@ int dds_col_append(dds_col* col, const uint8_t* operands_be, size_t width, size_
  * few bits above the modulus); the column is unchanged on error. */
 int dds_col_append_dec(dds_col* col, const char* chars, const uint64_t* offsets, size_t count);
 size_t dds_col_count(const dds_col* col);
+/* drop rows [count, dds_col_count) (the storage is kept for later appends) */
+int dds_col_truncate(dds_col* col, size_t count);
 /* download rows [first, first+count) as canonical residues (x mod N), big-endian, mod_bytes each */
 int dds_col_read(dds_col* col, size_t first, size_t count, uint8_t* out);
 /* fold rows [first, first+count) (SumAll/MultAll semantics as dds_modmul_fold; a column holds
@@ -159,11 +161,35 @@ int dds_paillier_encrypt_batch(dds_ctx* ctx, const uint8_t* n_be, size_t n_bytes
                                const uint32_t* m, const uint8_t* r_be, size_t r_width, size_t count, uint8_t* out,
                                size_t nsq_bytes);
 
+/* HomoAdd.encrypt(m, PaillierKey) with the private factors p, q (the client holds the whole
+ * key, SJHomoLibProvider.scala:43-58): bit-identical to dds_paillier_encrypt_batch with n = p*q,
+ * computed mod p^2 and q^2 and recombined (Garner) — half-width Montgomery work. r_i in [1, n)
+ * (DDS_E_RANGE otherwise); p, q distinct odd primes (DDS_E_ARG otherwise). */
+int dds_paillier_encrypt_batch_crt(dds_ctx* ctx, const uint8_t* p_be, size_t p_bytes, const uint8_t* q_be,
+                                   size_t q_bytes, const uint8_t* g_be, size_t g_bytes, const uint32_t* m,
+                                   const uint8_t* r_be, size_t r_width, size_t count, uint8_t* out, size_t nsq_bytes);
+
 /* Batched modular exponentiation out[i] = base[i]^exp mod modulus (mod_bytes each):
  * HomoMult.encrypt(pk, m) = m^e mod n (SJHomoLibProvider.scala:59) and decrypt-side
  * checks. Bases are validated like fold operands. */
 int dds_modexp_batch(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint8_t* exp_be, size_t exp_bytes,
                      const uint8_t* bases_be, size_t width, size_t count, uint8_t* out);
+
+/* ---- device-resident batched encryption (BASELINE.json config 4) --------------
+ * dds_col_fill_random: append `count` seeded random rows r < 2^bits (odd, so r != 0):
+ *   limb l of row i = splitmix64(splitmix64(seed ^ (row0+i)) + l) in the column's rW layout.
+ * dds_col_encrypt_paillier: append Enc(m_i; r_i) = g^m_i r_i^n mod n^2 for the `count` rows of
+ *   rcol starting at r_first (r_i in [1, n)), m on the device (d_m, uint32). Both columns are
+ *   over n^2. p, q (both or neither): CRT path, same result. */
+int dds_col_fill_random(dds_col* col, size_t bits, uint64_t seed, uint64_t row0, size_t count);
+/* Table-driven synthetic rows (BASELINE.json config 3): append row i = table[h_i % tcount],
+ * h_i = splitmix64(seed ^ splitmix64(row0+i)); table: tcount big-endian values of `width` bytes
+ * (e.g. table[j] = (j+1)^e mod n, RSA ciphertexts of the DDSDataGenerator.scala:274 plaintexts). */
+int dds_col_fill_table_synth(dds_col* col, const uint8_t* table_be, size_t width, size_t tcount, uint64_t seed,
+                             uint64_t row0, size_t count);
+int dds_col_encrypt_paillier(dds_col* out, dds_col* rcol, size_t r_first, const uint32_t* d_m, size_t count,
+                             const uint8_t* n_be, size_t n_bytes, const uint8_t* g_be, size_t g_bytes,
+                             const uint8_t* p_be, size_t p_bytes, const uint8_t* q_be, size_t q_bytes);
 
 /* ---- route-level entry points on decimal strings (what the Scala route holds) ----
  * values: count NUL-terminated decimal strings (contents(position) of the rows that
