@@ -70,8 +70,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
-    ap.add_argument("--workload", choices=("sum", "product_filter", "encrypt_sum"), default="sum",
-                    help="sum: BASELINE.json config 2 (headline); product_filter: config 3; encrypt_sum: config 4")
+    ap.add_argument("--workload", choices=("sum", "product_filter", "encrypt_sum", "order"), default="sum",
+                    help="sum: BASELINE.json config 2 (headline); product_filter: config 3; encrypt_sum: config 4; "
+                         "order: OrderLS over the config-3 OPE column (SURVEY.md §8f rank 2)")
     ap.add_argument("--rows", type=int, default=None,
                     help="rows per rank per step (weak scaling); whole job with --strong")
     ap.add_argument("--strong", action="store_true", help="split --rows over the ranks instead")
@@ -83,7 +84,7 @@ def main():
     ap.add_argument("--verify", type=int, default=1, help="check the result on rank 0")
     args = ap.parse_args()
     dflt = {"sum": (10_000_000, 20, 3, 2), "product_filter": (10_000_000, 10, 2, 3),
-            "encrypt_sum": (1_000_000, 2, 1, 4)}[args.workload]
+            "encrypt_sum": (1_000_000, 2, 1, 4), "order": (10_000_000, 10, 2, 3)}[args.workload]
     args.rows = dflt[0] if args.rows is None else args.rows
     args.steps = dflt[1] if args.steps is None else args.steps
     args.warmup = dflt[2] if args.warmup is None else args.warmup
@@ -111,7 +112,8 @@ def main():
     row0, mine = ddist.shard_range(total, world, rank)
     ctx = dict(args=args, eng=eng, world=world, rank=rank, local=local, total=total, row0=row0, mine=mine,
                per=(total + world - 1) // world, torch=torch, ddshe=ddshe, ddist=ddist)
-    wl = {"sum": SumWorkload, "product_filter": ProductFilterWorkload, "encrypt_sum": EncryptSumWorkload}[args.workload](ctx)
+    wl = {"sum": SumWorkload, "product_filter": ProductFilterWorkload, "encrypt_sum": EncryptSumWorkload,
+          "order": OrderWorkload}[args.workload](ctx)
     t_fill = time.time()
     wl.setup()
     torch.cuda.synchronize()
@@ -307,11 +309,14 @@ class ProductFilterWorkload(_Workload):
                 print("VERIFY FAILED", file=sys.stderr)
         roof = self.fold_roofline(64)
         roof["kernel"] = "k_fold<74,2,28> (first MultAll fold level, 2048-bit n)"
-        filt_s = self.filter_ms / 1e3 / (4 * a.steps)
+        _, _, filt_dev_ms, _ = self.eng.timing()  # HIP events around the filter launches (device time)
+        filt_s = filt_dev_ms / 1e3 / (4 * a.steps)
         matches = sum(counts.values()) / 4
         filt_bytes = 9 * self.mine + 4 * matches  # int64 OPE value + valid byte per row, u32 id per match
         filt = {"bound": "hbm", "achieved": filt_bytes / filt_s / 1e9, "peak": 8000.0, "unit": "GB/s",
                 "frac": filt_bytes / filt_s / 1e9 / 8000.0, "avg_filter_ms": filt_s * 1e3,
+                "kernel": "k_ope_count + k_ope_scatter (device time, HIP events on the launch stream)",
+                "avg_filter_call_ms": self.filter_ms / (4 * a.steps),
                 "algorithmic_bytes": filt_bytes, "traffic": None}
         cpu = None
         if self.world == 1 and not a.no_cpu_baseline:
@@ -416,6 +421,62 @@ class EncryptSumWorkload(_Workload):
     def close(self):
         self.rcol.close()
         self.out.close()
+
+
+class OrderWorkload(_Workload):
+    """OrderLS (DDSRestServer.scala:541-573) over a 10M-row OPE column: int64 values of a seeded
+    increasing map of U[1,10^4) plaintexts (many ties, as the generator's), 5 % of rows lacking
+    the position. Each rank orders its own shard (the route's result is per shard; a k-way merge
+    of shard orders is not part of this measurement)."""
+
+    def setup(self):
+        import numpy as np
+        torch = self.torch
+        rng = np.random.default_rng(self.args.seed)
+        ope_map = np.cumsum(rng.integers(1, 1 << 40, size=10001, dtype=np.int64)) - (1 << 52)
+        j = self.ddshe.synth_indices(self.args.seed, self.row0, self.mine, 9999)
+        self.col = ope_map[j.astype(np.int64) + 1]
+        self.valid = (rng.random(self.mine) > 0.05).astype(np.uint8)
+        self.d_col = torch.from_numpy(self.col).to("cuda")
+        self.d_valid = torch.from_numpy(self.valid).to("cuda")
+        self.d_out = torch.empty(max(1, self.mine), dtype=torch.int32, device="cuda")
+
+    def step(self):
+        self.eng.ope_order_device(self.d_col.data_ptr(), self.d_valid.data_ptr(), self.mine, True,
+                                  self.d_out.data_ptr())
+        return None
+
+    def report(self, res, elapsed):
+        import numpy as np
+        a = self.args
+        ok = None
+        if a.verify and self.world == 1:
+            idx = np.arange(self.mine)
+            hold, rest = idx[self.valid != 0], idx[self.valid == 0]
+            want = np.concatenate([hold[np.argsort(~self.col[hold], kind="stable")], rest])
+            ok = bool(np.array_equal(self.d_out.cpu().numpy().view(np.uint32), want))
+            if not ok:
+                print("VERIFY FAILED", file=sys.stderr)
+        step_s = elapsed / a.steps
+        alg = 13 * self.mine  # read key + valid byte, write one row id
+        roof = {"bound": "hbm", "kernel": "k_rs_hist/k_rs_scan/k_rs_scatter (8 LSD passes)",
+                "achieved": alg / step_s / 1e9, "peak": 8000.0, "unit": "GB/s", "frac": alg / step_s / 1e9 / 8000.0,
+                "algorithmic_bytes": alg, "issued_bytes_est": self.mine * (8 * 36 + 8 + 1),
+                "traffic": None}
+        cpu = None
+        if self.world == 1 and not a.no_cpu_baseline:
+            t = time.perf_counter()
+            idx = np.arange(self.mine)
+            hold = idx[self.valid != 0]
+            _ = np.concatenate([hold[np.argsort(~self.col[hold], kind="stable")], idx[self.valid == 0]])
+            dt = time.perf_counter() - t
+            cpu = {"value": self.mine / dt, "unit": "rows/s", "cores": 1, "kind": "port",
+                   "sample": f"all {self.mine} rows, numpy stable argsort (the reference sorts with sortWith), {dt:.2f}s"}
+        out = self.common("OPE OrderLS rows/sec (int64 keys, stable)", self.total * a.steps / elapsed, "rows/s",
+                          elapsed, "ope_orderls_10M", {})
+        out.update(data="synthetic (seeded OPE map of U[1,10^4) plaintexts, 5% rows lacking the position)",
+                   dtype="int64", roofline=roof, cpu_baseline=cpu, verified=ok)
+        return out
 
 
 def cpu_encrypt_baseline(k, rcol, ms, seconds, out_col=None):

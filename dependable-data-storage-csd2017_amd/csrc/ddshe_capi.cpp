@@ -1491,12 +1491,10 @@ int dds_ope_filter_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_v
     int rc;
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
-    const size_t nb = ope_blocks(n);
-    HIP_TRY(w->misc.ensure(nb * 4));
+    HIP_TRY(w->misc.ensure(ope_scratch_bytes(n)));
     HIP_TRY(w->flags.ensure(16));
     record_time(ctx, w, wl.st, true, 2);
-    HIP_TRY(launch_ope_filter(d_col, d_valid, n, bound, op, w->misc.as<uint32_t>(), w->flags.as<uint64_t>(), d_out,
-                              wl.st));
+    HIP_TRY(launch_ope_filter(d_col, d_valid, n, bound, op, w->misc.p, w->flags.as<uint64_t>(), d_out, wl.st));
     record_time(ctx, w, wl.st, false, 2);
     uint64_t total = 0;
     HIP_TRY(hipMemcpyAsync(&total, w->flags.p, 8, hipMemcpyDeviceToHost, wl.st));
@@ -1539,6 +1537,51 @@ int dds_ope_filter(dds_ctx* ctx, const int64_t* col, const uint8_t* valid, size_
     if ((rc = dds_ope_filter_device(ctx, dcol, dvalid, n, bound, op, dout, &got))) return rc;
     if (got) HIP_TRY(hipMemcpy(out_idx, dout, got * 4, hipMemcpyDeviceToHost));
     *out_n = got;
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+// ---- OPE ordering (OrderLS / OrderSL) ---------------------------------------------
+int dds_ope_order_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_valid, size_t n, int descending,
+                         uint32_t* d_out_idx) {
+  try {
+    if (!ctx || (n && (!d_col || !d_out_idx))) return fail(DDS_E_ARG, "bad arguments");
+    if (n > 0xFFFFFFFFull) return fail(DDS_E_ARG, "row index exceeds 32 bits");
+    if (n == 0) return DDS_OK;
+    WorkerLease wl(ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    HIP_TRY(w->tab.ensure(rs_scratch_bytes(n)));
+    HIP_TRY(launch_ope_order(d_col, d_valid, n, descending ? 1 : 0, w->tab.p, d_out_idx, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_ope_order(dds_ctx* ctx, const int64_t* col, const uint8_t* valid, size_t n, int descending,
+                  uint32_t* out_idx) {
+  try {
+    if (!ctx || (n && (!col || !out_idx))) return fail(DDS_E_ARG, "bad arguments");
+    if (n == 0) return DDS_OK;
+    WorkerLease wl(ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    HIP_TRY(w->in.ensure(n * 8));
+    HIP_TRY(w->in2.ensure(n));
+    HIP_TRY(w->out.ensure(n * 4));
+    HIP_TRY(hipMemcpyAsync(w->in.p, col, n * 8, hipMemcpyHostToDevice, wl.st));
+    if (valid) HIP_TRY(hipMemcpyAsync(w->in2.p, valid, n, hipMemcpyHostToDevice, wl.st));
+    HIP_TRY(w->tab.ensure(rs_scratch_bytes(n)));
+    HIP_TRY(launch_ope_order(w->in.as<int64_t>(), valid ? w->in2.as<uint8_t>() : nullptr, n, descending ? 1 : 0,
+                             w->tab.p, w->out.as<uint32_t>(), wl.st));
+    HIP_TRY(hipMemcpyAsync(out_idx, w->out.p, n * 4, hipMemcpyDeviceToHost, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
     return DDS_OK;
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");

@@ -8,7 +8,7 @@
 //   SumAll fold   dds/http/DDSRestServer.scala:397-446  -> k_fold + k_finalize
 //   MultAll fold  dds/http/DDSRestServer.scala:491-539  -> k_fold + k_finalize
 //   Sum / Mult    dds/http/DDSRestServer.scala:355-395, 447-490 -> k_pairs
-//   Search{Gt,GtEq,Lt,LtEq} DDSRestServer.scala:682-830 -> k_ope_count / k_ope_scatter
+//   Search{Gt,GtEq,Lt,LtEq} DDSRestServer.scala:682-830 -> k_ope_count + k_ope_scatter
 //   HomoAdd.encrypt  utils/SJHomoLibProvider.scala:58 -> k_modexp_pre + k_modexp_ladder (also HomoMult.encrypt, :59)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -397,92 +397,138 @@ __device__ __forceinline__ bool ope_pred(int64_t c, int64_t b, int op) {
 }
 
 constexpr int kOpeBlock = 256;
-constexpr int kOpeItems = 16;  // rows per thread
+constexpr int kOpeItems = 32;  // rows per thread (bits of the per-thread match mask)
 constexpr size_t kOpeTile = (size_t)kOpeBlock * kOpeItems;
 
+// Row layout of a tile: group k (< kOpeGroups) covers rows [k*1024, (k+1)*1024); thread tid owns
+// the 4 consecutive rows k*1024 + 4*tid + j (j < 4), bit 4k+j of its match mask. Full tiles of an
+// aligned column read 4 rows as two 16-byte loads (+ one 4-byte load of their valid bytes); the
+// last tile (or an unaligned column) uses scalar loads with the index clamped to n-1. All loads are
+// issued before any predicate so they are in flight together.
+constexpr int kOpeGroups = kOpeItems / 4;
+
+template <bool HasValid>
 __device__ __forceinline__ uint32_t ope_thread_mask(const int64_t* __restrict__ col, const uint8_t* __restrict__ valid,
-                                                    size_t n, int64_t bound, int op, size_t base) {
-  uint32_t mask = 0;
+                                                    size_t n, int64_t bound, int op, size_t tile, bool vec) {
+  const size_t t0 = tile * kOpeTile + 4 * (size_t)threadIdx.x;
+  int64_t c[kOpeItems];
+  uint32_t v[kOpeGroups];
+  if (vec && t0 + (kOpeGroups - 1) * 4 * kOpeBlock + 3 < n) {
 #pragma unroll
-  for (int k = 0; k < kOpeItems; ++k) {
-    const size_t i = base + (size_t)k * kOpeBlock;
-    if (i < n) {
-      const bool v = valid ? valid[i] != 0 : true;
-      if (v && ope_pred(col[i], bound, op)) mask |= 1u << k;
+    for (int k = 0; k < kOpeGroups; ++k) {
+      const size_t r = t0 + (size_t)k * 4 * kOpeBlock;
+      typedef long long i64x2 __attribute__((ext_vector_type(2)));
+      const i64x2* p = reinterpret_cast<const i64x2*>(col + r);
+      const i64x2 x = __builtin_nontemporal_load(p), y = __builtin_nontemporal_load(p + 1);
+      c[4 * k] = x.x;
+      c[4 * k + 1] = x.y;
+      c[4 * k + 2] = y.x;
+      c[4 * k + 3] = y.y;
+      if constexpr (HasValid) v[k] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(valid + r));
+      else v[k] = 0x01010101u;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kOpeGroups; ++k) {
+      uint32_t vk = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t r = t0 + (size_t)k * 4 * kOpeBlock + j;
+        const size_t i = min(r, n - 1);
+        c[4 * k + j] = col[i];
+        const uint32_t vb = HasValid ? (uint32_t)valid[i] : 1u;
+        vk |= (r < n ? vb : 0u) << (8 * j);
+      }
+      v[k] = vk;
     }
   }
+  uint32_t mask = 0;
+#pragma unroll
+  for (int k = 0; k < kOpeGroups; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (((v[k] >> (8 * j)) & 0xFFu) && ope_pred(c[4 * k + j], bound, op)) mask |= 1u << (4 * k + j);
   return mask;
 }
 
+// Stable compaction in two launches (no inter-block waiting: a decoupled look-back's tile-state
+// probes are agent-scope atomics that cross the 8 XCDs' L2s, and measured slower here):
+//   k_ope_count:   reads the column once; per-thread match mask (32 rows -> 1 u32, 1/72 of the
+//                  column bytes) and per-tile match count;
+//   k_ope_scatter: each block sums the counts of the tiles before it (<= a few thousand u32 from
+//                  L2), reloads its masks, ranks its matches in row order (k*256 + tid) and
+//                  writes the row ids; the last block writes the total.
+template <bool HasValid>
 __global__ void __launch_bounds__(kOpeBlock) k_ope_count(const int64_t* __restrict__ col,
                                                          const uint8_t* __restrict__ valid, size_t n, int64_t bound,
-                                                         int op, uint32_t* __restrict__ block_counts) {
+                                                         int op, uint32_t* __restrict__ masks,
+                                                         uint32_t* __restrict__ counts) {
   __shared__ uint32_t wsum[kOpeBlock / 64];
-  const size_t base = (size_t)blockIdx.x * kOpeTile + threadIdx.x;
-  const uint32_t c = __builtin_popcount(ope_thread_mask(col, valid, n, bound, op, base));
-  uint32_t s = c;
+  const size_t t = (size_t)blockIdx.x * kOpeBlock + threadIdx.x;
+  const bool vec = ((uintptr_t)col % 16 == 0) && (!HasValid || (uintptr_t)valid % 4 == 0);
+  const uint32_t m = ope_thread_mask<HasValid>(col, valid, n, bound, op, blockIdx.x, vec);
+  masks[t] = m;
+  uint32_t s = __builtin_popcount(m);
   for (int off = 32; off >= 1; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int w = 0; w < kOpeBlock / 64; ++w) t += wsum[w];
-    block_counts[blockIdx.x] = t;
+    uint32_t c = 0;
+    for (int w = 0; w < kOpeBlock / 64; ++w) c += wsum[w];
+    counts[blockIdx.x] = c;
   }
 }
 
-// exclusive scan of block counts (single block; nblocks up to 64k handled by a serial tail per thread)
-__global__ void __launch_bounds__(1024) k_ope_scan(uint32_t* __restrict__ counts, size_t nblocks,
-                                                   uint64_t* __restrict__ total) {
-  __shared__ uint64_t part[1024];
-  const size_t per = (nblocks + 1023) / 1024;
-  const size_t b0 = threadIdx.x * per, b1 = min(nblocks, b0 + per);
-  uint64_t s = 0;
-  for (size_t b = b0; b < b1; ++b) s += counts[b];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    uint64_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  uint64_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-  for (size_t b = b0; b < b1; ++b) {
-    uint32_t c = counts[b];
-    counts[b] = (uint32_t)run;
-    run += c;
-  }
-  if (threadIdx.x == 1023) *total = part[1023];
-}
-
-__global__ void __launch_bounds__(kOpeBlock) k_ope_scatter(const int64_t* __restrict__ col,
-                                                           const uint8_t* __restrict__ valid, size_t n, int64_t bound,
-                                                           int op, const uint32_t* __restrict__ block_offsets,
-                                                           uint32_t* __restrict__ out) {
-  // Stable order: rows of a tile are numbered k*256 + tid, so scan over (k, tid) in row order.
-  __shared__ uint32_t wtot[kOpeItems][kOpeBlock / 64];
+__global__ void __launch_bounds__(kOpeBlock) k_ope_scatter(const uint32_t* __restrict__ masks,
+                                                           const uint32_t* __restrict__ counts,
+                                                           uint32_t* __restrict__ out, uint64_t* __restrict__ total) {
+  constexpr int kWaves = kOpeBlock / 64;
+  __shared__ uint32_t wtot[kOpeGroups][kWaves];
+  __shared__ uint64_t s_part[kWaves];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const size_t base = (size_t)blockIdx.x * kOpeTile + tid;
-  const uint32_t mask = ope_thread_mask(col, valid, n, bound, op, base);
-  uint32_t before_in_wave[kOpeItems];
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const size_t tile = blockIdx.x;
+  const size_t t0 = tile * kOpeTile + 4 * (size_t)tid;
+  const uint32_t mask = masks[tile * kOpeBlock + tid];
+  // exclusive prefix of this tile: sum of the counts of tiles [0, tile)
+  uint64_t pre = 0;
+  for (size_t t = tid; t < tile; t += kOpeBlock) pre += counts[t];
+  for (int off = 32; off >= 1; off >>= 1) pre += (uint64_t)__shfl_xor((long long)pre, off);
+  if (lane == 0) s_part[wid] = pre;
+  // per group: matches of the lanes below me in my wave (4 bit-ballots), wave total
+  uint32_t below[kOpeGroups];
 #pragma unroll
-  for (int k = 0; k < kOpeItems; ++k) {
-    const uint64_t bal = __ballot((mask >> k) & 1u);
-    before_in_wave[k] = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) wtot[k][wid] = (uint32_t)__popcll(bal);
+  for (int k = 0; k < kOpeGroups; ++k) {
+    uint32_t b = 0, tot = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t bal = __ballot((mask >> (4 * k + j)) & 1u);
+      b += (uint32_t)__popcll(bal & lt);
+      tot += (uint32_t)__popcll(bal);
+    }
+    below[k] = b;
+    if (lane == 0) wtot[k][wid] = tot;
   }
   __syncthreads();
-  uint32_t off = block_offsets[blockIdx.x];
+  uint64_t off = 0;
 #pragma unroll
-  for (int k = 0; k < kOpeItems; ++k) {
-    uint32_t pre = 0;
-    for (int w = 0; w < kOpeBlock / 64; ++w) pre += (w < wid) ? wtot[k][w] : 0u;
-    if ((mask >> k) & 1u) out[off + pre + before_in_wave[k]] = (uint32_t)(base + (size_t)k * kOpeBlock);
-    uint32_t tot = 0;
-    for (int w = 0; w < kOpeBlock / 64; ++w) tot += wtot[k][w];
+  for (int w = 0; w < kWaves; ++w) off += s_part[w];
+#pragma unroll
+  for (int k = 0; k < kOpeGroups; ++k) {
+    uint32_t pw = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      pw += (w < wid) ? wtot[k][w] : 0u;
+      tot += wtot[k][w];
+    }
+    const uint32_t q = (mask >> (4 * k)) & 0xFu;
+    uint64_t dst = off + pw + below[k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((q >> j) & 1u) out[dst++] = (uint32_t)(t0 + (size_t)k * 4 * kOpeBlock + j);
     off += tot;
   }
+  if (tid == 0 && tile == gridDim.x - 1) *total = off;
 }
 
 // ------------------------------------------------------------------------------
@@ -710,14 +756,21 @@ hipError_t launch_gather_rows(const uint32_t* T, size_t tstride, uint32_t tcount
 
 size_t ope_blocks(size_t n) { return (n + kOpeTile - 1) / kOpeTile; }
 
-hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op,
-                             uint32_t* block_counts, uint64_t* total, uint32_t* out, hipStream_t st) {
+size_t ope_scratch_bytes(size_t n) { return ope_blocks(n) * (4 + 4 * kOpeBlock) + 8; }
+
+hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
+                             uint64_t* total, uint32_t* out, hipStream_t st) {
   const size_t nb = ope_blocks(n);
   if (nb == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ope_count, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, bound, op, block_counts);
-  hipLaunchKernelGGL(k_ope_scan, dim3(1), dim3(1024), 0, st, block_counts, nb, total);
-  hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, bound, op, block_counts,
-                     out);
+  uint32_t* counts = (uint32_t*)scratch;
+  uint32_t* masks = counts + nb;
+  if (valid)
+    hipLaunchKernelGGL(k_ope_count<true>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, bound, op, masks,
+                       counts);
+  else
+    hipLaunchKernelGGL(k_ope_count<false>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, bound, op, masks,
+                       counts);
+  hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, masks, counts, out, total);
   return hipGetLastError();
 }
 

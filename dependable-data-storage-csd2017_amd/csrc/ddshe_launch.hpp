@@ -57,8 +57,13 @@ hipError_t launch_synth_rows(int S, const uint32_t* T, size_t tstride, uint32_t 
                              size_t pstride, uint32_t pcount, uint64_t seed, uint64_t row0, size_t count,
                              const uint32_t* consts, uint32_t n0, uint32_t* X, size_t xstride, hipStream_t st);
 size_t ope_blocks(size_t n);
-hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op,
-                             uint32_t* block_counts, uint64_t* total, uint32_t* out, hipStream_t st);
+size_t ope_scratch_bytes(size_t n);  // per-tile match counts + per-thread match masks
+hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
+                             uint64_t* total, uint32_t* out, hipStream_t st);
+// OPE ordering (ddshe_sort.hip): stable radix sort of the int64 column -> row ids
+size_t rs_scratch_bytes(size_t n);
+hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
+                            uint32_t* out_ids, hipStream_t st);
 hipError_t launch_plain_sum(const uint32_t* X, size_t stride, size_t count, int S, size_t nthreads, uint64_t* part,
                             uint64_t* out, hipStream_t st);
 // unbounded product tree level: rows (2p, 2p+1) of A[count][len] (radix 2^16 in u32)

@@ -1,0 +1,227 @@
+// OPE ordering (OrderLS / OrderSL, DDSRestServer.scala:541-606): stable LSD radix sort of the
+// int64 OPE column (ciphertexts are Java Long, SJHomoLibProvider.scala:55; sort key
+// `contents(position).toLong`, :562 / :595) carrying the row ids.
+//   OrderLS: descending (`a > b`), rows lacking the position (`length-1 < position`) last;
+//   OrderSL: ascending  (`a < b`), rows lacking the position first.
+// scala's sortWith is a stable merge sort, so equal keys keep their input order: LSD radix with
+// a stable per-tile rank reproduces that. Descending order sorts ~key (still stable for ties).
+//
+// Per 8-bit digit pass (8 passes; the last one has 257 buckets: the validity of the row moves it
+// to the end / front): k_rs_hist (per-tile digit counts, digit-major) -> k_rs_scan_digits (per-digit
+// scan over tiles, one block per digit) + k_rs_scan_base (digit bases) -> k_rs_scatter (stable rank inside the tile: each wave walks a contiguous
+// quarter of the tile, peers with equal digits are found with 9 ballots, per-wave digit counters
+// in LDS). HBM traffic per pass: 12 B/row read twice (hist + scatter) + 12 B/row written.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ddshe_launch.hpp"
+
+namespace ddshe {
+
+constexpr int kRsBlock = 256;
+constexpr int kRsWaves = kRsBlock / 64;
+constexpr int kRsItems = 16;                      // rows per lane
+constexpr size_t kRsTile = (size_t)kRsBlock * kRsItems;
+constexpr int kRsDigits = 257;                    // 256 + the validity bucket of the last pass
+constexpr uint32_t kRsNone = 511;                 // digit of a lane past the end (never counted)
+constexpr uint64_t kSign = 0x8000000000000000ull;
+
+// rows lacking the position get key 0 so that passes 0..6 keep them in input order; the last
+// pass moves them to their bucket (256 / 0)
+__global__ void k_rs_prep(const int64_t* __restrict__ col, const uint8_t* __restrict__ valid, size_t n, int desc,
+                          uint64_t* __restrict__ keys, uint32_t* __restrict__ ids) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t u = (uint64_t)col[i] ^ kSign;  // signed order -> unsigned order
+  keys[i] = (valid && !valid[i]) ? 0ull : (desc ? ~u : u);
+  ids[i] = (uint32_t)i;
+}
+
+__device__ __forceinline__ uint32_t rs_digit(uint64_t k, uint32_t id, const uint8_t* __restrict__ valid, int pass,
+                                             int desc) {
+  uint32_t d = (uint32_t)(k >> (8 * pass)) & 0xFFu;
+  if (pass == 7 && valid) {
+    const bool v = valid[id] != 0;
+    d = desc ? (v ? d : 256u) : (v ? d + 1u : 0u);
+  }
+  return d;
+}
+
+// row of item k of a lane: each wave owns a contiguous quarter of the tile
+__device__ __forceinline__ size_t rs_row(size_t tile, int wid, int k, int lane) {
+  return tile * kRsTile + (size_t)wid * (kRsTile / kRsWaves) + (size_t)k * 64 + lane;
+}
+
+__global__ void __launch_bounds__(kRsBlock) k_rs_hist(const uint64_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ ids,
+                                                      const uint8_t* __restrict__ valid, size_t n, int pass,
+                                                      int desc, uint32_t* __restrict__ hist, size_t nblocks) {
+  __shared__ uint32_t cnt[kRsDigits];
+  for (int d = threadIdx.x; d < kRsDigits; d += kRsBlock) cnt[d] = 0;
+  __syncthreads();
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // all loads first (independent, in flight together), then the LDS counting
+  uint32_t d[kRsItems];
+  uint64_t key[kRsItems];
+  uint32_t id[kRsItems];
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {  // unconditional loads (index clamped), masked below
+    const size_t i = min(rs_row(blockIdx.x, wid, k, lane), n - 1);
+    key[k] = keys[i];
+    id[k] = ids[i];
+  }
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    const size_t i = rs_row(blockIdx.x, wid, k, lane);
+    d[k] = i < n ? rs_digit(key[k], id[k], valid, pass, desc) : kRsNone;
+  }
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k)
+    if (d[k] != kRsNone) atomicAdd(&cnt[d[k]], 1u);
+  __syncthreads();
+  for (int d = threadIdx.x; d < kRsDigits; d += kRsBlock) hist[(size_t)d * nblocks + blockIdx.x] = cnt[d];
+}
+
+// per digit d (one block each): exclusive scan of the tile counts hist[d][0..nblocks) in place,
+// digit total -> dtot[d]
+__global__ void __launch_bounds__(256) k_rs_scan_digits(uint32_t* __restrict__ hist, size_t nblocks,
+                                                        uint32_t* __restrict__ dtot) {
+  __shared__ uint32_t part[256];
+  uint32_t* h = hist + (size_t)blockIdx.x * nblocks;
+  const size_t per = (nblocks + 255) / 256;
+  const size_t b0 = threadIdx.x * per, b1 = min(nblocks, b0 + per);
+  uint32_t s = 0;
+  for (size_t b = b0; b < b1; ++b) s += h[b];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const uint32_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
+  for (size_t b = b0; b < b1; ++b) {
+    const uint32_t c = h[b];
+    h[b] = run;
+    run += c;
+  }
+  if (threadIdx.x == 255) dtot[blockIdx.x] = part[255];
+}
+
+// exclusive scan of the kRsDigits digit totals -> dbase (one block of 512 threads)
+__global__ void __launch_bounds__(512) k_rs_scan_base(const uint32_t* __restrict__ dtot, uint32_t* __restrict__ dbase) {
+  __shared__ uint32_t part[512];
+  const int t = threadIdx.x;
+  part[t] = t < kRsDigits ? dtot[t] : 0u;
+  __syncthreads();
+  for (int off = 1; off < 512; off <<= 1) {
+    const uint32_t v = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  if (t < kRsDigits) dbase[t] = t ? part[t - 1] : 0u;
+}
+
+__global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ ids,
+                                                         const uint8_t* __restrict__ valid, size_t n, int pass,
+                                                         int desc, const uint32_t* __restrict__ hist,
+                                                         const uint32_t* __restrict__ dbase, size_t nblocks,
+                                                         uint64_t* __restrict__ keys_out,
+                                                         uint32_t* __restrict__ ids_out) {
+  __shared__ uint32_t cnt[kRsWaves][kRsDigits];
+  for (int d = threadIdx.x; d < kRsWaves * kRsDigits; d += kRsBlock) (&cnt[0][0])[d] = 0;
+  __syncthreads();
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint64_t key[kRsItems];
+  uint32_t id[kRsItems], dr[kRsItems];  // dr = digit | rank << 9
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {  // all loads first, unconditional (index clamped), masked below
+    const size_t i = min(rs_row(blockIdx.x, wid, k, lane), n - 1);
+    key[k] = keys[i];
+    id[k] = ids[i];
+  }
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    const size_t i = rs_row(blockIdx.x, wid, k, lane);
+    dr[k] = i < n ? rs_digit(key[k], id[k], valid, pass, desc) : kRsNone;
+  }
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    const uint32_t d = dr[k];
+    // lanes holding the same digit: AND of 9 bit-ballots
+    uint64_t peers = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 9; ++b) {
+      const uint64_t bal = __ballot((d >> b) & 1u);
+      peers &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    uint32_t rank = 0;
+    if (d != kRsNone) {
+      const uint32_t before = cnt[wid][d];  // every peer reads before the leader writes (wave order)
+      rank = before + (uint32_t)__popcll(peers & lt);
+      if ((peers & lt) == 0) cnt[wid][d] = before + (uint32_t)__popcll(peers);
+    }
+    dr[k] = d | (rank << 9);
+  }
+  __syncthreads();
+  // base[w][d] = global bucket offset of this tile + counts of earlier waves
+  for (int d = threadIdx.x; d < kRsDigits; d += kRsBlock) {
+    uint32_t run = dbase[d] + hist[(size_t)d * nblocks + blockIdx.x];
+    for (int w = 0; w < kRsWaves; ++w) {
+      const uint32_t c = cnt[w][d];
+      cnt[w][d] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    const uint32_t d = dr[k] & 511u;
+    if (d == kRsNone) continue;
+    const uint32_t dst = cnt[wid][d] + (dr[k] >> 9);
+    if (keys_out) keys_out[dst] = key[k];
+    ids_out[dst] = id[k];
+  }
+}
+
+size_t rs_blocks(size_t n) { return (n + kRsTile - 1) / kRsTile; }
+size_t rs_scratch_bytes(size_t n) {
+  // keys x2 (8 B), ids x1 extra (4 B; the other id buffer is the caller's output), histogram
+  return 2 * n * 8 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 512;
+}
+
+hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
+                            uint32_t* out_ids, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const size_t nb = rs_blocks(n);
+  uint64_t* ka = (uint64_t*)scratch;
+  uint64_t* kb = ka + n;
+  uint32_t* ib = (uint32_t*)(kb + n);
+  uint32_t* hist = (uint32_t*)(((uintptr_t)(ib + n) + 255) & ~(uintptr_t)255);
+  uint32_t* dtot = hist + (size_t)kRsDigits * nb;
+  uint32_t* dbase = dtot + kRsDigits;
+  // 8 passes (even): ids ping-pong out_ids -> ib -> out_ids ..., so the last pass writes out_ids
+  uint32_t* ia = out_ids;
+  uint32_t* ic = ib;
+  hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, col, valid, n, desc, ka, ia);
+  for (int pass = 0; pass < 8; ++pass) {
+    hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)nb), dim3(kRsBlock), 0, st, ka, ia, valid, n, pass, desc, hist, nb);
+    hipLaunchKernelGGL(k_rs_scan_digits, dim3(kRsDigits), dim3(256), 0, st, hist, nb, dtot);
+    hipLaunchKernelGGL(k_rs_scan_base, dim3(1), dim3(512), 0, st, dtot, dbase);
+    hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)nb), dim3(kRsBlock), 0, st, ka, ia, valid, n, pass, desc, hist,
+                       dbase, nb, pass == 7 ? nullptr : kb, ic);
+    uint64_t* tk = ka;
+    ka = kb;
+    kb = tk;
+    uint32_t* ti = ia;
+    ia = ic;
+    ic = ti;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace ddshe

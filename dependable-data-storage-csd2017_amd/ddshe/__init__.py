@@ -20,6 +20,14 @@ LIB_PATH = os.path.join(_HERE, "libddshe.so")
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"libddshe.so not built at {LIB_PATH}: run `make -C dependable-data-storage-csd2017_amd/csrc` "
                       "or __graft_entry__.build()")
+# One HIP runtime per process: PyTorch ships its own libamdhip64.so.7 (same soname as
+# /opt/rocm's). Loading torch first makes libddshe.so bind to that copy, so device pointers and
+# streams are shared with torch; loading ours first would start a second runtime that torch
+# then cannot initialise beside ("No HIP GPUs are available").
+try:
+    import torch  # noqa: F401
+except ImportError:  # plain C-ABI use without PyTorch: /opt/rocm's runtime
+    pass
 _lib = C.CDLL(LIB_PATH)
 
 # status codes (include/ddshe.h)
@@ -38,6 +46,7 @@ EXPORTS = [
     "dds_ope_filter", "dds_ope_filter_device", "dds_paillier_encrypt_batch", "dds_modexp_batch", "dds_sum_all_dec",
     "dds_mult_all_dec", "dds_paillier_encrypt_batch_crt", "dds_col_fill_random", "dds_col_encrypt_paillier",
     "dds_col_fill_table_synth", "dds_col_truncate",
+    "dds_ope_order", "dds_ope_order_device",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -83,6 +92,8 @@ _sig("dds_col_fill_paillier_synth", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_ch
      _sz, C.c_uint32)
 _sig("dds_ope_filter", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int64, C.c_int, C.c_void_p, _szp)
 _sig("dds_ope_filter_device", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int64, C.c_int, C.c_void_p, _szp)
+_sig("dds_ope_order", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int, C.c_void_p)
+_sig("dds_ope_order_device", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int, C.c_void_p)
 _sig("dds_paillier_encrypt_batch", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, C.POINTER(C.c_uint32),
      C.c_char_p, _sz, _sz, _u8p, _sz)
 _sig("dds_paillier_encrypt_batch_crt", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, C.c_char_p, _sz,
@@ -245,6 +256,20 @@ class Engine:
         _check(_lib.dds_ope_filter_device(self._h, C.c_void_p(d_col), C.c_void_p(d_valid or 0), n, int(bound),
                                           OPE_OPS[op], C.c_void_p(d_out), C.byref(got)), "dds_ope_filter_device")
         return got.value
+
+    def ope_order(self, col, valid, descending: bool) -> np.ndarray:
+        """OrderLS (descending=True) / OrderSL row permutation (dds_ope_order)."""
+        col = np.ascontiguousarray(col, dtype=np.int64)
+        v = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
+        out = np.empty(len(col), dtype=np.uint32)
+        _check(_lib.dds_ope_order(self._h, col.ctypes.data_as(C.c_void_p),
+                                  None if v is None else v.ctypes.data_as(C.c_void_p), len(col), int(descending),
+                                  out.ctypes.data_as(C.c_void_p)), "dds_ope_order")
+        return out
+
+    def ope_order_device(self, d_col: int, d_valid: int | None, n: int, descending: bool, d_out: int):
+        _check(_lib.dds_ope_order_device(self._h, C.c_void_p(d_col), C.c_void_p(d_valid or 0), n, int(descending),
+                                         C.c_void_p(d_out)), "dds_ope_order_device")
 
     # ---- encryption ----
     def paillier_encrypt_batch(self, n: int, g: int, ms, rs) -> list[int]:

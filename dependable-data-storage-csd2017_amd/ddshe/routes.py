@@ -138,3 +138,26 @@ def search(eng: Engine, route: str, keyed_rows, position: int, value) -> list:
     op, bound = _clamp_bound(op, item)
     idx = _call(eng.ope_filter, np.array(col, dtype=np.int64), np.array(valid, dtype=np.uint8), bound, op)
     return [keys[i] for i in idx]
+
+
+def order(eng: Engine, route: str, keyed_rows, position: int) -> list:
+    """GET /OrderLS|/OrderSL?position — DDSRestServer.scala:541-606: keys of the non-empty
+    rows, holders of the position (length-1 >= position) by contents(position).toLong
+    descending (OrderLS, others last) or ascending (OrderSL, others first); stable for ties."""
+    if route not in ("OrderLS", "OrderSL"):
+        raise ValueError(route)
+    keys, col, valid = [], [], []
+    for key, row in keyed_rows:
+        if row is None:
+            continue
+        ok = len(row) - 1 >= position
+        v = _parse_int(row[position]) if ok else 0
+        if ok and not (INT64_MIN <= v <= INT64_MAX):
+            raise ServerError("NumberFormatException: value outside Long (String.toLong)")
+        keys.append(key)
+        col.append(v)
+        valid.append(1 if ok else 0)
+    if not keys:
+        return []
+    idx = _call(eng.ope_order, np.array(col, dtype=np.int64), np.array(valid, dtype=np.uint8), route == "OrderLS")
+    return [keys[i] for i in idx]

@@ -154,6 +154,18 @@ int dds_ope_filter(dds_ctx* ctx, const int64_t* col, const uint8_t* valid, size_
 int dds_ope_filter_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_valid, size_t n, int64_t bound, int op,
                           uint32_t* d_out_idx, size_t* out_n);
 
+/* ---- OPE ordering (OrderLS / OrderSL, DDSRestServer.scala:541-606) ------------
+ * out_idx receives a permutation of [0, n): rows with valid[i] != 0 (the row holds the
+ * position: contents.length-1 >= position, :556 / :589) ordered by col (signed 64-bit, the
+ * route's `.toLong`) descending (OrderLS, descending != 0) or ascending (OrderSL); rows with
+ * valid[i] == 0 go last (OrderLS) or first (OrderSL). Equal keys keep their input order
+ * (scala sortWith is stable). valid may be NULL (all rows hold the position). */
+int dds_ope_order(dds_ctx* ctx, const int64_t* col, const uint8_t* valid, size_t n, int descending,
+                  uint32_t* out_idx);
+/* same on device-resident arrays (device pointers) */
+int dds_ope_order_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_valid, size_t n, int descending,
+                         uint32_t* d_out_idx);
+
 /* ---- batched Paillier encryption (HomoAdd.encrypt, SJHomoLibProvider.scala:58) ----
  * c_i = g^m_i * r_i^n mod n^2 with caller-supplied r_i (big-endian, r_width bytes,
  * values in [1, n^2)). out receives n of nsq_bytes each. */

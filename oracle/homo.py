@@ -199,6 +199,36 @@ def search(route: str, keyed_rows, position: int, value) -> set:
     return out
 
 
+def java_long(s) -> int:
+    """``String.toLong`` (java.lang.Long.parseLong): optional sign, decimal digits, int64 range."""
+    s = str(s)
+    body = s[1:] if s[:1] in "+-" else s
+    if not body or not body.isascii() or not body.isdigit():
+        raise ValueError(f"NumberFormatException: {s!r}")
+    v = int(s)
+    if not -(1 << 63) <= v < (1 << 63):
+        raise ValueError(f"NumberFormatException: {s!r} (out of Long range)")
+    return v
+
+
+def order(route: str, keyed_rows, position: int) -> list:
+    """``GET /OrderLS|/OrderSL?position`` — ``DDSRestServer.scala:541-606``.
+    Keys of the non-empty rows (``:553``, ``:586``) sorted with the route's comparator
+    (``:555-563``, ``:588-596``): a row holds the position iff ``length-1 >= position``;
+    OrderLS puts holders first, by ``contents(position).toLong`` descending; OrderSL puts the
+    others first, then holders ascending. ``sortWith`` is stable, so equal keys keep the input
+    order. (OrderSL's comparator is not strict between two non-holders — ``lt`` is true both
+    ways — so the JVM's order among them is an artefact of TimSort; unpinned, kept stable here.)"""
+    rows = [(k, r) for k, r in keyed_rows if r is not None]
+    hold = [(k, java_long(r[position])) for k, r in rows if len(r) - 1 >= position]
+    rest = [k for k, r in rows if len(r) - 1 < position]
+    if route == "OrderLS":
+        return [k for k, _ in sorted(hold, key=lambda kv: -kv[1])] + rest
+    if route == "OrderSL":
+        return rest + [k for k, _ in sorted(hold, key=lambda kv: kv[1])]
+    raise ValueError(route)
+
+
 # ---------------------------------------------------------------------------
 # Fold primitives used by the tests at sizes beyond route-level vectors
 # ---------------------------------------------------------------------------

@@ -1,0 +1,61 @@
+"""GPU parity of the OPE ordering routes (OrderLS / OrderSL, DDSRestServer.scala:541-606):
+stable radix sort of the int64 OPE column through the C-ABI against numpy's stable argsort
+and the route restatement in oracle/homo.py."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import homo
+
+pytestmark = pytest.mark.gpu
+
+
+def expected(col, valid, descending):
+    idx = np.arange(len(col))
+    hold = idx[valid != 0]
+    rest = idx[valid == 0]
+    key = col[hold]
+    # stable (ties keep the input order); descending = ascending on ~key, which reverses the
+    # int64 order exactly (~x = -x-1) without overflow at INT64_MIN
+    o = np.argsort(~key if descending else key, kind="stable")
+    s = hold[o]
+    return np.concatenate([s, rest]) if descending else np.concatenate([rest, s])
+
+
+@pytest.mark.parametrize("n", [1, 2, 255, 4096, 4097, 65537, 1_000_003])
+def test_order_vs_numpy(eng, n):
+    rng = np.random.default_rng(n)
+    col = rng.integers(-2**63, 2**63 - 1, size=n, dtype=np.int64)
+    if n > 20:
+        col[:10] = [-2**63, 2**63 - 1, 0, -1, 1, 5, 5, 5, 7, -7]
+        col[10:20] = col[0:10]          # duplicates of the extremes
+    valid = (rng.random(n) > 0.1).astype(np.uint8)
+    for desc in (True, False):
+        got = eng.ope_order(col, valid, desc)
+        assert np.array_equal(got, expected(col, valid, desc)), (n, desc)
+    got = eng.ope_order(col, None, False)
+    assert np.array_equal(got, np.argsort(col, kind="stable"))
+
+
+def test_order_many_ties(eng):
+    """Small key range (OPE values of DDSDataGenerator-sized plaintexts): stability dominates."""
+    rng = np.random.default_rng(3)
+    n = 3_000_017
+    col = rng.integers(0, 50, size=n, dtype=np.int64) - 25
+    valid = (rng.random(n) > 0.3).astype(np.uint8)
+    for desc in (True, False):
+        assert np.array_equal(eng.ope_order(col, valid, desc), expected(col, valid, desc))
+
+
+def test_order_routes_vs_oracle(eng):
+    from ddshe import routes
+    rng = random.Random(8)
+    keyed = []
+    for i in range(500):
+        length = rng.randrange(0, 5)
+        row = [str(rng.randrange(-50, 50)) for _ in range(length)]
+        keyed.append((f"key{i}", row if rng.random() > 0.05 else None))
+    for position in (0, 1, 3):
+        for route in ("OrderLS", "OrderSL"):
+            assert routes.order(eng, route, keyed, position) == homo.order(route, keyed, position), (route, position)

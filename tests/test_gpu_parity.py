@@ -239,7 +239,7 @@ def test_large_fold_property(eng, keys):
 # ---------------------------------------------------------------------------
 # OPE range filter
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("n", [1, 63, 4096, 4097, 100_000, 3_000_001])
+@pytest.mark.parametrize("n", [1, 63, 4096, 4097, 8192, 8193, 100_000, 3_000_001])
 def test_ope_filter_vs_numpy(eng, n):
     rng = np.random.default_rng(n)
     col = rng.integers(-2**63, 2**63 - 1, size=n, dtype=np.int64)
@@ -252,3 +252,16 @@ def test_ope_filter_vs_numpy(eng, n):
             assert np.array_equal(got, exp), (n, bound, op)
     got = eng.ope_filter(col, None, 0, "ge")
     assert np.array_equal(got, np.nonzero(col >= 0)[0].astype(np.uint32))
+
+
+def test_ope_filter_long_lookback(eng):
+    """> 256 x 8192-row tiles: the single-pass compaction's look-back crosses several probe
+    windows; matches are dense (all rows) and sparse (every 1000th row) so tile counts vary."""
+    n = 12_000_017
+    col = np.arange(n, dtype=np.int64)
+    valid = np.ones(n, dtype=np.uint8)
+    got = eng.ope_filter(col, valid, -1, "gt")
+    assert len(got) == n and np.array_equal(got, np.arange(n, dtype=np.uint32))
+    sparse = (col % 1000 == 0).astype(np.int64)
+    got = eng.ope_filter(sparse, valid, 0, "gt")
+    assert np.array_equal(got, np.nonzero(sparse)[0].astype(np.uint32))

@@ -196,3 +196,13 @@ def test_c_restatement_matches_python_oracle(keys):
         xs = [N + 5, 3 * N + 1, rng.randrange(N)]        # unreduced inputs
         assert cref.fold(N, xs) == homo.modmul_fold(xs, N)
         assert cref.fold(N, [N + 5]) == N + 5              # k == 1 verbatim
+
+
+def test_order_route_semantics():
+    """OrderLS / OrderSL restatement (DDSRestServer.scala:541-606) on a hand-checked case."""
+    rows = [("a", ["5"]), ("b", []), ("c", ["-3"]), ("d", ["5"]), ("e", None), ("f", ["x", "9"]), ("g", ["+7"])]
+    assert homo.order("OrderLS", [r for r in rows if r[0] != "f"], 0) == ["g", "a", "d", "c", "b"]
+    assert homo.order("OrderSL", [r for r in rows if r[0] != "f"], 0) == ["b", "c", "a", "d", "g"]
+    assert homo.order("OrderSL", rows, 1) == ["a", "b", "c", "d", "g", "f"]  # only f holds position 1
+    with pytest.raises(ValueError):
+        homo.order("OrderLS", rows, 0)                                   # "x".toLong
