@@ -64,6 +64,29 @@ hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n,
 size_t rs_scratch_bytes(size_t n);
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
                             uint32_t* out_ids, hipStream_t st);
+// deterministic-equality scans (ddshe_strscan.hip)
+// 64-bit digest of an element string (FNV-1a over the bytes, splitmix finaliser); identical on
+// host (needles) and device (table)
+__host__ __device__ inline uint64_t str_digest(const uint8_t* p, uint64_t len) {
+  uint64_t h = 0xcbf29ce484222325ull ^ len;
+  for (uint64_t i = 0; i < len; ++i) h = (h ^ p[i]) * 0x100000001b3ull;
+  h ^= h >> 30;
+  h *= 0xbf58476d1ce4e5b9ull;
+  h ^= h >> 27;
+  h *= 0x94d049bb133111ebull;
+  return h ^ (h >> 31);
+}
+struct StrNeedles {  // up to 3 items (SearchEntryAND/OR triplets), bytes in a device buffer
+  uint64_t h[3];
+  uint64_t len[3];
+  uint64_t off[3];
+  int n;
+};
+hipError_t launch_str_digest(const uint8_t* chars, const uint64_t* elem_off, size_t nelems, uint64_t* digest,
+                             hipStream_t st);
+hipError_t launch_str_scan(const uint64_t* row_off, size_t nrows, const uint64_t* elem_off, const uint8_t* chars,
+                           const uint64_t* digest, const uint8_t* nchars, const StrNeedles& nd, int mode,
+                           uint64_t position, int negate, int64_t* flags, hipStream_t st);
 hipError_t launch_plain_sum(const uint32_t* X, size_t stride, size_t count, int S, size_t nthreads, uint64_t* part,
                             uint64_t* out, hipStream_t st);
 // unbounded product tree level: rows (2p, 2p+1) of A[count][len] (radix 2^16 in u32)

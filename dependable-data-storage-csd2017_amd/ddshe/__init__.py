@@ -46,7 +46,8 @@ EXPORTS = [
     "dds_ope_filter", "dds_ope_filter_device", "dds_paillier_encrypt_batch", "dds_modexp_batch", "dds_sum_all_dec",
     "dds_mult_all_dec", "dds_paillier_encrypt_batch_crt", "dds_col_fill_random", "dds_col_encrypt_paillier",
     "dds_col_fill_table_synth", "dds_col_truncate",
-    "dds_ope_order", "dds_ope_order_device",
+    "dds_ope_order", "dds_ope_order_device", "dds_strtab_create", "dds_strtab_destroy", "dds_search_eq",
+    "dds_search_entry", "dds_is_element",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -94,6 +95,12 @@ _sig("dds_ope_filter", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int
 _sig("dds_ope_filter_device", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int64, C.c_int, C.c_void_p, _szp)
 _sig("dds_ope_order", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int, C.c_void_p)
 _sig("dds_ope_order_device", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int, C.c_void_p)
+_sig("dds_strtab_create", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_void_p, _sz, C.POINTER(C.c_void_p))
+_sig("dds_strtab_destroy", C.c_int, C.c_void_p)
+_sig("dds_search_eq", C.c_int, C.c_void_p, _sz, C.c_char_p, _sz, C.c_int, C.c_void_p, _szp)
+_sig("dds_search_entry", C.c_int, C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), _sz, C.c_int, C.c_void_p,
+     _szp)
+_sig("dds_is_element", C.c_int, C.c_void_p, _sz, C.c_char_p, _sz, C.POINTER(C.c_int))
 _sig("dds_paillier_encrypt_batch", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, C.POINTER(C.c_uint32),
      C.c_char_p, _sz, _sz, _u8p, _sz)
 _sig("dds_paillier_encrypt_batch_crt", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, C.c_char_p, _sz,
@@ -309,6 +316,10 @@ class Engine:
         raw = bytes(out)
         return [int.from_bytes(raw[i * mb:(i + 1) * mb], "big") for i in range(len(bases))]
 
+    def strtab(self, rows) -> "StrTable":
+        """Device-resident string table of the rows' contents (lists of values, str()-ed)."""
+        return StrTable(self, rows)
+
     def column(self, modulus: int, capacity: int) -> "Column":
         return Column(self, modulus, capacity)
 
@@ -422,6 +433,64 @@ class Column:
                                              int_to_be(n, nbytes(n)), nbytes(n), int_to_be(g, nbytes(g)), nbytes(g),
                                              pb, nbytes(p) if p else 0, qb, nbytes(q) if q else 0),
                "dds_col_encrypt_paillier")
+
+
+class StrTable:
+    """Device-resident contents of DDSSet rows for the deterministic-equality scans (dds_strtab)."""
+
+    def __init__(self, eng: Engine, rows=None, *, chars: bytes | None = None, elem_off=None, row_off=None):
+        if rows is not None:
+            enc = [[str(v).encode() for v in row] for row in rows]
+            lens = np.fromiter((len(x) for row in enc for x in row), dtype=np.uint64)
+            elem_off = np.zeros(len(lens) + 1, dtype=np.uint64)
+            np.cumsum(lens, out=elem_off[1:])
+            row_off = np.zeros(len(enc) + 1, dtype=np.uint64)
+            np.cumsum(np.fromiter((len(r) for r in enc), dtype=np.uint64, count=len(enc)), out=row_off[1:])
+            chars = b"".join(x for row in enc for x in row)
+        self.elem_off = np.ascontiguousarray(elem_off, dtype=np.uint64)
+        self.row_off = np.ascontiguousarray(row_off, dtype=np.uint64)
+        self.nrows = len(self.row_off) - 1
+        self._chars = chars or b"\0"
+        h = C.c_void_p()
+        _check(_lib.dds_strtab_create(eng._h, C.c_char_p(self._chars), self.elem_off.ctypes.data_as(C.c_void_p),
+                                      len(self.elem_off) - 1, self.row_off.ctypes.data_as(C.c_void_p), self.nrows,
+                                      C.byref(h)), "dds_strtab_create")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            _lib.dds_strtab_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def search_eq(self, position: int, value, negate: bool = False) -> np.ndarray:
+        v = str(value).encode()
+        out = np.empty(max(1, self.nrows), dtype=np.uint32)
+        n = C.c_size_t()
+        _check(_lib.dds_search_eq(self._h, position, v, len(v), int(negate), out.ctypes.data_as(C.c_void_p),
+                                  C.byref(n)), "dds_search_eq")
+        return out[: n.value].copy()
+
+    def search_entry(self, values, require_all: bool = False) -> np.ndarray:
+        vs = [str(v).encode() for v in values]
+        arr = (C.c_char_p * len(vs))(*vs)
+        lens = (C.c_size_t * len(vs))(*[len(v) for v in vs])
+        out = np.empty(max(1, self.nrows), dtype=np.uint32)
+        n = C.c_size_t()
+        _check(_lib.dds_search_entry(self._h, arr, lens, len(vs), int(require_all), out.ctypes.data_as(C.c_void_p),
+                                     C.byref(n)), "dds_search_entry")
+        return out[: n.value].copy()
+
+    def is_element(self, row: int, value) -> bool:
+        v = str(value).encode()
+        f = C.c_int()
+        _check(_lib.dds_is_element(self._h, row, v, len(v), C.byref(f)), "dds_is_element")
+        return bool(f.value)
 
 
 # ---- synthetic-row plaintexts (mirror of k_synth_rows' index derivation) ----

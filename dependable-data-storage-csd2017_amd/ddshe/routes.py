@@ -161,3 +161,57 @@ def order(eng: Engine, route: str, keyed_rows, position: int) -> list:
         return []
     idx = _call(eng.ope_order, np.array(col, dtype=np.int64), np.array(valid, dtype=np.uint8), route == "OrderLS")
     return [keys[i] for i in idx]
+
+
+def _live(keyed_rows):
+    keys, rows, seen = [], [], set()
+    for key, row in keyed_rows:
+        if row is None or key in seen:
+            continue
+        seen.add(key)
+        keys.append(key)
+        rows.append(row)
+    return keys, rows
+
+
+def search_eq(eng: Engine, route: str, keyed_rows, position: int, value) -> list:
+    """POST /SearchEq|/SearchNEq?position — DDSRestServer.scala:607-681 (HomoDet.compare as
+    string equality). Keys in row order (the reference's prepend order is unspecified)."""
+    if route not in ("SearchEq", "SearchNEq"):
+        raise ValueError(route)
+    keys, rows = _live(keyed_rows)
+    if not keys:
+        return []
+    tab = eng.strtab(rows)
+    try:
+        idx = _call(tab.search_eq, position, value, route == "SearchNEq")
+    finally:
+        tab.close()
+    return [keys[i] for i in idx]
+
+
+def search_entry(eng: Engine, route: str, keyed_rows, values) -> list:
+    """POST /SearchEntry (one value) | /SearchEntryOR | /SearchEntryAND (three) —
+    DDSRestServer.scala:831-938."""
+    if route not in ("SearchEntry", "SearchEntryOR", "SearchEntryAND"):
+        raise ValueError(route)
+    keys, rows = _live(keyed_rows)
+    if not keys:
+        return []
+    tab = eng.strtab(rows)
+    try:
+        idx = _call(tab.search_entry, list(values), route == "SearchEntryAND")
+    finally:
+        tab.close()
+    return [keys[i] for i in idx]
+
+
+def is_element(eng: Engine, row, value) -> bool:
+    """POST /IsElement/{key} — DDSRestServer.scala:322-353: 404 for a missing row."""
+    if row is None:
+        raise NotFound("no such key")
+    tab = eng.strtab([row])
+    try:
+        return _call(tab.is_element, 0, value)
+    finally:
+        tab.close()

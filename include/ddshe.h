@@ -50,6 +50,7 @@ typedef enum dds_status {
 
 typedef struct dds_ctx dds_ctx;
 typedef struct dds_col dds_col;
+typedef struct dds_strtab dds_strtab;
 
 /* OPE predicates of SearchGt / SearchGtEq / SearchLt / SearchLtEq:
  * keep row iff col <op> bound (DDSRestServer.scala:704, :742, :779, :816). */
@@ -165,6 +166,27 @@ int dds_ope_order(dds_ctx* ctx, const int64_t* col, const uint8_t* valid, size_t
 /* same on device-resident arrays (device pointers) */
 int dds_ope_order_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_valid, size_t n, int descending,
                          uint32_t* d_out_idx);
+
+/* ---- deterministic-equality scans ---------------------------
+ * HomoDet.compare (hlib, absent) is taken as equality of the ciphertext strings.
+ * A string table holds the rows' contents: element e is chars[elem_offsets[e], elem_offsets[e+1]),
+ * row r is elements [row_offsets[r], row_offsets[r+1]) (its DDSSet.contents, in column order;
+ * DDSSet.scala:3). The table is device-resident with a 64-bit digest per element; results are
+ * exact (bytes are compared on a digest hit). out_rows receives ascending row ids (capacity nrows).
+ *   dds_search_eq     SearchEq / SearchNEq (negate != 0), DDSRestServer.scala:607-681: rows with
+ *                     length-1 > position whose element `position` equals / differs from value.
+ *   dds_search_entry  SearchEntry (1 value), SearchEntryOR (3, require_all = 0) and
+ *                     SearchEntryAND (3, require_all != 0: all three distinct values present),
+ *                     DDSRestServer.scala:831-938.
+ *   dds_is_element    IsElement, DDSRestServer.scala:322-353 (row out of range: DDS_E_EMPTY, 404). */
+int dds_strtab_create(dds_ctx* ctx, const char* chars, const uint64_t* elem_offsets, size_t nelems,
+                      const uint64_t* row_offsets, size_t nrows, dds_strtab** out);
+int dds_strtab_destroy(dds_strtab* tab);
+int dds_search_eq(dds_strtab* tab, size_t position, const char* value, size_t len, int negate, uint32_t* out_rows,
+                  size_t* out_n);
+int dds_search_entry(dds_strtab* tab, const char* const* values, const size_t* lens, size_t nvalues, int require_all,
+                     uint32_t* out_rows, size_t* out_n);
+int dds_is_element(dds_strtab* tab, size_t row, const char* value, size_t len, int* found);
 
 /* ---- batched Paillier encryption (HomoAdd.encrypt, SJHomoLibProvider.scala:58) ----
  * c_i = g^m_i * r_i^n mod n^2 with caller-supplied r_i (big-endian, r_width bytes,

@@ -229,6 +229,55 @@ def order(route: str, keyed_rows, position: int) -> list:
     raise ValueError(route)
 
 
+# Deterministic-equality scans. hlib's HomoDet.compare(a, b) is absent (lib/README.txt:1); a
+# deterministic scheme compares ciphertexts by equality, so compare(a, b) := a == b on the
+# strings (unpinned beyond that assumption).
+def homo_det_compare(a, b) -> bool:
+    return str(a) == str(b)
+
+
+def search_eq(route: str, keyed_rows, position: int, value) -> set:
+    """``POST /SearchEq|/SearchNEq?position`` — ``DDSRestServer.scala:607-681``: keys of the
+    non-empty rows with ``length-1 > position`` (strict, ``:629``) whose ``contents(position)``
+    does (Eq) / does not (NEq, ``:667``) compare equal to the item. Key set (prepended list)."""
+    out = set()
+    for key, row in keyed_rows:
+        if row is None or not len(row) - 1 > position:
+            continue
+        eq = homo_det_compare(row[position], value)
+        if eq == (route == "SearchEq"):
+            out.add(key)
+    return out
+
+
+def search_entry(route: str, keyed_rows, values) -> set:
+    """``POST /SearchEntry`` (one value), ``/SearchEntryOR`` and ``/SearchEntryAND`` (three) —
+    ``DDSRestServer.scala:831-938``: a row qualifies when some element equals the value (Entry),
+    any of the three (OR, ``:881-883``), or when the set of its elements equal to one of the three
+    reaches size 3 (AND, ``:918-927``: all three present and pairwise distinct). The per-row
+    ``break`` (``:851,886,926``) is read as "stop scanning this row"."""
+    values = [str(v) for v in values]
+    out = set()
+    for key, row in keyed_rows:
+        if row is None:
+            continue
+        if route == "SearchEntryAND":
+            found = {str(e) for e in row if str(e) in values}
+            if len(found) == 3:
+                out.add(key)
+        elif any(str(e) in values for e in row):
+            out.add(key)
+    return out
+
+
+def is_element(row, value) -> bool:
+    """``POST /IsElement/{key}`` — ``DDSRestServer.scala:322-353``: some element of the row
+    compares equal; a missing row is 404 (``:348``)."""
+    if row is None:
+        raise NotFound()
+    return any(homo_det_compare(e, value) for e in row)
+
+
 # ---------------------------------------------------------------------------
 # Fold primitives used by the tests at sizes beyond route-level vectors
 # ---------------------------------------------------------------------------
