@@ -70,9 +70,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
-    ap.add_argument("--workload", choices=("sum", "product_filter", "encrypt_sum", "order"), default="sum",
+    ap.add_argument("--workload", choices=("sum", "product_filter", "encrypt_sum", "order", "entry_search"),
+                    default="sum",
                     help="sum: BASELINE.json config 2 (headline); product_filter: config 3; encrypt_sum: config 4; "
-                         "order: OrderLS over the config-3 OPE column (SURVEY.md §8f rank 2)")
+                         "order: OrderLS over the config-3 OPE column (SURVEY.md §8f rank 2); "
+                         "entry_search: SearchEntryOR + SearchEq over a string table (§8f rank 3)")
     ap.add_argument("--rows", type=int, default=None,
                     help="rows per rank per step (weak scaling); whole job with --strong")
     ap.add_argument("--strong", action="store_true", help="split --rows over the ranks instead")
@@ -84,7 +86,8 @@ def main():
     ap.add_argument("--verify", type=int, default=1, help="check the result on rank 0")
     args = ap.parse_args()
     dflt = {"sum": (10_000_000, 20, 3, 2), "product_filter": (10_000_000, 10, 2, 3),
-            "encrypt_sum": (1_000_000, 2, 1, 4), "order": (10_000_000, 10, 2, 3)}[args.workload]
+            "encrypt_sum": (1_000_000, 2, 1, 4), "order": (10_000_000, 10, 2, 3),
+            "entry_search": (10_000_000, 10, 2, 5)}[args.workload]
     args.rows = dflt[0] if args.rows is None else args.rows
     args.steps = dflt[1] if args.steps is None else args.steps
     args.warmup = dflt[2] if args.warmup is None else args.warmup
@@ -113,7 +116,7 @@ def main():
     ctx = dict(args=args, eng=eng, world=world, rank=rank, local=local, total=total, row0=row0, mine=mine,
                per=(total + world - 1) // world, torch=torch, ddshe=ddshe, ddist=ddist)
     wl = {"sum": SumWorkload, "product_filter": ProductFilterWorkload, "encrypt_sum": EncryptSumWorkload,
-          "order": OrderWorkload}[args.workload](ctx)
+          "order": OrderWorkload, "entry_search": EntrySearchWorkload}[args.workload](ctx)
     t_fill = time.time()
     wl.setup()
     torch.cuda.synchronize()
@@ -477,6 +480,77 @@ class OrderWorkload(_Workload):
         out.update(data="synthetic (seeded OPE map of U[1,10^4) plaintexts, 5% rows lacking the position)",
                    dtype="int64", roofline=roof, cpu_baseline=cpu, verified=ok)
         return out
+
+
+class EntrySearchWorkload(_Workload):
+    """SearchEntryOR (DDSRestServer.scala:879-903) + SearchEq at position 3 (:607-643) over a
+    device-resident string table: 10M rows x 8 elements, each a 32-hex-char deterministic
+    ciphertext drawn from a seeded vocabulary of 100k (HomoDet.compare = string equality).
+    The table (chars, offsets, 32-bit fingerprints) is built once in setup, as a resident index."""
+
+    ELEMS, WIDTH, VOCAB = 8, 32, 100_000
+
+    def setup(self):
+        import numpy as np
+        rng = np.random.default_rng(self.args.seed)
+        vocab = rng.integers(0, 16, size=(self.VOCAB, self.WIDTH), dtype=np.uint8)
+        self.vocab = np.where(vocab < 10, vocab + 48, vocab + 87).astype(np.uint8)  # '0'-'9','a'-'f'
+        nel = self.mine * self.ELEMS
+        self.pick = rng.integers(0, self.VOCAB, size=nel, dtype=np.int64)
+        chars = self.vocab[self.pick].tobytes()
+        elem_off = np.arange(nel + 1, dtype=np.uint64) * self.WIDTH
+        row_off = np.arange(self.mine + 1, dtype=np.uint64) * self.ELEMS
+        self.tab = self.ddshe.StrTable(self.eng, chars=chars, elem_off=elem_off, row_off=row_off)
+        del chars
+        self.needles = [self.vocab[j].tobytes().decode() for j in (11, 222, 3333)]
+
+    def step(self):
+        a = self.tab.search_entry(self.needles, False)
+        b = self.tab.search_eq(3, self.needles[0])
+        return a, b
+
+    def report(self, res, elapsed):
+        import numpy as np
+        a = self.args
+        ok = None
+        if a.verify and self.world == 1:
+            p = self.pick.reshape(self.mine, self.ELEMS)
+            want_or = np.nonzero(np.isin(p, [11, 222, 3333]).any(axis=1))[0]
+            want_eq = np.nonzero(p[:, 3] == 11)[0]
+            ok = bool(np.array_equal(res[0], want_or) and np.array_equal(res[1], want_eq))
+            if not ok:
+                print("VERIFY FAILED", file=sys.stderr)
+        _, _, dev_ms, _ = self.eng.timing()
+        scan_s = dev_ms / 1e3 / (2 * a.steps)
+        # per scan: the 4-byte fingerprints of the elements it must look at (OR: all; Eq: one per
+        # row + that row's 8-byte offset) + one 4-byte id per match
+        alg_or = self.mine * 4 * self.ELEMS + 4 * len(res[0])
+        alg_eq = self.mine * (8 + 4) + 4 * len(res[1])
+        alg = (alg_or + alg_eq) / 2
+        roof = {"bound": "hbm", "kernel": "k_str_any / k_str_eq + k_flag_count/k_ope_scatter (device time)",
+                "achieved": alg / scan_s / 1e9, "peak": 8000.0, "unit": "GB/s", "frac": alg / scan_s / 1e9 / 8000.0,
+                "avg_scan_ms": scan_s * 1e3, "algorithmic_bytes": alg, "traffic": None}
+        cpu = None
+        if self.world == 1 and not a.no_cpu_baseline:
+            from oracle import homo
+            sample = 200_000
+            rows = [[self.vocab[j].tobytes().decode() for j in r] for r in
+                    self.pick[: sample * self.ELEMS].reshape(sample, self.ELEMS)]
+            keyed = list(enumerate(rows))
+            t = time.perf_counter()
+            homo.search_entry("SearchEntryOR", keyed, self.needles)
+            dt = time.perf_counter() - t
+            cpu = {"value": sample / dt, "unit": "rows/s", "cores": 1, "kind": "port",
+                   "sample": f"first {sample} rows, SearchEntryOR restated in Python (oracle/homo.py), {dt:.2f}s"}
+        out = self.common("Deterministic-equality scan rows/sec (SearchEntryOR + SearchEq)",
+                          self.total * 2 * a.steps / elapsed, "rows/s", elapsed, "det_entry_search_10Mx8",
+                          {"elements_per_row": self.ELEMS, "element_bytes": self.WIDTH})
+        out.update(data="synthetic (seeded 32-hex-char ciphertext vocabulary)", dtype="u64 digest + u8",
+                   roofline=roof, cpu_baseline=cpu, verified=ok, matches={"or": len(res[0]), "eq": len(res[1])})
+        return out
+
+    def close(self):
+        self.tab.close()
 
 
 def cpu_encrypt_baseline(k, rcol, ms, seconds, out_col=None):

@@ -1593,10 +1593,11 @@ struct dds_strtab {
   dds_ctx* ctx = nullptr;
   size_t nrows = 0, nelems = 0, nchars = 0;
   uint8_t* chars = nullptr;
-  uint64_t *elem_off = nullptr, *row_off = nullptr, *digest = nullptr;
+  uint64_t *elem_off = nullptr, *row_off = nullptr;
+  uint32_t* fp = nullptr;  // per-element 32-bit fingerprint
   std::mutex mu;
   ~dds_strtab() {
-    for (void* p : {(void*)chars, (void*)elem_off, (void*)row_off, (void*)digest})
+    for (void* p : {(void*)chars, (void*)elem_off, (void*)row_off, (void*)fp})
       if (p) (void)hipFree(p);
   }
 };
@@ -1622,7 +1623,7 @@ int dds_strtab_create(dds_ctx* ctx, const char* chars, const uint64_t* elem_offs
     if (hipMalloc(&t->chars, std::max<size_t>(t->nchars, 1)) != hipSuccess ||
         hipMalloc(&t->elem_off, (nelems + 1) * 8) != hipSuccess ||
         hipMalloc(&t->row_off, (nrows + 1) * 8) != hipSuccess ||
-        hipMalloc(&t->digest, std::max<size_t>(nelems, 1) * 8) != hipSuccess)
+        hipMalloc(&t->fp, std::max<size_t>(nelems, 1) * 4) != hipSuccess)
       return fail(DDS_E_NOMEM, "string table allocation");
     WorkerLease wl(ctx);
     int rc;
@@ -1630,7 +1631,7 @@ int dds_strtab_create(dds_ctx* ctx, const char* chars, const uint64_t* elem_offs
     if (t->nchars) HIP_TRY(hipMemcpyAsync(t->chars, chars, t->nchars, hipMemcpyHostToDevice, wl.st));
     HIP_TRY(hipMemcpyAsync(t->elem_off, elem_offsets, (nelems + 1) * 8, hipMemcpyHostToDevice, wl.st));
     HIP_TRY(hipMemcpyAsync(t->row_off, row_offsets, (nrows + 1) * 8, hipMemcpyHostToDevice, wl.st));
-    HIP_TRY(launch_str_digest(t->chars, t->elem_off, nelems, t->digest, wl.st));
+    HIP_TRY(launch_str_digest(t->chars, t->elem_off, nelems, t->fp, wl.st));
     HIP_TRY(hipStreamSynchronize(wl.st));
     *out = t.release();
     return DDS_OK;
@@ -1664,17 +1665,30 @@ int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values
   if ((rc = wl.acquire())) return rc;
   Worker* w = wl.w;
   HIP_TRY(w->in2.ensure(std::max<size_t>(nb.size(), 1)));
-  HIP_TRY(w->x.ensure(nrows * 8));
+  HIP_TRY(w->x.ensure(nrows * 4));
   HIP_TRY(w->misc.ensure(ope_scratch_bytes(nrows)));
   HIP_TRY(w->flags.ensure(16));
   if (!device_out) HIP_TRY(w->out.ensure(nrows * 4));
   if (!nb.empty()) HIP_TRY(hipMemcpyAsync(w->in2.p, nb.data(), nb.size(), hipMemcpyHostToDevice, wl.st));
   record_time(ctx, w, wl.st, true, 2);
-  HIP_TRY(launch_str_scan(t->row_off + row0, nrows, t->elem_off, t->chars, t->digest, w->in2.as<uint8_t>(), nd, mode,
-                          position, negate, w->x.as<int64_t>(), wl.st));
+  uint32_t* flags = w->x.as<uint32_t>();
+  if (mode == 0) {
+    HIP_TRY(launch_str_eq(t->row_off + row0, nrows, t->elem_off, t->chars, t->fp, w->in2.as<uint8_t>(), nd, position,
+                          negate, flags, wl.st));
+  } else {
+    uint64_t e_first = 0, e_last = 0;  // element range of rows [row0, row0 + nrows)
+    HIP_TRY(hipMemcpy(&e_first, t->row_off + row0, 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&e_last, t->row_off + row0 + nrows, 8, hipMemcpyDeviceToHost));
+    if (row0 == 0 && nrows == t->nrows) {
+      e_first = 0;
+      e_last = t->nelems;
+    }
+    HIP_TRY(launch_str_any(t->fp, e_first, e_last - e_first, t->row_off + row0, nrows, t->elem_off, t->chars,
+                           w->in2.as<uint8_t>(), nd, flags, wl.st));
+  }
   uint32_t* dst = device_out ? out_rows : w->out.as<uint32_t>();
-  HIP_TRY(launch_ope_filter(w->x.as<int64_t>(), nullptr, nrows, 0, DDS_OPE_GT, w->misc.p, w->flags.as<uint64_t>(), dst,
-                            wl.st));
+  const uint32_t req = mode == 2 ? (1u << nvalues) - 1u : 0u;
+  HIP_TRY(launch_flag_compact(flags, nrows, req, w->misc.p, w->flags.as<uint64_t>(), dst, wl.st));
   record_time(ctx, w, wl.st, false, 2);
   uint64_t total = 0;
   HIP_TRY(hipMemcpyAsync(&total, w->flags.p, 8, hipMemcpyDeviceToHost, wl.st));

@@ -479,6 +479,48 @@ __global__ void __launch_bounds__(kOpeBlock) k_ope_count(const int64_t* __restri
   }
 }
 
+// Row-flag compaction front end (deterministic-equality scans): same tile layout and masks as
+// k_ope_count, predicate on u32 row flags: req == 0 -> flag != 0, else (flag & req) == req.
+__global__ void __launch_bounds__(kOpeBlock) k_flag_count(const uint32_t* __restrict__ flags, size_t n, uint32_t req,
+                                                          uint32_t* __restrict__ masks,
+                                                          uint32_t* __restrict__ counts) {
+  __shared__ uint32_t wsum[kOpeBlock / 64];
+  const size_t t0 = (size_t)blockIdx.x * kOpeTile + 4 * (size_t)threadIdx.x;
+  uint32_t f[kOpeItems];
+  if (t0 + (kOpeGroups - 1) * 4 * kOpeBlock + 3 < n) {
+#pragma unroll
+    for (int k = 0; k < kOpeGroups; ++k) {
+      const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(flags + t0 + (size_t)k * 4 * kOpeBlock));
+      f[4 * k] = x.x;
+      f[4 * k + 1] = x.y;
+      f[4 * k + 2] = x.z;
+      f[4 * k + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kOpeGroups; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t r = t0 + (size_t)k * 4 * kOpeBlock + j;
+        f[4 * k + j] = r < n ? flags[r] : 0u;
+      }
+  }
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < kOpeItems; ++i)
+    if (req ? (f[i] & req) == req : f[i] != 0) m |= 1u << i;
+  masks[(size_t)blockIdx.x * kOpeBlock + threadIdx.x] = m;
+  uint32_t s = __builtin_popcount(m);
+  for (int off = 32; off >= 1; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    for (int w = 0; w < kOpeBlock / 64; ++w) c += wsum[w];
+    counts[blockIdx.x] = c;
+  }
+}
+
 __global__ void __launch_bounds__(kOpeBlock) k_ope_scatter(const uint32_t* __restrict__ masks,
                                                            const uint32_t* __restrict__ counts,
                                                            uint32_t* __restrict__ out, uint64_t* __restrict__ total) {
@@ -757,6 +799,17 @@ hipError_t launch_gather_rows(const uint32_t* T, size_t tstride, uint32_t tcount
 size_t ope_blocks(size_t n) { return (n + kOpeTile - 1) / kOpeTile; }
 
 size_t ope_scratch_bytes(size_t n) { return ope_blocks(n) * (4 + 4 * kOpeBlock) + 8; }
+
+hipError_t launch_flag_compact(const uint32_t* flags, size_t n, uint32_t req, void* scratch, uint64_t* total,
+                               uint32_t* out, hipStream_t st) {
+  const size_t nb = ope_blocks(n);
+  if (nb == 0) return hipSuccess;
+  uint32_t* counts = (uint32_t*)scratch;
+  uint32_t* masks = counts + nb;
+  hipLaunchKernelGGL(k_flag_count, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, flags, n, req, masks, counts);
+  hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, masks, counts, out, total);
+  return hipGetLastError();
+}
 
 hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
                              uint64_t* total, uint32_t* out, hipStream_t st) {

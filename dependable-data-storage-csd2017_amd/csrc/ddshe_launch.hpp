@@ -6,6 +6,8 @@
 
 namespace ddshe {
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // 16-byte vector loads
+
 // per-modulus constant block: 5 vectors of S r27 limbs each
 enum { kConstN = 0, kConstRmod = 1, kConstR2 = 2, kConstOne = 3, kConstN2x = 4, kConstCount = 5 };
 
@@ -58,6 +60,9 @@ hipError_t launch_synth_rows(int S, const uint32_t* T, size_t tstride, uint32_t 
                              const uint32_t* consts, uint32_t n0, uint32_t* X, size_t xstride, hipStream_t st);
 size_t ope_blocks(size_t n);
 size_t ope_scratch_bytes(size_t n);  // per-tile match counts + per-thread match masks
+// rows with flags[r] != 0 (req == 0) or (flags[r] & req) == req -> ascending ids; scratch as above
+hipError_t launch_flag_compact(const uint32_t* flags, size_t n, uint32_t req, void* scratch, uint64_t* total,
+                               uint32_t* out, hipStream_t st);
 hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
                              uint64_t* total, uint32_t* out, hipStream_t st);
 // OPE ordering (ddshe_sort.hip): stable radix sort of the int64 column -> row ids
@@ -66,7 +71,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
                             uint32_t* out_ids, hipStream_t st);
 // deterministic-equality scans (ddshe_strscan.hip)
 // 64-bit digest of an element string (FNV-1a over the bytes, splitmix finaliser); identical on
-// host (needles) and device (table)
+// host (needles) and device (table). The table keeps its top 32 bits as a per-element fingerprint.
 __host__ __device__ inline uint64_t str_digest(const uint8_t* p, uint64_t len) {
   uint64_t h = 0xcbf29ce484222325ull ^ len;
   for (uint64_t i = 0; i < len; ++i) h = (h ^ p[i]) * 0x100000001b3ull;
@@ -82,11 +87,17 @@ struct StrNeedles {  // up to 3 items (SearchEntryAND/OR triplets), bytes in a d
   uint64_t off[3];
   int n;
 };
-hipError_t launch_str_digest(const uint8_t* chars, const uint64_t* elem_off, size_t nelems, uint64_t* digest,
+hipError_t launch_str_digest(const uint8_t* chars, const uint64_t* elem_off, size_t nelems, uint32_t* fp,
                              hipStream_t st);
-hipError_t launch_str_scan(const uint64_t* row_off, size_t nrows, const uint64_t* elem_off, const uint8_t* chars,
-                           const uint64_t* digest, const uint8_t* nchars, const StrNeedles& nd, int mode,
-                           uint64_t position, int negate, int64_t* flags, hipStream_t st);
+// SearchEq/NEq: flags[r] = contents(position) == needle 0 (xor negate), rows with length-1 > position
+hipError_t launch_str_eq(const uint64_t* row_off, size_t nrows, const uint64_t* elem_off, const uint8_t* chars,
+                         const uint32_t* fp, const uint8_t* nchars, const StrNeedles& nd, uint64_t position,
+                         int negate, uint32_t* flags, hipStream_t st);
+// SearchEntry/OR/AND/IsElement: flags[row] |= bit j for every element equal to needle j (flags zeroed
+// by the launcher); elements [e_first, e_first + nelems), rows [0, nrows) of row_off
+hipError_t launch_str_any(const uint32_t* fp, uint64_t e_first, size_t nelems, const uint64_t* row_off, size_t nrows,
+                          const uint64_t* elem_off, const uint8_t* chars, const uint8_t* nchars, const StrNeedles& nd,
+                          uint32_t* flags, hipStream_t st);
 hipError_t launch_plain_sum(const uint32_t* X, size_t stride, size_t count, int S, size_t nthreads, uint64_t* part,
                             uint64_t* out, hipStream_t st);
 // unbounded product tree level: rows (2p, 2p+1) of A[count][len] (radix 2^16 in u32)
