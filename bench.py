@@ -554,44 +554,73 @@ class EntrySearchWorkload(_Workload):
 
 
 def cpu_encrypt_baseline(k, rcol, ms, seconds, out_col=None):
-    """Paillier encryption restated on the host (oracle/homo.py: Python int pow, one thread) on
-    the first rows of the same r column; the GPU ciphertexts of those rows are compared."""
-    from oracle import homo
+    """Paillier encryption g^m r^n mod n^2 with OpenSSL BN_mod_exp (Montgomery + sliding window,
+    oracle/csrc/bn_baseline.c), public key, 1 thread and cpu_threads() threads, on the first rows of
+    the same r column; the GPU ciphertexts of those rows are compared."""
+    from oracle import cref
+    rs = rcol.read(0, min(len(rcol), 64))
     t = time.perf_counter()
-    done, i = 0, 0
-    rs = rcol.read(0, min(len(rcol), 256))
-    out = []
-    while time.perf_counter() - t < seconds and i < len(rs):
-        out.append(homo.paillier_encrypt(int(ms[i]), rs[i], k))
-        i += 1
+    cref.bn_paillier_encrypt(k["n"], k["g"], ms[:8], rs[:8], 1)
+    rate = 8 / (time.perf_counter() - t)
+    sample = int(min(len(rcol), max(16, rate * seconds), 4096))
+    rs = rcol.read(0, sample)
+    t = time.perf_counter()
+    ref = cref.bn_paillier_encrypt(k["n"], k["g"], ms[:sample], rs, 1)
     dt = time.perf_counter() - t
-    done = i
-    res = {"value": done / dt, "unit": "encrypt/s", "cores": 1, "kind": "port",
-           "sample": f"first {done} rows, g^m r^n mod n^2 with Python int pow (public key), {dt:.1f}s"}
+    th = cpu_threads()
+    sample_mt = min(len(rcol), sample * th)
+    rs_mt = rcol.read(0, sample_mt)
+    t = time.perf_counter()
+    cref.bn_paillier_encrypt(k["n"], k["g"], ms[:sample_mt], rs_mt, th)
+    dt_mt = time.perf_counter() - t
+    res = {"value": sample / dt, "unit": "encrypt/s", "cores": 1, "kind": "port",
+           "sample": f"first {sample} rows, g^m r^n mod n^2 with OpenSSL BN_mod_exp (public key), {dt:.1f}s",
+           "multi_thread": {"value": sample_mt / dt_mt, "cores": th, "sample": f"first {sample_mt} rows"}}
     if out_col is not None:
-        res["gpu_matches_sample"] = out_col.read(0, done) == out
+        res["gpu_matches_sample"] = out_col.read(0, sample) == ref
     return res
 
 
+def cpu_threads():
+    """Host threads for the multi-threaded baseline: the box's CPU share for one GPU (16), not
+    os.cpu_count(), which reports the whole machine there."""
+    return max(1, min(16, os.cpu_count() or 1))
+
+
 def cpu_baseline(col, nsq, mb, seconds):
-    """Reference fold restated in C (oracle/csrc/fold_ref.c: BigInteger multiply+mod),
-    1 thread, on a bounded prefix of the same column; also checks the GPU on that prefix."""
+    """Reference fold restated with OpenSSL (oracle/csrc/bn_baseline.c: acc = acc*x mod N with
+    BN_mod_mul, the BigInteger multiply+mod analogue), 1 thread as the reference's single
+    onComplete loop, on a bounded prefix of the same column; the GPU fold of that prefix is compared.
+    Also: the same prefix sliced over cpu_threads() threads, and the schoolbook C restatement."""
     from oracle import cref
-    calib = min(len(col), 2000)
+    calib = min(len(col), 4000)
     ops = b"".join(x.to_bytes(mb, "big") for x in col.read(0, calib))
     mod_be = nsq.to_bytes(mb, "big")
     t = time.perf_counter()
-    cref.fold_be(mod_be, ops, mb, calib)
+    cref.bn_fold_be(mod_be, ops, mb, calib)
     rate = (calib - 1) / (time.perf_counter() - t)
     sample = int(min(len(col), max(calib, rate * seconds)))
     ops = b"".join(x.to_bytes(mb, "big") for x in col.read(0, sample))
     t = time.perf_counter()
-    ref = cref.fold_be(mod_be, ops, mb, sample)
+    ref = cref.bn_fold_be(mod_be, ops, mb, sample)
     dt = time.perf_counter() - t
+    th = cpu_threads()
+    t = time.perf_counter()
+    ref_mt = cref.bn_fold_be(mod_be, ops, mb, sample, th)
+    dt_mt = time.perf_counter() - t
+    small = min(sample, 20000)
+    t = time.perf_counter()
+    ref_sb = cref.fold_be(mod_be, ops[: small * mb], mb, small)
+    dt_sb = time.perf_counter() - t
     gpu = col.fold(0, sample)
     return {"value": (sample - 1) / dt, "unit": "HomoAdd/s", "cores": 1, "kind": "port",
-            "sample": f"first {sample} rows of the same column, acc=acc*x mod n^2 (schoolbook+Knuth D), {dt:.1f}s",
-            "gpu_matches_sample": gpu == int.from_bytes(ref, "big")}
+            "sample": f"first {sample} rows of the same column, acc=acc*x mod N with OpenSSL BN_mod_mul, {dt:.1f}s",
+            "gpu_matches_sample": gpu == int.from_bytes(ref, "big") == int.from_bytes(ref_mt, "big"),
+            "multi_thread": {"value": (sample - 1) / dt_mt, "cores": th,
+                             "sample": "same prefix in contiguous slices, partials combined"},
+            "schoolbook_port": {"value": (small - 1) / dt_sb, "cores": 1,
+                                "sample": f"first {small} rows, oracle/csrc/fold_ref.c (schoolbook + Knuth D)",
+                                "matches": int.from_bytes(ref_sb, "big") == col.fold(0, small)}}
 
 
 if __name__ == "__main__":

@@ -206,3 +206,22 @@ def test_order_route_semantics():
     assert homo.order("OrderSL", rows, 1) == ["a", "b", "c", "d", "g", "f"]  # only f holds position 1
     with pytest.raises(ValueError):
         homo.order("OrderLS", rows, 0)                                   # "x".toLong
+
+
+def test_openssl_baselines_match_oracle(keys):
+    """The OpenSSL CPU baselines (bench.py cpu_baseline) compute what the oracle computes."""
+    from oracle import cref
+    if not os.path.exists(cref.BNLIB) and not os.path.exists("/usr/include/openssl/bn.h"):
+        pytest.skip("OpenSSL headers absent")
+    k = keys["paillier1024_seed1"]
+    rng = random.Random(5)
+    N = k["nsquare"]
+    xs = [rng.randrange(N) for _ in range(101)]
+    mb = (N.bit_length() + 7) // 8
+    ops = b"".join(x.to_bytes(mb, "big") for x in xs)
+    want = homo.modmul_fold(xs, N)
+    for threads in (1, 4):
+        assert int.from_bytes(cref.bn_fold_be(N.to_bytes(mb, "big"), ops, mb, len(xs), threads), "big") == want
+    ms = [rng.randrange(10000) for _ in range(6)]
+    rs = [rng.randrange(1, k["n"]) for _ in ms]
+    assert cref.bn_paillier_encrypt(k["n"], k["g"], ms, rs, 2) == [homo.paillier_encrypt(m, r, k) for m, r in zip(ms, rs)]
