@@ -8,7 +8,7 @@
 //
 // Per 8-bit digit pass (8 passes; the last one has 257 buckets: the validity of the row moves it
 // to the end / front): k_rs_hist (per-tile digit counts, digit-major) -> k_rs_scan_digits (per-digit
-// scan over tiles, one block per digit) + k_rs_scan_base (digit bases) -> k_rs_scatter (stable rank inside the tile: each wave walks a contiguous
+// scan over tiles, one block per digit; the scatter blocks scan the 257 digit totals themselves) -> k_rs_scatter (stable rank inside the tile: each wave walks a contiguous
 // quarter of the tile, peers with equal digits are found with 9 ballots, per-wave digit counters
 // in LDS). HBM traffic per pass: 12 B/row read twice (hist + scatter) + 12 B/row written.
 #include <hip/hip_runtime.h>
@@ -26,15 +26,74 @@ constexpr int kRsDigits = 257;                    // 256 + the validity bucket o
 constexpr uint32_t kRsNone = 511;                 // digit of a lane past the end (never counted)
 constexpr uint64_t kSign = 0x8000000000000000ull;
 
-// rows lacking the position get key 0 so that passes 0..6 keep them in input order; the last
-// pass moves them to their bucket (256 / 0)
-__global__ void k_rs_prep(const int64_t* __restrict__ col, const uint8_t* __restrict__ valid, size_t n, int desc,
-                          uint64_t* __restrict__ keys, uint32_t* __restrict__ ids) {
+// rows lacking the position get key 0 so that earlier passes keep them in input order; the last
+// pass moves them to their bucket (256 / 0). Also reduces OR / AND of all keys (per block, then
+// k_rs_red): a byte where they agree is the same digit for every row, and its pass is skipped.
+constexpr int kRsPrepRows = 16;  // rows per thread of k_rs_prep
+
+__global__ void __launch_bounds__(256) k_rs_prep(const int64_t* __restrict__ col, const uint8_t* __restrict__ valid,
+                                                 size_t n, int desc, uint64_t* __restrict__ keys,
+                                                 uint64_t* __restrict__ part) {
+  __shared__ uint64_t so[4], sa[4];
+  uint64_t o = 0, a = ~0ull;
+  const size_t base = (size_t)blockIdx.x * 256 * kRsPrepRows + threadIdx.x;
+#pragma unroll 4
+  for (int k = 0; k < kRsPrepRows; ++k) {
+    const size_t i = base + (size_t)k * 256;
+    if (i < n) {
+      const uint64_t u = (uint64_t)col[i] ^ kSign;  // signed order -> unsigned order
+      const uint64_t key = (valid && !valid[i]) ? 0ull : (desc ? ~u : u);
+      keys[i] = key;
+      o |= key;
+      a &= key;
+    }
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    o |= (uint64_t)__shfl_xor((long long)o, off);
+    a &= (uint64_t)__shfl_xor((long long)a, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    so[threadIdx.x >> 6] = o;
+    sa[threadIdx.x >> 6] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = so[0] | so[1] | so[2] | so[3];
+    part[2 * blockIdx.x + 1] = sa[0] & sa[1] & sa[2] & sa[3];
+  }
+}
+
+// OR / AND of the per-block partials -> red[0..1] (one block)
+__global__ void __launch_bounds__(1024) k_rs_red(const uint64_t* __restrict__ part, size_t nparts,
+                                                 uint64_t* __restrict__ red) {
+  __shared__ uint64_t so[16], sa[16];
+  uint64_t o = 0, a = ~0ull;
+  for (size_t i = threadIdx.x; i < nparts; i += 1024) {
+    o |= part[2 * i];
+    a &= part[2 * i + 1];
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    o |= (uint64_t)__shfl_xor((long long)o, off);
+    a &= (uint64_t)__shfl_xor((long long)a, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    so[threadIdx.x >> 6] = o;
+    sa[threadIdx.x >> 6] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 16; ++w) {
+      o |= so[w];
+      a &= sa[w];
+    }
+    red[0] = so[0] | o;
+    red[1] = sa[0] & a;
+  }
+}
+
+__global__ void k_rs_iota(uint32_t* __restrict__ ids, size_t n) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t u = (uint64_t)col[i] ^ kSign;  // signed order -> unsigned order
-  keys[i] = (valid && !valid[i]) ? 0ull : (desc ? ~u : u);
-  ids[i] = (uint32_t)i;
+  if (i < n) ids[i] = (uint32_t)i;
 }
 
 __device__ __forceinline__ uint32_t rs_digit(uint64_t k, uint32_t id, const uint8_t* __restrict__ valid, int pass,
@@ -60,24 +119,31 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_hist(const uint64_t* __restrict
   for (int d = threadIdx.x; d < kRsDigits; d += kRsBlock) cnt[d] = 0;
   __syncthreads();
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const bool need_id = pass == 7 && valid;
   // all loads first (independent, in flight together), then the LDS counting
-  uint32_t d[kRsItems];
   uint64_t key[kRsItems];
   uint32_t id[kRsItems];
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {  // unconditional loads (index clamped), masked below
     const size_t i = min(rs_row(blockIdx.x, wid, k, lane), n - 1);
     key[k] = keys[i];
-    id[k] = ids[i];
+    id[k] = need_id ? (ids ? ids[i] : (uint32_t)i) : 0u;
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
     const size_t i = rs_row(blockIdx.x, wid, k, lane);
-    d[k] = i < n ? rs_digit(key[k], id[k], valid, pass, desc) : kRsNone;
-  }
+    const uint32_t d = i < n ? rs_digit(key[k], id[k], valid, pass, desc) : kRsNone;
+    // one LDS atomic per distinct digit of the wave (OPE columns repeat digits a lot; measured
+    // faster than per-wave histograms with one atomic per row)
+    uint64_t peers = ~0ull;
 #pragma unroll
-  for (int k = 0; k < kRsItems; ++k)
-    if (d[k] != kRsNone) atomicAdd(&cnt[d[k]], 1u);
+    for (int b = 0; b < 9; ++b) {
+      const uint64_t bal = __ballot((d >> b) & 1u);
+      peers &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    if (d != kRsNone && (peers & lt) == 0) atomicAdd(&cnt[d], (uint32_t)__popcll(peers));
+  }
   __syncthreads();
   for (int d = threadIdx.x; d < kRsDigits; d += kRsBlock) hist[(size_t)d * nblocks + blockIdx.x] = cnt[d];
 }
@@ -109,40 +175,47 @@ __global__ void __launch_bounds__(256) k_rs_scan_digits(uint32_t* __restrict__ h
   if (threadIdx.x == 255) dtot[blockIdx.x] = part[255];
 }
 
-// exclusive scan of the kRsDigits digit totals -> dbase (one block of 512 threads)
-__global__ void __launch_bounds__(512) k_rs_scan_base(const uint32_t* __restrict__ dtot, uint32_t* __restrict__ dbase) {
-  __shared__ uint32_t part[512];
-  const int t = threadIdx.x;
-  part[t] = t < kRsDigits ? dtot[t] : 0u;
-  __syncthreads();
-  for (int off = 1; off < 512; off <<= 1) {
-    const uint32_t v = t >= off ? part[t - off] : 0u;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  if (t < kRsDigits) dbase[t] = t ? part[t - 1] : 0u;
-}
-
 __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ ids,
                                                          const uint8_t* __restrict__ valid, size_t n, int pass,
                                                          int desc, const uint32_t* __restrict__ hist,
-                                                         const uint32_t* __restrict__ dbase, size_t nblocks,
+                                                         const uint32_t* __restrict__ dtot, size_t nblocks,
                                                          uint64_t* __restrict__ keys_out,
                                                          uint32_t* __restrict__ ids_out) {
   __shared__ uint32_t cnt[kRsWaves][kRsDigits];
+  __shared__ uint32_t dbase[kRsDigits + 1];
   for (int d = threadIdx.x; d < kRsWaves * kRsDigits; d += kRsBlock) (&cnt[0][0])[d] = 0;
-  __syncthreads();
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t lt = (1ull << lane) - 1ull;
+  if (wid == 0) {  // digit bases: exclusive scan of the kRsDigits totals (5 per lane, then a wave scan)
+    uint32_t v[5], s = 0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const int d = lane * 5 + q;
+      v[q] = d < kRsDigits ? dtot[d] : 0u;
+      s += v[q];
+    }
+    uint32_t inc = s;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)inc, off);
+      if (lane >= off) inc += y;
+    }
+    uint32_t run = inc - s;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const int d = lane * 5 + q;
+      if (d <= kRsDigits) dbase[d] = run;
+      run += v[q];
+    }
+  }
+  __syncthreads();
   uint64_t key[kRsItems];
   uint32_t id[kRsItems], dr[kRsItems];  // dr = digit | rank << 9
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {  // all loads first, unconditional (index clamped), masked below
     const size_t i = min(rs_row(blockIdx.x, wid, k, lane), n - 1);
     key[k] = keys[i];
-    id[k] = ids[i];
+    id[k] = ids ? ids[i] : (uint32_t)i;  // ids == nullptr: first executed pass, identity
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
@@ -152,7 +225,7 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
     const uint32_t d = dr[k];
-    // lanes holding the same digit: AND of 9 bit-ballots
+    // lanes holding the same digit: AND of 9 bit-ballots (bit 8 only set in the last pass)
     uint64_t peers = ~0ull;
 #pragma unroll
     for (int b = 0; b < 9; ++b) {
@@ -190,8 +263,9 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
 
 size_t rs_blocks(size_t n) { return (n + kRsTile - 1) / kRsTile; }
 size_t rs_scratch_bytes(size_t n) {
-  // keys x2 (8 B), ids x1 extra (4 B; the other id buffer is the caller's output), histogram
-  return 2 * n * 8 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 512;
+  // keys x2 (8 B), ids x1 extra (4 B; the other id buffer is the caller's output), histogram, OR/AND
+  return 2 * n * 8 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 1024 +
+         16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows));
 }
 
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
@@ -203,23 +277,38 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   uint32_t* ib = (uint32_t*)(kb + n);
   uint32_t* hist = (uint32_t*)(((uintptr_t)(ib + n) + 255) & ~(uintptr_t)255);
   uint32_t* dtot = hist + (size_t)kRsDigits * nb;
-  uint32_t* dbase = dtot + kRsDigits;
-  // 8 passes (even): ids ping-pong out_ids -> ib -> out_ids ..., so the last pass writes out_ids
-  uint32_t* ia = out_ids;
-  uint32_t* ic = ib;
-  hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, col, valid, n, desc, ka, ia);
-  for (int pass = 0; pass < 8; ++pass) {
-    hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)nb), dim3(kRsBlock), 0, st, ka, ia, valid, n, pass, desc, hist, nb);
+  uint64_t* red = (uint64_t*)(((uintptr_t)(dtot + kRsDigits) + 15) & ~(uintptr_t)15);
+  uint64_t* part = red + 2;
+  const size_t pb = (n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows);
+  hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, ka, part);
+  hipLaunchKernelGGL(k_rs_red, dim3(1), dim3(1024), 0, st, part, pb, red);
+  uint64_t hred[2];
+  hipError_t e = hipMemcpyAsync(hred, red, sizeof(hred), hipMemcpyDeviceToHost, st);
+  if (e != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+  // passes whose byte differs between keys (+ the last one when rows may lack the position)
+  int passes[8], np = 0;
+  for (int p = 0; p < 8; ++p)
+    if ((((hred[0] ^ hred[1]) >> (8 * p)) & 0xFFu) || (p == 7 && valid)) passes[np++] = p;
+  if (np == 0) {
+    hipLaunchKernelGGL(k_rs_iota, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out_ids, n);
+    return hipGetLastError();
+  }
+  // executed pass j writes ids to out_ids when (np-1-j) is even, so the last one lands there
+  const uint32_t* ids_in = nullptr;  // identity before the first pass
+  for (int j = 0; j < np; ++j) {
+    const int pass = passes[j];
+    uint32_t* ids_out = ((np - 1 - j) % 2 == 0) ? out_ids : ib;
+    const bool last = j == np - 1;
+    hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)nb), dim3(kRsBlock), 0, st, ka, ids_in, valid, n, pass, desc, hist,
+                       nb);
     hipLaunchKernelGGL(k_rs_scan_digits, dim3(kRsDigits), dim3(256), 0, st, hist, nb, dtot);
-    hipLaunchKernelGGL(k_rs_scan_base, dim3(1), dim3(512), 0, st, dtot, dbase);
-    hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)nb), dim3(kRsBlock), 0, st, ka, ia, valid, n, pass, desc, hist,
-                       dbase, nb, pass == 7 ? nullptr : kb, ic);
+    hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)nb), dim3(kRsBlock), 0, st, ka, ids_in, valid, n, pass, desc,
+                       hist, dtot, nb, last ? nullptr : kb, ids_out);
     uint64_t* tk = ka;
     ka = kb;
     kb = tk;
-    uint32_t* ti = ia;
-    ia = ic;
-    ic = ti;
+    ids_in = ids_out;
   }
   return hipGetLastError();
 }

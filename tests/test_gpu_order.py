@@ -59,3 +59,21 @@ def test_order_routes_vs_oracle(eng):
     for position in (0, 1, 3):
         for route in ("OrderLS", "OrderSL"):
             assert routes.order(eng, route, keyed, position) == homo.order(route, keyed, position), (route, position)
+
+
+@pytest.mark.parametrize("kind", ["constant", "small_positive", "one_byte"])
+def test_order_skipped_passes(eng, kind):
+    """Columns whose keys agree on some bytes: those radix passes are skipped (OR/AND of the keys);
+    a constant column without the validity pass is the identity permutation."""
+    rng = np.random.default_rng(11)
+    n = 300_001
+    if kind == "constant":
+        col = np.full(n, -12345, dtype=np.int64)
+    elif kind == "small_positive":
+        col = rng.integers(0, 10_000, size=n, dtype=np.int64)
+    else:
+        col = (rng.integers(0, 256, size=n, dtype=np.int64) << 24) | 7
+    valid = (rng.random(n) > 0.2).astype(np.uint8)
+    for desc in (True, False):
+        assert np.array_equal(eng.ope_order(col, valid, desc), expected(col, valid, desc)), (kind, desc)
+        assert np.array_equal(eng.ope_order(col, None, desc), expected(col, np.ones(n, np.uint8), desc)), (kind, desc)
