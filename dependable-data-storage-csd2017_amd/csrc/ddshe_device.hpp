@@ -42,12 +42,15 @@ __device__ __forceinline__ uint32_t grp_bcast0(uint32_t x) {
   else if constexpr (TPI == 8) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x18);  // and_mask 0b11000
   else { static_assert(TPI == 16, "TPI"); return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150, 0xF, 0xF, false); }  // row_newbcast:0
 }
-// value of lane r+1 (caller masks the group's top lane)
+// value of lane r+1; the group's top lane receives the value of a group's lane 0 (TPI <= 4: its own
+// group's, quad_perm wraps; TPI 8: the next group's; TPI 16: 0 via bound_ctrl at the row end).
+// Montgomery steps pass lo0 through this, and lo0 == 0 on every group's lane 0, so the top lane
+// gets 0 without a select.
 template <int TPI>
 __device__ __forceinline__ uint32_t grp_from_next(uint32_t x) {
   if constexpr (TPI == 1) return 0u;
-  else if constexpr (TPI == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xF5, 0xF, 0xF, false);  // [1,1,3,3]
-  else if constexpr (TPI == 4) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xF9, 0xF, 0xF, false);  // [1,2,3,3]
+  else if constexpr (TPI == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+  else if constexpr (TPI == 4) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x39, 0xF, 0xF, false);  // [1,2,3,0]
   else return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x101, 0xF, 0xF, true);                          // row_shl:1
 }
 // value of lane r-1 (caller masks the group's bottom lane)
@@ -93,8 +96,9 @@ struct Mont {
     t[0] = (uint64_t)m * n[1] + (t[1] + (u0 >> kW));
 #pragma unroll
     for (int l = 2; l < L; ++l) t[l - 1] = (uint64_t)m * n[l] + t[l];
-    const uint32_t up = grp_from_next<TPI>(lo0);
-    t[L - 1] = top ? 0ull : (uint64_t)up;
+    // top lane: lo0 of a group's lane 0, which is 0 (see grp_from_next) — no select needed
+    (void)top;
+    t[L - 1] = (uint64_t)grp_from_next<TPI>(lo0);
   }
 
   // 64-bit lazy sums -> almost-normalised limbs (< 2^(W+1)) in a[].
