@@ -10,7 +10,8 @@
 // to the end / front): k_rs_hist (per-tile digit counts, digit-major) -> k_rs_scan_digits (per-digit
 // scan over tiles, one block per digit; the scatter blocks scan the 257 digit totals themselves) -> k_rs_scatter (stable rank inside the tile: each wave walks a contiguous
 // quarter of the tile, peers with equal digits are found with 9 ballots, per-wave digit counters
-// in LDS). HBM traffic per pass: 12 B/row read twice (hist + scatter) + 12 B/row written.
+// in LDS). HBM traffic per pass: 12 B/row read twice (hist + scatter) + 12 B/row written; the
+// validity of a row rides in bit 31 of its id (no random gather of valid[] in the last pass).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,13 +28,19 @@ constexpr uint32_t kRsNone = 511;                 // digit of a lane past the en
 constexpr uint64_t kSign = 0x8000000000000000ull;
 
 // rows lacking the position get key 0 so that earlier passes keep them in input order; the last
-// pass moves them to their bucket (256 / 0). Also reduces OR / AND of all keys (per block, then
-// k_rs_red): a byte where they agree is the same digit for every row, and its pass is skipped.
+// pass moves them to their bucket (256 / 0). The first executed pass derives the keys from the
+// column itself (no separate key buffer is written up front).
+__device__ __forceinline__ uint64_t rs_key_of(uint64_t raw, const uint8_t* __restrict__ valid, size_t i, int desc) {
+  const uint64_t u = raw ^ kSign;  // signed order -> unsigned order
+  return (valid && !valid[i]) ? 0ull : (desc ? ~u : u);
+}
+
+// OR / AND of all keys (per block, then k_rs_red): a byte where they agree is the same digit for
+// every row, and its pass is skipped. Reads the column once, writes nothing per row.
 constexpr int kRsPrepRows = 16;  // rows per thread of k_rs_prep
 
 __global__ void __launch_bounds__(256) k_rs_prep(const int64_t* __restrict__ col, const uint8_t* __restrict__ valid,
-                                                 size_t n, int desc, uint64_t* __restrict__ keys,
-                                                 uint64_t* __restrict__ part) {
+                                                 size_t n, int desc, uint64_t* __restrict__ part) {
   __shared__ uint64_t so[4], sa[4];
   uint64_t o = 0, a = ~0ull;
   const size_t base = (size_t)blockIdx.x * 256 * kRsPrepRows + threadIdx.x;
@@ -41,9 +48,7 @@ __global__ void __launch_bounds__(256) k_rs_prep(const int64_t* __restrict__ col
   for (int k = 0; k < kRsPrepRows; ++k) {
     const size_t i = base + (size_t)k * 256;
     if (i < n) {
-      const uint64_t u = (uint64_t)col[i] ^ kSign;  // signed order -> unsigned order
-      const uint64_t key = (valid && !valid[i]) ? 0ull : (desc ? ~u : u);
-      keys[i] = key;
+      const uint64_t key = rs_key_of((uint64_t)col[i], valid, i, desc);
       o |= key;
       a &= key;
     }
@@ -96,11 +101,21 @@ __global__ void k_rs_iota(uint32_t* __restrict__ ids, size_t n) {
   if (i < n) ids[i] = (uint32_t)i;
 }
 
+// Row id as carried between passes. vbit (n <= 2^31): bit 31 holds "row lacks the position", set
+// from a coalesced valid[i] read where the identity ids start, so the last pass reads it from the
+// id instead of gathering valid[id] at random; the last pass strips it.
+constexpr uint32_t kRsLack = 0x80000000u;
+__device__ __forceinline__ uint32_t rs_load_id(const uint32_t* __restrict__ ids, size_t i,
+                                               const uint8_t* __restrict__ valid, bool vbit) {
+  if (ids) return ids[i];
+  return (uint32_t)i | ((vbit && valid && !valid[i]) ? kRsLack : 0u);
+}
+
 __device__ __forceinline__ uint32_t rs_digit(uint64_t k, uint32_t id, const uint8_t* __restrict__ valid, int pass,
-                                             int desc) {
+                                             int desc, bool vbit) {
   uint32_t d = (uint32_t)(k >> (8 * pass)) & 0xFFu;
   if (pass == 7 && valid) {
-    const bool v = valid[id] != 0;
+    const bool v = vbit ? (id & kRsLack) == 0 : valid[id] != 0;
     d = desc ? (v ? d : 256u) : (v ? d + 1u : 0u);
   }
   return d;
@@ -114,7 +129,8 @@ __device__ __forceinline__ size_t rs_row(size_t tile, int wid, int k, int lane) 
 __global__ void __launch_bounds__(kRsBlock) k_rs_hist(const uint64_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ ids,
                                                       const uint8_t* __restrict__ valid, size_t n, int pass,
-                                                      int desc, uint32_t* __restrict__ hist, size_t nblocks) {
+                                                      int desc, bool vbit, uint32_t* __restrict__ hist,
+                                                      size_t nblocks) {
   __shared__ uint32_t cnt[kRsDigits];
   for (int d = threadIdx.x; d < kRsDigits; d += kRsBlock) cnt[d] = 0;
   __syncthreads();
@@ -127,13 +143,13 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_hist(const uint64_t* __restrict
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {  // unconditional loads (index clamped), masked below
     const size_t i = min(rs_row(blockIdx.x, wid, k, lane), n - 1);
-    key[k] = keys[i];
-    id[k] = need_id ? (ids ? ids[i] : (uint32_t)i) : 0u;
+    key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc);  // first pass: keys = the column
+    id[k] = need_id ? rs_load_id(ids, i, valid, vbit) : 0u;
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
     const size_t i = rs_row(blockIdx.x, wid, k, lane);
-    const uint32_t d = i < n ? rs_digit(key[k], id[k], valid, pass, desc) : kRsNone;
+    const uint32_t d = i < n ? rs_digit(key[k], id[k], valid, pass, desc, vbit) : kRsNone;
     // one LDS atomic per distinct digit of the wave (OPE columns repeat digits a lot; measured
     // faster than per-wave histograms with one atomic per row)
     uint64_t peers = ~0ull;
@@ -178,7 +194,8 @@ __global__ void __launch_bounds__(256) k_rs_scan_digits(uint32_t* __restrict__ h
 __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ ids,
                                                          const uint8_t* __restrict__ valid, size_t n, int pass,
-                                                         int desc, const uint32_t* __restrict__ hist,
+                                                         int desc, bool vbit, bool last,
+                                                         const uint32_t* __restrict__ hist,
                                                          const uint32_t* __restrict__ dtot, size_t nblocks,
                                                          uint64_t* __restrict__ keys_out,
                                                          uint32_t* __restrict__ ids_out) {
@@ -214,13 +231,13 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {  // all loads first, unconditional (index clamped), masked below
     const size_t i = min(rs_row(blockIdx.x, wid, k, lane), n - 1);
-    key[k] = keys[i];
-    id[k] = ids ? ids[i] : (uint32_t)i;  // ids == nullptr: first executed pass, identity
+    key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc);  // first pass: keys = the column
+    id[k] = rs_load_id(ids, i, valid, vbit);  // ids == nullptr: first executed pass, identity
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
     const size_t i = rs_row(blockIdx.x, wid, k, lane);
-    dr[k] = i < n ? rs_digit(key[k], id[k], valid, pass, desc) : kRsNone;
+    dr[k] = i < n ? rs_digit(key[k], id[k], valid, pass, desc, vbit) : kRsNone;
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
@@ -257,7 +274,7 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
     if (d == kRsNone) continue;
     const uint32_t dst = cnt[wid][d] + (dr[k] >> 9);
     if (keys_out) keys_out[dst] = key[k];
-    ids_out[dst] = id[k];
+    ids_out[dst] = (last && vbit) ? (id[k] & ~kRsLack) : id[k];
   }
 }
 
@@ -280,7 +297,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   uint64_t* red = (uint64_t*)(((uintptr_t)(dtot + kRsDigits) + 15) & ~(uintptr_t)15);
   uint64_t* part = red + 2;
   const size_t pb = (n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows);
-  hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, ka, part);
+  hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
   hipLaunchKernelGGL(k_rs_red, dim3(1), dim3(1024), 0, st, part, pb, red);
   uint64_t hred[2];
   hipError_t e = hipMemcpyAsync(hred, red, sizeof(hred), hipMemcpyDeviceToHost, st);
@@ -296,18 +313,20 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   }
   // executed pass j writes ids to out_ids when (np-1-j) is even, so the last one lands there
   const uint32_t* ids_in = nullptr;  // identity before the first pass
+  const uint64_t* kin = (const uint64_t*)col;  // raw column before the first pass
+  uint64_t* kout = ka;
   for (int j = 0; j < np; ++j) {
     const int pass = passes[j];
     uint32_t* ids_out = ((np - 1 - j) % 2 == 0) ? out_ids : ib;
     const bool last = j == np - 1;
-    hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)nb), dim3(kRsBlock), 0, st, ka, ids_in, valid, n, pass, desc, hist,
-                       nb);
+    const bool vbit = valid && n <= (size_t)kRsLack;
+    hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)nb), dim3(kRsBlock), 0, st, kin, ids_in, valid, n, pass, desc, vbit,
+                       hist, nb);
     hipLaunchKernelGGL(k_rs_scan_digits, dim3(kRsDigits), dim3(256), 0, st, hist, nb, dtot);
-    hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)nb), dim3(kRsBlock), 0, st, ka, ids_in, valid, n, pass, desc,
-                       hist, dtot, nb, last ? nullptr : kb, ids_out);
-    uint64_t* tk = ka;
-    ka = kb;
-    kb = tk;
+    hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)nb), dim3(kRsBlock), 0, st, kin, ids_in, valid, n, pass, desc,
+                       vbit, last, hist, dtot, nb, last ? nullptr : kout, ids_out);
+    kin = kout;
+    kout = kout == ka ? kb : ka;
     ids_in = ids_out;
   }
   return hipGetLastError();
