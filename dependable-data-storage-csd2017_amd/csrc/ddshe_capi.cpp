@@ -1058,8 +1058,9 @@ int window_schedule(const bn::Limbs& E, std::vector<uint32_t>* sched) {
 }
 
 // out[i] = g^m[i] * x[i]^E mod N on the device (d_m == nullptr: x[i]^E). x rows are rW,
-// fully normalised, < 2N. Processes the batch in chunks so the per-row window table
-// (nodd * S words per row) stays within ~2 GiB of HBM.
+// fully normalised, < 2N. Processes the batch in equal chunks so the per-row window table
+// (nodd * S words per row) stays within kModexpTabBytes of HBM.
+constexpr size_t kModexpTabBytes = (size_t)8 << 30;
 int modexp_device(Worker* w, hipStream_t st, ModConsts& mc, const bn::Limbs& E, const bn::Limbs* g,
                   const uint32_t* d_x, size_t xstride, const uint32_t* d_m, size_t count, uint32_t* d_out,
                   size_t ostride) {
@@ -1078,7 +1079,10 @@ int modexp_device(Worker* w, hipStream_t st, ModConsts& mc, const bn::Limbs& E, 
   if (!sched.empty())
     HIP_TRY(hipMemcpyAsync(d_sched, sched.data(), sched.size() * 4, hipMemcpyHostToDevice, st));
   const size_t row_bytes = (size_t)nodd * S * 4;
-  const size_t chunk = std::min(round_up(count, 64), std::max<size_t>(64, ((size_t)2 << 30) / row_bytes / 64 * 64));
+  // equal chunks (a short last chunk would leave most CUs idle for a whole ladder)
+  const size_t cap = std::max<size_t>(64, kModexpTabBytes / row_bytes / 64 * 64);
+  const size_t nch = (count + cap - 1) / cap;
+  const size_t chunk = round_up((count + nch - 1) / nch, 64);
   HIP_TRY(w->tab.ensure((size_t)nodd * S * chunk * 4));
   for (size_t c0 = 0; c0 < count; c0 += chunk) {
     const size_t cc = std::min(chunk, count - c0);

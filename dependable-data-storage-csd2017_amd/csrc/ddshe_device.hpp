@@ -286,8 +286,11 @@ struct Mont {
   }
 
   // Almost-normalised (limbs < 2^(W+1)) -> fully normalised (limbs < 2^W); value unchanged.
+  // After one round only limb 0 of a lane can hold 2^W (its carry-in landed on 2^W - 1); further
+  // rounds run only while some lane of the wave has that (wave-uniform test, almost never taken).
   __device__ __forceinline__ static void normalize(uint32_t (&a)[L], bool bottom) {
     for (int round = 0; round < TPI; ++round) {
+      if (round > 0 && !__builtin_amdgcn_ballot_w64((a[0] >> kW) != 0u)) break;
       uint32_t c = 0;
 #pragma unroll
       for (int l = 0; l < L; ++l) {
