@@ -99,9 +99,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DDSHE_DIST_BACKEND=gloo rehearses the N > 1 flow with every rank on one GPU (the partial
+    # gather then goes through host memory); the driver's multi-GPU runs use RCCL ("nccl").
+    backend = os.environ.get("DDSHE_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
+    coll_dev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
 
     import ddshe
     import ddshe.dist as ddist
@@ -113,7 +122,7 @@ def main():
     # shard rows by contiguous key range; weak scaling: each rank owns --rows rows
     total = args.rows if args.strong else args.rows * world
     row0, mine = ddist.shard_range(total, world, rank)
-    ctx = dict(args=args, eng=eng, world=world, rank=rank, local=local, total=total, row0=row0, mine=mine,
+    ctx = dict(args=args, coll_dev=coll_dev, eng=eng, world=world, rank=rank, local=local, total=total, row0=row0, mine=mine,
                per=(total + world - 1) // world, torch=torch, ddshe=ddshe, ddist=ddist)
     wl = {"sum": SumWorkload, "product_filter": ProductFilterWorkload, "encrypt_sum": EncryptSumWorkload,
           "order": OrderWorkload, "entry_search": EntrySearchWorkload}[args.workload](ctx)
@@ -139,7 +148,7 @@ def main():
     elapsed = time.perf_counter() - t0
     eng.set_timing(False)
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
@@ -168,7 +177,7 @@ class _Workload:
         if self.world == 1:
             return col.fold()
         part, rows = col.fold_partial()
-        parts, rows_all = self.ddist.gather_partials(part, rows, device=self.torch.device("cuda", self.local))
+        parts, rows_all = self.ddist.gather_partials(part, rows, device=self.coll_dev)
         if self.rank != 0:
             return None
         return self.eng.combine_partials(modulus, parts, rows_all)
