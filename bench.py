@@ -83,6 +83,8 @@ def main():
     ap.add_argument("--public", action="store_true", help="encrypt_sum: public-key path (no CRT)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="sum: skip the host-boundary (PCIe/decimal) rates")
+    ap.add_argument("--e2e-dec-rows", type=int, default=100_000, help="sum: decimal-route sample rows")
     ap.add_argument("--verify", type=int, default=1, help="check the result on rank 0")
     args = ap.parse_args()
     dflt = {"sum": (10_000_000, 20, 3, 2), "product_filter": (10_000_000, 10, 2, 3),
@@ -242,12 +244,53 @@ class SumWorkload(_Workload):
         cpu = None
         if self.world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(self.col, nsq, (nsq.bit_length() + 7) // 8, a.cpu_seconds)
+        e2e = None
+        if self.world == 1 and not a.no_e2e:
+            e2e = self.end_to_end(res)
         out = self.common("Paillier homomorphic adds/sec (2048-bit key, mod n^2)",
                           (self.total - 1) * a.steps / elapsed, "HomoAdd/s", elapsed,
                           "paillier_sumall_fold_10M_2048bit",
                           {"key_bits": key["n"].bit_length(), "modulus_bits": nsq.bit_length()})
         out.update(data="synthetic (seeded Paillier ciphertexts, committed key)", roofline=roof, cpu_baseline=cpu,
-                   verified=ok)
+                   end_to_end=e2e, verified=ok)
+        return out
+
+    def end_to_end(self, res):
+        """Host-boundary rates, outside the timed region (never `value`): (1) the binary boundary
+        (dds_paillier_sum on a host buffer of 512-byte big-endian rows: H2D + ingest + fold), all rows;
+        (2) the decimal route (BigInteger.toString rows, DDSRestServer.scala:417-422: host chars ->
+        GPU parse -> resident column -> fold -> decimal result) on a bounded sample."""
+        import numpy as np
+        nsq = self.nsq
+        out = {}
+        buf = self.col.read_buffer(0, self.mine)
+        for rep in range(2):  # first call sizes the context's device buffers
+            t = time.perf_counter()
+            got = self.eng.fold_buffer(nsq, buf)
+            dt = time.perf_counter() - t
+        out["binary"] = {"rows": self.mine, "seconds": dt, "rows_per_s": self.mine / dt,
+                         "host_GBps": buf.nbytes / dt / 1e9, "matches": got == res,
+                         "path": "dds_paillier_sum (pageable host buffer -> H2D -> k_ingest_be -> fold)"}
+        del buf
+        k = min(self.mine, self.args.e2e_dec_rows)
+        rows = [str(x) for x in self.col.read(0, k)]
+        chars = "".join(rows).encode()  # Arrow-style (chars, offsets): how a JNA shim passes String[]
+        offs = np.zeros(k + 1, dtype=np.uint64)
+        np.cumsum([len(r) for r in rows], out=offs[1:])
+        t = time.perf_counter()
+        dcol = self.eng.column(nsq, k)
+        dcol.append_dec((chars, offs))
+        dec = str(dcol.fold())
+        dt = time.perf_counter() - t
+        dcol.close()
+        out["decimal"] = {"rows": k, "seconds": dt, "rows_per_s": k / dt, "chars": len(chars),
+                          "matches_resident_fold": dec == str(self.col.fold(0, k)),
+                          "path": "dds_col_append_dec (k_dec_parse on the GPU) + dds_col_fold, decimal result"}
+        # CPU side of the same decimal boundary: what the reference route does per row before the
+        # modmul (BigInteger(String) parse, :417,419), restated as Python int() on the sample
+        t = time.perf_counter()
+        _ = [int(r) for r in rows[: min(k, 20000)]]
+        out["decimal"]["cpu_parse_rows_per_s_1core"] = min(k, 20000) / (time.perf_counter() - t)
         return out
 
     def close(self):

@@ -10,11 +10,14 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "bn_host.hpp"
@@ -374,16 +377,111 @@ int emit_be(const bn::Limbs& v, size_t width, uint8_t* out, size_t out_cap, size
 }
 
 // Upload `count` big-endian operands into an rW column (X, stride) validated against mc.
+// Parallel host memcpy (pageable caller buffer -> pinned staging). One thread copies ~10-15 GB/s,
+// below what PCIe moves; the pool's threads each copy one contiguous piece of a chunk.
+class CopyPool {
+ public:
+  static CopyPool& get() {
+    static CopyPool pool;
+    return pool;
+  }
+  void copy(void* dst, const void* src, size_t n) {
+    if (th_.empty() || n < ((size_t)4 << 20)) {
+      memcpy(dst, src, n);
+      return;
+    }
+    std::lock_guard<std::mutex> job(job_mu_);
+    const size_t T = th_.size() + 1;
+    size_t piece = (n + T - 1) / T;
+    piece = (piece + 4095) & ~(size_t)4095;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      dst_ = (char*)dst;
+      src_ = (const char*)src;
+      n_ = n;
+      piece_ = piece;
+      pending_ = (int)th_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    memcpy(dst, src, std::min(piece, n));  // piece 0 on the calling thread
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+
+ private:
+  CopyPool() {
+    int n = 8;
+    if (const char* e = getenv("DDSHE_COPY_THREADS")) n = atoi(e);
+    n = std::max(1, std::min(n, 64));
+    for (int i = 1; i < n; ++i) th_.emplace_back([this, i] { run(i); });
+  }
+  void run(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      char* d = dst_;
+      const char* s = src_;
+      const size_t n = n_, a = (size_t)id * piece_;
+      const size_t len = a < n ? std::min(piece_, n - a) : 0;
+      lk.unlock();
+      if (len) memcpy(d + a, s + a, len);
+      lk.lock();
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_, job_mu_;
+  std::condition_variable cv_, done_;
+  char* dst_ = nullptr;
+  const char* src_ = nullptr;
+  size_t n_ = 0, piece_ = 0;
+  uint64_t gen_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
+};
+
+constexpr size_t kIngestChunkBytes = (size_t)64 << 20;  // binary rows per pinned chunk
+
 int ingest(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint8_t* ops, size_t width, size_t count,
            DevBuf& raw, uint32_t* X, size_t stride) {
   (void)ctx;
   if (count == 0) return DDS_OK;
-  HIP_TRY(raw.ensure(count * width));
   HIP_TRY(w->flags.ensure(16));
-  HIP_TRY(hipMemcpyAsync(raw.p, ops, count * width, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, st));
-  HIP_TRY(launch_ingest_be(raw.as<uint8_t>(), width, count, mc.S, mc.W, mc.d + (size_t)kConstN2x * mc.S, X, stride,
-                           w->flags.as<uint32_t>(), st));
+  const uint32_t* n2x = mc.d + (size_t)kConstN2x * mc.S;
+  const size_t crows = std::max<size_t>(1, kIngestChunkBytes / width);
+  if (count <= crows) {
+    HIP_TRY(raw.ensure(count * width));
+    HIP_TRY(hipMemcpyAsync(raw.p, ops, count * width, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_ingest_be(raw.as<uint8_t>(), width, count, mc.S, mc.W, n2x, X, stride, w->flags.as<uint32_t>(), st));
+  } else {
+    // chunked: the pool fills pinned slot s while the DMA + k_ingest_be of slot s^1 run
+    bool used[2] = {false, false};
+    HIP_TRY(raw.ensure(2 * crows * width));
+    for (size_t b = 0, slot = 0; b < count; b += crows, slot ^= 1) {
+      const size_t nrows = std::min(crows, count - b), bytes = nrows * width;
+      if (used[slot]) HIP_TRY(hipEventSynchronize(w->ev_dec[slot]));
+      HIP_TRY(w->hch[slot].ensure(crows * width));
+      CopyPool::get().copy(w->hch[slot].p, ops + b * width, bytes);
+      uint8_t* d = raw.as<uint8_t>() + slot * crows * width;
+      HIP_TRY(hipMemcpyAsync(d, w->hch[slot].p, bytes, hipMemcpyHostToDevice, st));
+      HIP_TRY(hipEventRecord(w->ev_dec[slot], st));
+      HIP_TRY(launch_ingest_be(d, width, nrows, mc.S, mc.W, n2x, X + b, stride, w->flags.as<uint32_t>(), st));
+      used[slot] = true;
+    }
+  }
   uint32_t flags = 0;
   HIP_TRY(hipMemcpyAsync(&flags, w->flags.p, 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));

@@ -73,7 +73,7 @@ _sig("dds_ctx_get_timing", C.c_int, C.c_void_p, C.POINTER(C.c_double), C.POINTER
 _sig("dds_ctx_reset_timing", C.c_int, C.c_void_p)
 _sig("dds_ctx_get_fold_work", C.c_int, C.c_void_p, C.POINTER(C.c_uint64))
 for _n in ("dds_modmul_fold", "dds_paillier_sum", "dds_rsa_product"):
-    _sig(_n, C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, _sz, _u8p, _sz, _szp)
+    _sig(_n, C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_void_p, _sz, _sz, _u8p, _sz, _szp)
 _sig("dds_modmul_pairs", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, C.c_char_p, _sz, _sz, _u8p)
 _sig("dds_bigint_sum", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz, _u8p, _sz, _szp)
 _sig("dds_bigint_product", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz, _u8p, _sz, _szp)
@@ -189,6 +189,18 @@ class Engine:
         out = (C.c_uint8 * max(width, mb))()
         olen = C.c_size_t()
         _check(fn(self._h, int_to_be(modulus, mb), mb, buf, width, len(ops), out, len(out), C.byref(olen)), fn.__name__)
+        return int.from_bytes(bytes(out[: olen.value]), "big")
+
+    def fold_buffer(self, modulus: int, buf: np.ndarray) -> int:
+        """dds_modmul_fold over a host buffer of fixed-width big-endian rows (uint8 [count, width]):
+        the binary boundary a JNA shim hands over, without per-row Python conversion."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        count, width = buf.shape
+        mb = nbytes(modulus)
+        out = (C.c_uint8 * max(width, mb))()
+        olen = C.c_size_t()
+        _check(_lib.dds_modmul_fold(self._h, int_to_be(modulus, mb), mb, buf.ctypes.data, width, count, out, len(out),
+                                    C.byref(olen)), "dds_modmul_fold")
         return int.from_bytes(bytes(out[: olen.value]), "big")
 
     def modmul_fold(self, modulus: int, ops, width=None) -> int:
@@ -390,6 +402,12 @@ class Column:
         _check(_lib.dds_col_read(self._h, first, count, out), "dds_col_read")
         raw = bytes(out)
         return [int.from_bytes(raw[i * self.mb:(i + 1) * self.mb], "big") for i in range(count)]
+
+    def read_buffer(self, first: int, count: int) -> np.ndarray:
+        """Rows [first, first+count) as canonical big-endian bytes, uint8 [count, modulus bytes]."""
+        out = np.empty((max(1, count), self.mb), dtype=np.uint8)
+        _check(_lib.dds_col_read(self._h, first, count, out.ctypes.data_as(_u8p)), "dds_col_read")
+        return out[:count]
 
     def fold(self, first: int = 0, count: int | None = None) -> int:
         count = len(self) - first if count is None else count

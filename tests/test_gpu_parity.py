@@ -265,3 +265,25 @@ def test_ope_filter_long_lookback(eng):
     sparse = (col % 1000 == 0).astype(np.int64)
     got = eng.ope_filter(sparse, valid, 0, "gt")
     assert np.array_equal(got, np.nonzero(sparse)[0].astype(np.uint32))
+
+
+def test_fold_host_buffer_chunked(eng, keys):
+    """dds_paillier_sum on a host buffer larger than one pinned ingest chunk (64 MiB): rows cross
+    chunk boundaries, and an operand in [N, 2N) in a later chunk still folds as its residue."""
+    import ddshe
+    key = keys["paillier2048_committed"]
+    N = key["nsquare"]
+    k = 300_001  # 512-byte rows: 3 chunks of 131072 rows
+    col = eng.column(N, k)
+    col.fill_paillier_synth(key["n"], key["g"], 7, 0, k)
+    buf = col.read_buffer(0, k)
+    assert buf.shape == (k, 512)
+    want = col.fold()
+    assert eng.fold_buffer(N, buf) == want
+    r = 250_000
+    x = int.from_bytes(bytes(buf[r]), "big")
+    buf[r] = np.frombuffer((x + N).to_bytes(512, "big"), dtype=np.uint8)
+    assert eng.fold_buffer(N, buf) == want
+    ms = ddshe.synth_plaintexts(7, 0, k)
+    assert homo.paillier_decrypt(want, key) == int(ms.astype("int64").sum()) % key["n"]
+    col.close()
