@@ -84,7 +84,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="sum: skip the host-boundary (PCIe/decimal) rates")
-    ap.add_argument("--e2e-dec-rows", type=int, default=100_000, help="sum: decimal-route sample rows")
+    ap.add_argument("--e2e-dec-rows", type=int, default=1_000_000, help="sum: decimal-route sample rows")
     ap.add_argument("--verify", type=int, default=1, help="check the result on rank 0")
     args = ap.parse_args()
     dflt = {"sum": (10_000_000, 20, 3, 2), "product_filter": (10_000_000, 10, 2, 3),
@@ -272,19 +272,26 @@ class SumWorkload(_Workload):
                          "host_GBps": buf.nbytes / dt / 1e9, "matches": got == res,
                          "path": "dds_paillier_sum (pageable host buffer -> H2D -> k_ingest_be -> fold)"}
         del buf
-        k = min(self.mine, self.args.e2e_dec_rows)
-        rows = [str(x) for x in self.col.read(0, k)]
-        chars = "".join(rows).encode()  # Arrow-style (chars, offsets): how a JNA shim passes String[]
+        # u distinct decimal rows (Python str() costs ~30 us per 4096-bit row), tiled `rep` times
+        u = min(self.mine, 100_000, self.args.e2e_dec_rows)
+        rep = max(1, self.args.e2e_dec_rows // u)
+        k = u * rep
+        rows = [str(x) for x in self.col.read(0, u)]
+        chars = "".join(rows).encode() * rep  # Arrow-style (chars, offsets): how a JNA shim passes String[]
+        lens = np.tile(np.array([len(r) for r in rows], dtype=np.uint64), rep)
         offs = np.zeros(k + 1, dtype=np.uint64)
-        np.cumsum([len(r) for r in rows], out=offs[1:])
-        t = time.perf_counter()
-        dcol = self.eng.column(nsq, k)
-        dcol.append_dec((chars, offs))
-        dec = str(dcol.fold())
-        dt = time.perf_counter() - t
-        dcol.close()
-        out["decimal"] = {"rows": k, "seconds": dt, "rows_per_s": k / dt, "chars": len(chars),
-                          "matches_resident_fold": dec == str(self.col.fold(0, k)),
+        np.cumsum(lens, out=offs[1:])
+        for _ in range(2):
+            t = time.perf_counter()
+            dcol = self.eng.column(nsq, k)
+            dcol.append_dec((chars, offs))
+            dec = dcol.fold()
+            dec_s = str(dec)
+            dt = time.perf_counter() - t
+            dcol.close()
+        out["decimal"] = {"rows": k, "distinct_rows": u, "seconds": dt, "rows_per_s": k / dt, "chars": len(chars),
+                          "host_GBps": len(chars) / dt / 1e9,
+                          "matches_resident_fold": dec == pow(self.col.fold(0, u), rep, nsq),
                           "path": "dds_col_append_dec (k_dec_parse on the GPU) + dds_col_fold, decimal result"}
         # CPU side of the same decimal boundary: what the reference route does per row before the
         # modmul (BigInteger(String) parse, :417,419), restated as Python int() on the sample

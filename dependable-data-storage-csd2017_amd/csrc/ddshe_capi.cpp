@@ -565,6 +565,21 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
     uint64_t* o = (uint64_t*)w->hoff[slot].p;
     size_t pos = 0, e = b;
     o[0] = 0;
+    if (!src.strs) {  // Arrow-style rows: one bulk copy of the chunk's chars, offsets rebased
+      const uint64_t base = src.offs[b];
+      size_t lo = b, hi = std::min(count, b + kDecChunkRows);  // largest e in [b, hi] with chars <= chunk
+      while (lo < hi) {
+        const size_t mid = lo + (hi - lo + 1) / 2;
+        if (src.offs[mid] - base <= kDecChunkBytes - 64) lo = mid;
+        else hi = mid - 1;
+      }
+      if (lo > b) {
+        e = lo;
+        pos = (size_t)(src.offs[e] - base);
+        CopyPool::get().copy(dst, src.chars + base, pos);
+        for (size_t i = b; i <= e; ++i) o[i - b] = src.offs[i] - base;
+      }
+    }
     while (e < count && e - b < kDecChunkRows) {
       size_t n = src.len(e);
       const bool longrow = n > kDecChunkBytes - 64;
