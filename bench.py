@@ -304,6 +304,22 @@ class SumWorkload(_Workload):
         self.col.close()
 
 
+def pmc_traffic(workload, kernels, per_step=False):
+    """HBM bytes per call from the committed rocprofv3 PMC passes (10M rows): the sum over `kernels`
+    of bytes per dispatch (times dispatches per call when per_step: the PMC run did one call)."""
+    tf = os.path.join(ROOT, "profiles", "r01_pmc_filter_order.json")
+    if not os.path.exists(tf):
+        return None
+    ks = json.load(open(tf))["kernels"]
+    tot = 0.0
+    for k in kernels:
+        d = ks.get(f"{workload}:{k}")
+        if d is None:
+            return None
+        tot += d["hbm_bytes_per_dispatch"] * (d["dispatches"] if per_step else 1)
+    return tot
+
+
 def load_keyset(name):
     raw = json.load(open(os.path.join(ROOT, "tests", "golden", "keys.json")))
     return {k: (int(v, 16) if k != "x509_hex" else v) for k, v in raw[name].items()}
@@ -379,7 +395,8 @@ class ProductFilterWorkload(_Workload):
                 "frac": filt_bytes / filt_s / 1e9 / 8000.0, "avg_filter_ms": filt_s * 1e3,
                 "kernel": "k_ope_count + k_ope_scatter (device time, HIP events on the launch stream)",
                 "avg_filter_call_ms": self.filter_ms / (4 * a.steps),
-                "algorithmic_bytes": filt_bytes, "traffic": None}
+                "algorithmic_bytes": filt_bytes, "traffic": pmc_traffic("product_filter", ("k_ope_count<true>", "k_ope_scatter")),
+                "traffic_unit": "HBM bytes per filter call (PMC, profiles/r01_pmc_filter_order.json)"}
         cpu = None
         if self.world == 1 and not a.no_cpu_baseline:
             n = key["n"]
@@ -524,7 +541,9 @@ class OrderWorkload(_Workload):
         roof = {"bound": "hbm", "kernel": "k_rs_hist/k_rs_scan/k_rs_scatter (8 LSD passes)",
                 "achieved": alg / step_s / 1e9, "peak": 8000.0, "unit": "GB/s", "frac": alg / step_s / 1e9 / 8000.0,
                 "algorithmic_bytes": alg, "issued_bytes_est": self.mine * (8 * 36 + 8 + 1),
-                "traffic": None}
+                "traffic": pmc_traffic("order", ("k_rs_prep", "k_rs_red", "k_rs_hist", "k_rs_scan_digits", "k_rs_scatter"),
+                                       per_step=True),
+                "traffic_unit": "HBM bytes per OrderLS call (PMC, profiles/r01_pmc_filter_order.json)"}
         cpu = None
         if self.world == 1 and not a.no_cpu_baseline:
             t = time.perf_counter()
