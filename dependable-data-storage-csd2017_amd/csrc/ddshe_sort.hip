@@ -8,10 +8,13 @@
 //
 // Per 8-bit digit pass (8 passes; the last one has 257 buckets: the validity of the row moves it
 // to the end / front): k_rs_hist (per-tile digit counts, digit-major) -> k_rs_scan_digits (per-digit
-// scan over tiles, one block per digit; the scatter blocks scan the 257 digit totals themselves) -> k_rs_scatter (stable rank inside the tile: each wave walks a contiguous
-// quarter of the tile, peers with equal digits are found with 9 ballots, per-wave digit counters
-// in LDS). HBM traffic per pass: 12 B/row read twice (hist + scatter) + 12 B/row written; the
-// validity of a row rides in bit 31 of its id (no random gather of valid[] in the last pass).
+// scan over tiles, one block per digit, coalesced 1024-count chunks; the scatter blocks scan the 257
+// digit totals themselves) -> k_rs_scatter (stable rank inside the tile: each wave walks a contiguous
+// quarter of the tile, peers with equal digits are found with 9 ballots, per-wave digit counters in
+// LDS; the ranked rows are staged in LDS in tile-local digit order and written out by consecutive
+// threads, so a store instruction covers a few digit runs instead of 64 buckets). HBM traffic per
+// pass: 8 B/row read by hist, 12 B/row read + 12 B/row written by scatter; the validity of a row
+// rides in bit 31 of its id (no random gather of valid[] in the last pass).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -21,7 +24,7 @@ namespace ddshe {
 
 constexpr int kRsBlock = 256;
 constexpr int kRsWaves = kRsBlock / 64;
-constexpr int kRsItems = 16;                      // rows per lane
+constexpr int kRsItems = 8;                       // rows per lane
 constexpr size_t kRsTile = (size_t)kRsBlock * kRsItems;
 constexpr int kRsDigits = 257;                    // 256 + the validity bucket of the last pass
 constexpr uint32_t kRsNone = 511;                 // digit of a lane past the end (never counted)
@@ -165,32 +168,54 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_hist(const uint64_t* __restrict
 }
 
 // per digit d (one block each): exclusive scan of the tile counts hist[d][0..nblocks) in place,
-// digit total -> dtot[d]
+// digit total -> dtot[d]. Chunks of 1024 counts: thread t owns counts 4t..4t+3 of a chunk (a wave's
+// loads cover 1 KiB contiguous); up to kScanRegChunks chunks are loaded before any is scanned.
+constexpr int kScanRegChunks = 8;
 __global__ void __launch_bounds__(256) k_rs_scan_digits(uint32_t* __restrict__ hist, size_t nblocks,
                                                         uint32_t* __restrict__ dtot) {
-  __shared__ uint32_t part[256];
+  __shared__ uint32_t wtot[4];
   uint32_t* h = hist + (size_t)blockIdx.x * nblocks;
-  const size_t per = (nblocks + 255) / 256;
-  const size_t b0 = threadIdx.x * per, b1 = min(nblocks, b0 + per);
-  uint32_t s = 0;
-  for (size_t b = b0; b < b1; ++b) s += h[b];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    const uint32_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  uint32_t carry = 0;
+  for (size_t c0 = 0; c0 < nblocks; c0 += (size_t)1024 * kScanRegChunks) {
+    uint32_t v[kScanRegChunks][4];
+#pragma unroll
+    for (int c = 0; c < kScanRegChunks; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t b = c0 + (size_t)c * 1024 + 4 * tid + j;
+        v[c][j] = b < nblocks ? h[b] : 0u;
+      }
+#pragma unroll
+    for (int c = 0; c < kScanRegChunks; ++c) {
+      if (c0 + (size_t)c * 1024 >= nblocks) break;  // block-uniform
+      const uint32_t s = v[c][0] + v[c][1] + v[c][2] + v[c][3];
+      uint32_t inc = s;
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, off);
+        if (lane >= off) inc += y;
+      }
+      if (lane == 63) wtot[wid] = inc;
+      __syncthreads();
+      uint32_t run = carry + inc - s;
+      for (int w = 0; w < wid; ++w) run += wtot[w];
+      const uint32_t ctot = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t b = c0 + (size_t)c * 1024 + 4 * tid + j;
+        if (b < nblocks) h[b] = run;
+        run += v[c][j];
+      }
+      carry += ctot;
+    }
   }
-  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
-  for (size_t b = b0; b < b1; ++b) {
-    const uint32_t c = h[b];
-    h[b] = run;
-    run += c;
-  }
-  if (threadIdx.x == 255) dtot[blockIdx.x] = part[255];
+  if (tid == 0) dtot[blockIdx.x] = carry;
 }
 
+// The ranked rows are first placed in tile-local digit order in LDS, then written out by
+// consecutive threads: lanes of a store instruction hit consecutive addresses of a digit run
+// (runs average kRsTile/256 = 16 rows), instead of 64 different buckets per store.
 __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ ids,
                                                          const uint8_t* __restrict__ valid, size_t n, int pass,
@@ -200,16 +225,21 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
                                                          uint64_t* __restrict__ keys_out,
                                                          uint32_t* __restrict__ ids_out) {
   __shared__ uint32_t cnt[kRsWaves][kRsDigits];
-  __shared__ uint32_t dbase[kRsDigits + 1];
+  __shared__ uint32_t dbase[kRsDigits + 1];   // global start of digit d, then of this tile's run of d
+  __shared__ uint32_t lstart[kRsDigits + 1];  // tile-local start of digit d
+  __shared__ uint64_t skey[kRsTile];
+  __shared__ uint32_t sid[kRsTile];
+  __shared__ uint16_t sdig[kRsTile];
   for (int d = threadIdx.x; d < kRsWaves * kRsDigits; d += kRsBlock) (&cnt[0][0])[d] = 0;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t lt = (1ull << lane) - 1ull;
-  if (wid == 0) {  // digit bases: exclusive scan of the kRsDigits totals (5 per lane, then a wave scan)
+  // exclusive scan of kRsDigits values v(d) into out[] by one wave (5 digits per lane)
+  auto wave_scan = [&](auto v_of, uint32_t* out) {
     uint32_t v[5], s = 0;
 #pragma unroll
     for (int q = 0; q < 5; ++q) {
       const int d = lane * 5 + q;
-      v[q] = d < kRsDigits ? dtot[d] : 0u;
+      v[q] = d < kRsDigits ? v_of(d) : 0u;
       s += v[q];
     }
     uint32_t inc = s;
@@ -221,10 +251,11 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
 #pragma unroll
     for (int q = 0; q < 5; ++q) {
       const int d = lane * 5 + q;
-      if (d <= kRsDigits) dbase[d] = run;
+      if (d <= kRsDigits) out[d] = run;
       run += v[q];
     }
-  }
+  };
+  if (wid == 0) wave_scan([&](int d) { return dtot[d]; }, dbase);  // digit bases over all tiles
   __syncthreads();
   uint64_t key[kRsItems];
   uint32_t id[kRsItems], dr[kRsItems];  // dr = digit | rank << 9
@@ -258,23 +289,36 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
     dr[k] = d | (rank << 9);
   }
   __syncthreads();
-  // base[w][d] = global bucket offset of this tile + counts of earlier waves
+  if (wid == 0) wave_scan([&](int d) { return cnt[0][d] + cnt[1][d] + cnt[2][d] + cnt[3][d]; }, lstart);
+  __syncthreads();
+  // cnt[w][d] <- tile-local start of wave w's rows of digit d; dbase[d] <- global start of the tile's run
   for (int d = threadIdx.x; d < kRsDigits; d += kRsBlock) {
-    uint32_t run = dbase[d] + hist[(size_t)d * nblocks + blockIdx.x];
+    uint32_t run = lstart[d];
     for (int w = 0; w < kRsWaves; ++w) {
       const uint32_t c = cnt[w][d];
       cnt[w][d] = run;
       run += c;
     }
+    dbase[d] += hist[(size_t)d * nblocks + blockIdx.x];
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
     const uint32_t d = dr[k] & 511u;
     if (d == kRsNone) continue;
-    const uint32_t dst = cnt[wid][d] + (dr[k] >> 9);
-    if (keys_out) keys_out[dst] = key[k];
-    ids_out[dst] = (last && vbit) ? (id[k] & ~kRsLack) : id[k];
+    const uint32_t lp = cnt[wid][d] + (dr[k] >> 9);
+    if (keys_out) skey[lp] = key[k];
+    sid[lp] = (last && vbit) ? (id[k] & ~kRsLack) : id[k];
+    sdig[lp] = (uint16_t)d;
+  }
+  __syncthreads();
+  const size_t t0 = (size_t)blockIdx.x * kRsTile;
+  const uint32_t rows = (uint32_t)min(kRsTile, n - t0);
+  for (uint32_t q = threadIdx.x; q < rows; q += kRsBlock) {
+    const uint32_t d = sdig[q];
+    const uint32_t dst = dbase[d] + (q - lstart[d]);
+    if (keys_out) keys_out[dst] = skey[q];
+    ids_out[dst] = sid[q];
   }
 }
 
