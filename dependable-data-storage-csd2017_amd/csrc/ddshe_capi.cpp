@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -386,7 +387,8 @@ class CopyPool {
     return pool;
   }
   void copy(void* dst, const void* src, size_t n) {
-    if (th_.empty() || n < ((size_t)4 << 20)) {
+    // a forked child inherits the pool object but not its threads: copy on the calling thread
+    if (th_.empty() || n < ((size_t)4 << 20) || getpid() != owner_) {
       memcpy(dst, src, n);
       return;
     }
@@ -418,7 +420,7 @@ class CopyPool {
   }
 
  private:
-  CopyPool() {
+  CopyPool() : owner_(getpid()) {
     int n = 8;
     if (const char* e = getenv("DDSHE_COPY_THREADS")) n = atoi(e);
     n = std::max(1, std::min(n, 64));
@@ -441,6 +443,7 @@ class CopyPool {
       if (--pending_ == 0) done_.notify_one();
     }
   }
+  pid_t owner_;
   std::vector<std::thread> th_;
   std::mutex mu_, job_mu_;
   std::condition_variable cv_, done_;
