@@ -243,6 +243,83 @@ struct Mont {
     settle(t, a, bottom);
   }
 
+  // Row-chained form of mul_col for the fold's row loop: the first two limb blocks of `row` arrive
+  // in `pre` (requested during the previous row), and the first two blocks of `next` are requested
+  // during this row's last two blocks and returned in `pre`, so no row starts on an HBM miss.
+  static constexpr int kPF = (S % 4 == 0) ? 4 : 2;
+  __device__ __forceinline__ static void load_blocks2(uint32_t (&pre)[2][kPF], const uint32_t* __restrict__ X,
+                                                      size_t stride, uint32_t row) {
+    const uint32_t voff = row * 4u, sstride = (uint32_t)stride * 4u;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (size_t)d * kPF * stride), (short)0,
+                                                        (int)(kPF * sstride), 0x00020000);
+#pragma unroll
+      for (int q = 0; q < kPF; ++q) pre[d][q] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, q * sstride, 0);
+    }
+  }
+  __device__ __forceinline__ static void mul_col_chain(uint32_t (&a)[L], const uint32_t (&n)[L],
+                                                       const uint32_t* __restrict__ X, size_t stride, uint32_t row,
+                                                       uint32_t next, uint32_t (&pre)[2][kPF], uint32_t n0,
+                                                       bool top, bool bottom) {
+    constexpr int PF = kPF;
+    static_assert(S % PF == 0 && S >= 2 * PF, "S % PF");
+    uint64_t t[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) t[l] = 0;
+    const uint32_t voff = row * 4u;
+    const uint32_t sstride = (uint32_t)stride * 4u;
+    auto block_rsrc = [&](int i) {
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(X + (size_t)i * stride), (short)0, (int)(PF * sstride),
+                                               0x00020000);
+    };
+    uint32_t bq[PF], bm[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      bq[q] = pre[0][q];
+      bm[q] = pre[1][q];
+    }
+#pragma unroll 1
+    for (int i = 0; i < S - 2 * PF; i += PF) {
+      const auto rs = block_rsrc(i + 2 * PF);
+      uint32_t bn[PF];
+#pragma unroll
+      for (int q = 0; q < PF; ++q) bn[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, q * sstride, 0);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        step(t, a, n, bq[q], n0, top);
+        fence_t(t);
+      }
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        bq[q] = bm[q];
+        bm[q] = bn[q];
+      }
+    }
+    const uint32_t nvoff = next * 4u;
+    {
+      const auto rs = block_rsrc(0);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) pre[0][q] = __builtin_amdgcn_raw_buffer_load_b32(rs, nvoff, q * sstride, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      step(t, a, n, bq[q], n0, top);
+      fence_t(t);
+    }
+    {
+      const auto rs = block_rsrc(PF);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) pre[1][q] = __builtin_amdgcn_raw_buffer_load_b32(rs, nvoff, q * sstride, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      step(t, a, n, bm[q], n0, top);
+      fence_t(t);
+    }
+    settle(t, a, bottom);
+  }
+
   // a <- MonPro(a, B), B in LDS (limb i at lb[i], fully normalised, value < 2N). The TPI
   // lanes of a group read the same address (broadcast); group arrays sit S dwords apart.
   __device__ __forceinline__ static void mul_lds(uint32_t (&a)[L], const uint32_t (&n)[L], const uint32_t* lb,

@@ -97,8 +97,14 @@ __global__ void __launch_bounds__(256, 2) k_fold(const uint32_t* __restrict__ X,
   uint32_t n[L], a[L];
   g.load_vec(n, consts + kConstN * S);
   g.load_col(a, X, xstride, grp);
-  for (size_t row = grp + ngroups; row < count; row += ngroups)
-    M::template mul_col<false>(a, n, X, xstride, (uint32_t)row, n0, g.top, g.bottom);
+  if (grp + ngroups < count) {
+    uint32_t pre[2][M::kPF];  // first limb blocks of the next row, requested one row ahead
+    M::load_blocks2(pre, X, xstride, (uint32_t)(grp + ngroups));
+    for (size_t row = grp + ngroups; row < count; row += ngroups) {
+      const size_t nxt = row + ngroups < count ? row + ngroups : row;  // last row: a harmless re-read
+      M::mul_col_chain(a, n, X, xstride, (uint32_t)row, (uint32_t)nxt, pre, n0, g.top, g.bottom);
+    }
+  }
   M::normalize(a, g.bottom);
   g.store_col(a, P, pstride, grp);
 }
