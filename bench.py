@@ -241,6 +241,12 @@ class SumWorkload(_Workload):
             pm = json.load(open(tf))
             traffic = pm["hbm_bytes_per_launch"] / pm["rows_per_launch"] * self.mine  # each row read once
         roof.update(traffic=traffic, traffic_unit="bytes/launch (PMC, profiles/r01_pmc_traffic.json)")
+        vf = os.path.join(ROOT, "profiles", "r01_pmc_valu_fold.json")
+        if os.path.exists(vf):  # rocprofv3 VALU counters of the same kernel (north star: VALU-roofline fraction)
+            dv = json.load(open(vf))["derived"]
+            roof["valu_pmc"] = {"mad_issue_frac_at_measured_clock": dv["mad_issue_frac_of_half_rate_peak_at_measured_clock"],
+                                "int64_share_of_valu": dv["valu_int64_share_of_valu"], "clock_GHz": dv["clock_GHz_est"],
+                                "source": "profiles/r01_pmc_valu_fold.json"}
         cpu = None
         if self.world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(self.col, nsq, (nsq.bit_length() + 7) // 8, a.cpu_seconds)
