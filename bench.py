@@ -16,6 +16,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
 import sys
 import time
 
@@ -680,13 +681,13 @@ def cpu_baseline(col, nsq, mb, seconds):
     Also: the same prefix sliced over cpu_threads() threads, and the schoolbook C restatement."""
     from oracle import cref
     calib = min(len(col), 4000)
-    ops = b"".join(x.to_bytes(mb, "big") for x in col.read(0, calib))
+    ops = col.read_buffer(0, calib).tobytes()  # canonical big-endian rows, mb bytes each
     mod_be = nsq.to_bytes(mb, "big")
     t = time.perf_counter()
     cref.bn_fold_be(mod_be, ops, mb, calib)
     rate = (calib - 1) / (time.perf_counter() - t)
     sample = int(min(len(col), max(calib, rate * seconds)))
-    ops = b"".join(x.to_bytes(mb, "big") for x in col.read(0, sample))
+    ops = col.read_buffer(0, sample).tobytes()
     t = time.perf_counter()
     ref = cref.bn_fold_be(mod_be, ops, mb, sample)
     dt = time.perf_counter() - t
@@ -706,7 +707,9 @@ def cpu_baseline(col, nsq, mb, seconds):
                              "sample": "same prefix in contiguous slices, partials combined"},
             "schoolbook_port": {"value": (small - 1) / dt_sb, "cores": 1,
                                 "sample": f"first {small} rows, oracle/csrc/fold_ref.c (schoolbook + Knuth D)",
-                                "matches": int.from_bytes(ref_sb, "big") == col.fold(0, small)}}
+                                "matches": int.from_bytes(ref_sb, "big") == col.fold(0, small)},
+            # a JVM BigInteger harness when `java` exists on the box (it does not in this image)
+            "jvm": shutil.which("java")}
 
 
 if __name__ == "__main__":
