@@ -13,6 +13,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -378,37 +379,46 @@ int emit_be(const bn::Limbs& v, size_t width, uint8_t* out, size_t out_cap, size
 }
 
 // Upload `count` big-endian operands into an rW column (X, stride) validated against mc.
-// Parallel host memcpy (pageable caller buffer -> pinned staging). One thread copies ~10-15 GB/s,
-// below what PCIe moves; the pool's threads each copy one contiguous piece of a chunk.
+// Host worker pool for the boundary codecs: parallel copies of caller buffers into pinned staging
+// (one thread copies ~10-15 GB/s, below what PCIe moves). parallel_for(n, f) splits [0, n) into
+// one contiguous slice per thread, aligned to `align`, and calls f(begin, end) on each.
 class CopyPool {
  public:
   static CopyPool& get() {
     static CopyPool pool;
     return pool;
   }
-  void copy(void* dst, const void* src, size_t n) {
-    // a forked child inherits the pool object but not its threads: copy on the calling thread
-    if (th_.empty() || n < ((size_t)4 << 20) || getpid() != owner_) {
-      memcpy(dst, src, n);
+  template <class F>
+  void parallel_for(size_t n, size_t align, F&& f) {
+    // a forked child inherits the pool object but not its threads: run on the calling thread
+    if (th_.empty() || getpid() != owner_) {
+      f((size_t)0, n);
       return;
     }
     std::lock_guard<std::mutex> job(job_mu_);
     const size_t T = th_.size() + 1;
     size_t piece = (n + T - 1) / T;
-    piece = (piece + 4095) & ~(size_t)4095;
+    piece = (piece + align - 1) / align * align;
+    std::function<void(size_t, size_t)> fn = f;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      dst_ = (char*)dst;
-      src_ = (const char*)src;
+      fn_ = &fn;
       n_ = n;
       piece_ = piece;
       pending_ = (int)th_.size();
       ++gen_;
     }
     cv_.notify_all();
-    memcpy(dst, src, std::min(piece, n));  // piece 0 on the calling thread
+    f((size_t)0, std::min(piece, n));  // slice 0 on the calling thread
     std::unique_lock<std::mutex> lk(mu_);
     done_.wait(lk, [&] { return pending_ == 0; });
+  }
+  void copy(void* dst, const void* src, size_t n) {
+    if (n < ((size_t)4 << 20)) {
+      memcpy(dst, src, n);
+      return;
+    }
+    parallel_for(n, 4096, [&](size_t a, size_t e) { memcpy((char*)dst + a, (const char*)src + a, e - a); });
   }
   ~CopyPool() {
     {
@@ -433,12 +443,11 @@ class CopyPool {
       cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
       if (stop_) return;
       seen = gen_;
-      char* d = dst_;
-      const char* s = src_;
+      const std::function<void(size_t, size_t)>* fn = fn_;
       const size_t n = n_, a = (size_t)id * piece_;
-      const size_t len = a < n ? std::min(piece_, n - a) : 0;
+      const size_t e = a < n ? std::min(n, a + piece_) : a;
       lk.unlock();
-      if (len) memcpy(d + a, s + a, len);
+      if (e > a) (*fn)(a, e);
       lk.lock();
       if (--pending_ == 0) done_.notify_one();
     }
@@ -447,8 +456,7 @@ class CopyPool {
   std::vector<std::thread> th_;
   std::mutex mu_, job_mu_;
   std::condition_variable cv_, done_;
-  char* dst_ = nullptr;
-  const char* src_ = nullptr;
+  const std::function<void(size_t, size_t)>* fn_ = nullptr;
   size_t n_ = 0, piece_ = 0;
   uint64_t gen_ = 0;
   int pending_ = 0;
@@ -560,6 +568,7 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
   HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, st));
   bool used[2] = {false, false};
   int slot = 0;
+  std::vector<size_t> lens;
   for (size_t b = 0; b < count;) {
     if (used[slot]) HIP_TRY(hipEventSynchronize(w->ev_dec[slot]));
     HIP_TRY(w->hch[slot].ensure(kDecChunkBytes + 64));
@@ -582,6 +591,26 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
         CopyPool::get().copy(dst, src.chars + base, pos);
         for (size_t i = b; i <= e; ++i) o[i - b] = src.offs[i] - base;
       }
+    }
+    if (src.strs && count - b >= 4096) {
+      // NUL-terminated rows (JNA String[]): lengths and copies spread over the host pool; the
+      // chunk cut and the offsets are one sequential pass over the lengths
+      const size_t hi = std::min(count, b + kDecChunkRows);
+      lens.resize(hi - b);
+      CopyPool::get().parallel_for(hi - b, 1024, [&](size_t x, size_t y) {
+        for (size_t i = x; i < y; ++i) lens[i] = strlen(src.strs[b + i]);
+      });
+      while (e < hi) {
+        const size_t n = lens[e - b] > kDecChunkBytes - 64 ? 1 : lens[e - b];
+        if (pos + n > kDecChunkBytes) break;
+        if (n != lens[e - b]) long_rows->push_back(e);
+        pos += n;
+        o[++e - b] = pos;
+      }
+      CopyPool::get().parallel_for(e - b, 256, [&](size_t x, size_t y) {
+        for (size_t i = x; i < y; ++i)
+          memcpy(dst + o[i], o[i + 1] - o[i] == lens[i] ? src.strs[b + i] : "0", o[i + 1] - o[i]);
+      });
     }
     while (e < count && e - b < kDecChunkRows) {
       size_t n = src.len(e);

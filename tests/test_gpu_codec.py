@@ -141,3 +141,22 @@ def test_sum_all_dec_long_zero_padded_row(eng, keys):
     N = keys["paillier1024_seed1"]["nsquare"]
     rows = ["3", "0" * (65 << 20) + "5", "7"]
     assert eng.sum_all_dec(rows, str(N)) == str(3 * 5 * 7 % N)
+
+
+def test_sum_all_dec_string_rows_parallel_chunks(eng, keys):
+    """NUL-terminated rows (the JNA String[] of the route) over several 64 MiB staging chunks, with
+    BigInteger spellings ('+', leading zeros, negatives), a row >= N and one row longer than a chunk:
+    the host pool's lengths/copies and the chunk cut keep every row intact."""
+    k = keys["paillier1024_seed1"]
+    N = k["nsquare"]
+    rng = random.Random(21)
+    xs = [rng.randrange(N) for _ in range(120_000)]
+    xs[7] = N + 12345
+    xs[60_001] = -rng.randrange(N)
+    rows = [fmt(x, rng) for x in xs]
+    rows[90_000] = "0" * (65 << 20) + "9"  # longer than one chunk: parsed on the boundary path
+    xs[90_000] = 9
+    want = 1
+    for x in xs:
+        want = want * x % N
+    assert eng.sum_all_dec(rows, str(N)) == str(want)
