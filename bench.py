@@ -305,6 +305,21 @@ class SumWorkload(_Workload):
         t = time.perf_counter()
         _ = [int(r) for r in rows[: min(k, 20000)]]
         out["decimal"]["cpu_parse_rows_per_s_1core"] = min(k, 20000) / (time.perf_counter() - t)
+        # (3) the route entry point a JNA binding calls with the String[] it holds (dds_sum_all_dec:
+        # NUL-terminated rows -> GPU parse -> fold -> decimal text), same rows
+        import ctypes as C
+        enc = [r.encode() for r in rows]
+        arr = (C.c_char_p * k)(*(enc * rep))
+        cap = 4 * len(str(nsq)) + 64
+        res_buf = C.create_string_buffer(cap)
+        olen = C.c_size_t()
+        for _ in range(2):
+            t = time.perf_counter()
+            st = self.ddshe._lib.dds_sum_all_dec(self.eng._h, arr, k, str(nsq).encode(), res_buf, cap, C.byref(olen))
+            dt = time.perf_counter() - t
+        out["strings"] = {"rows": k, "seconds": dt, "rows_per_s": k / dt, "host_GBps": len(chars) / dt / 1e9,
+                          "matches": st == 0 and res_buf.value.decode() == str(dec),
+                          "path": "dds_sum_all_dec (String[] rows, the route-level JNA entry point)"}
         return out
 
     def close(self):
