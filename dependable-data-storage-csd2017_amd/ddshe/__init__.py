@@ -15,7 +15,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libddshe.so")
+LIB_PATH = os.environ.get("DDSHE_LIB") or os.path.join(_HERE, "libddshe.so")  # DDSHE_LIB: A/B builds
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"libddshe.so not built at {LIB_PATH}: run `make -C dependable-data-storage-csd2017_amd/csrc` "
