@@ -40,10 +40,19 @@ __device__ __forceinline__ uint32_t grp_bcast0(uint32_t x) {
   else if constexpr (TPI == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xA0, 0xF, 0xF, false);  // quad_perm [0,0,2,2]
   else if constexpr (TPI == 4) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x00, 0xF, 0xF, false);  // quad_perm [0,0,0,0]
   else if constexpr (TPI == 8) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x18);  // and_mask 0b11000
-  else { static_assert(TPI == 16, "TPI"); return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150, 0xF, 0xF, false); }  // row_newbcast:0
+  else if constexpr (TPI == 16) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150, 0xF, 0xF, false);  // row_newbcast:0
+  else {
+    static_assert(TPI == 32, "TPI");
+    // row_newbcast:0 gives every row its lane 0; row_bcast:15 then hands row 0's (row 2's) value,
+    // now in its lane 15, to row 1 (row 3) — rows 0 and 2 keep theirs (row_mask 0b1010)
+    const int r0 = __builtin_amdgcn_mov_dpp((int)x, 0x150, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(r0, r0, 0x142, 0xA, 0xF, false);
+  }
 }
 // value of lane r+1; the group's top lane receives the value of a group's lane 0 (TPI <= 4: its own
-// group's, quad_perm wraps; TPI 8: the next group's; TPI 16: 0 via bound_ctrl at the row end).
+// group's, quad_perm wraps; TPI 8: the next group's; TPI 16: 0 via bound_ctrl at the row end;
+// TPI 32: wave_shl:1 crosses rows, lane 31 reads lane 32 (forced to 0 by the select: the next
+// group may have exited), lane 63 gets 0 via bound_ctrl).
 // Montgomery steps pass lo0 through this, and lo0 == 0 on every group's lane 0, so the top lane
 // gets 0 without a select.
 template <int TPI>
@@ -51,6 +60,10 @@ __device__ __forceinline__ uint32_t grp_from_next(uint32_t x) {
   if constexpr (TPI == 1) return 0u;
   else if constexpr (TPI == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
   else if constexpr (TPI == 4) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x39, 0xF, 0xF, false);  // [1,2,3,0]
+  else if constexpr (TPI == 32) {
+    const uint32_t v = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x130, 0xF, 0xF, true);  // wave_shl:1
+    return (lane_id() & 31) == 31 ? 0u : v;
+  }
   else return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x101, 0xF, 0xF, true);                          // row_shl:1
 }
 // value of lane r-1 (caller masks the group's bottom lane)
@@ -59,6 +72,7 @@ __device__ __forceinline__ uint32_t grp_from_prev(uint32_t x) {
   if constexpr (TPI == 1) return 0u;
   else if constexpr (TPI == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xA0, 0xF, 0xF, false);  // [0,0,2,2]
   else if constexpr (TPI == 4) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x90, 0xF, 0xF, false);  // [0,0,1,2]
+  else if constexpr (TPI == 32) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x138, 0xF, 0xF, true);  // wave_shr:1
   else return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x111, 0xF, 0xF, true);                          // row_shr:1
 }
 

@@ -12,6 +12,7 @@
 //   HomoAdd.encrypt  utils/SJHomoLibProvider.scala:58 -> k_modexp_pre + k_modexp_ladder (also HomoMult.encrypt, :59)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "ddshe_device.hpp"
 #include "ddshe_fold.hpp"
@@ -704,9 +705,28 @@ hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, c
   return hipGetLastError();
 }
 
+// Latency-bound tree levels of the 4096-bit tail shape (S = 160, W = 28) run with 32 lanes per
+// bignum (L = 5 limbs per lane): a Montgomery step issues 10 mads per wave instead of 20, and
+// these levels have at most one wave per SIMD, so the step time is the issue time of one wave.
+// Levels with more groups stay at TPI = 16 (fewer exchange instructions per mad). Same limb
+// layout and constants for both, so levels mix freely. DDSHE_TAIL32=0 disables (A/B timing).
+constexpr size_t kTail32MaxGroups = 2048;
+static bool use_tail32(int S, size_t ngroups) {
+  static const bool on = [] {
+    const char* e = getenv("DDSHE_TAIL32");
+    return !(e && e[0] == '0');
+  }();
+  return on && S == 160 && ngroups <= kTail32MaxGroups;
+}
+
 hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
                             uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups, hipStream_t st) {
   if (ngroups == 0 || ngroups > count) return hipErrorInvalidValue;
+  if (use_tail32(S, ngroups)) {
+    hipLaunchKernelGGL((k_fold<160, 32, 28>), dim3(grid_for(ngroups * 32)), dim3(256), 0, st, X, xstride, count,
+                       consts, n0, P, pstride, ngroups);
+    return hipGetLastError();
+  }
   DDSHE_TAIL_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X,
                                           xstride, count, consts, n0, P, pstride, ngroups));
   return hipGetLastError();
@@ -714,6 +734,10 @@ hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t cou
 
 hipError_t launch_finalize_tail(int S, const uint32_t* P, size_t pstride, const uint32_t* consts, const uint32_t* Y,
                                 uint32_t n0, uint32_t* out, hipStream_t st) {
+  if (use_tail32(S, 1)) {
+    hipLaunchKernelGGL((k_finalize<160, 32, 28>), dim3(1), dim3(64), 0, st, P, pstride, consts, Y, n0, out);
+    return hipGetLastError();
+  }
   DDSHE_TAIL_SWITCH(S, hipLaunchKernelGGL((k_finalize<S, TPI, W>), dim3(1), dim3(64), 0, st, P, pstride, consts, Y, n0,
                                           out));
   return hipGetLastError();
