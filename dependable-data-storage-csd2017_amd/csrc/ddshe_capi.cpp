@@ -118,6 +118,7 @@ struct ModConsts {
   std::vector<uint32_t> host2;   // kConstCount * S2 (tail shape)
   uint32_t* d = nullptr;         // device copies
   uint32_t* d2 = nullptr;
+  uint32_t* dq = nullptr;        // N~ = N·n0 in tail limbs (tail_qp shapes), else null
   std::mutex ymu;
   std::map<int64_t, std::vector<uint32_t>> ycache;  // E -> 2^(W*S2 - E) mod N, tail limbs
   // decimal codec table (k_dec_parse), built on first use: Pt[l*jpad + j] = limb l of 10^(8j)
@@ -128,6 +129,7 @@ struct ModConsts {
   ~ModConsts() {
     if (d) (void)hipFree(d);
     if (d2) (void)hipFree(d2);
+    if (dq) (void)hipFree(dq);
     if (dtab) (void)hipFree(dtab);
   }
   std::vector<uint32_t> rw(const bn::Limbs& v) const { return bn::to_rw(v, S, W); }
@@ -275,6 +277,15 @@ int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_p
   if (hipMemcpy(mc->d, mc->host.data(), mc->host.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(mc->d2, mc->host2.data(), mc->host2.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
     return fail(DDS_E_HIP, "const upload");
+  if (tail_qp(mc->S2)) {
+    // N~ = N·n0 ≡ -1 mod 2^W: R2 = 2^(W·S2) > 4N~ holds (W·S2 >= bits(N) + W + 2)
+    const bn::Limbs nq = bn::mul(N, bn::Limbs{mc->n0});
+    if ((size_t)mc->W * mc->S2 < bn::bit_length(nq) + 2) return fail(DDS_E_UNSUPPORTED, "tail shape too narrow");
+    const std::vector<uint32_t> q = bn::to_rw(nq, mc->S2, mc->W);
+    if (hipMalloc(&mc->dq, q.size() * 4) != hipSuccess) return fail(DDS_E_NOMEM, "const alloc");
+    if (hipMemcpy(mc->dq, q.data(), q.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(DDS_E_HIP, "const upload");
+  }
   std::lock_guard<std::mutex> lk(ctx->mu);
   auto it = ctx->mods.find(N);
   if (it != ctx->mods.end()) {
@@ -331,7 +342,7 @@ int fold_partial_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, 
   size_t n = G, cs = ps;
   while (n > 1) {
     size_t ng = (n + 1) / 2, ns = round_up(ng, 64);
-    HIP_TRY(launch_fold_tail(S2, cur, cs, n, mc.d2, mc.n0, nxt, ns, ng, st));
+    HIP_TRY(launch_fold_tail(S2, cur, cs, n, mc.d2, mc.dq, mc.n0, nxt, ns, ng, st));
     std::swap(cur, nxt);
     n = ng;
     cs = ns;
@@ -1144,7 +1155,7 @@ int dds_combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, 
     int flip = 0;
     while (n > 1) {
       size_t ng = (n + 1) / 2, ns = round_up(ng, 64);
-      HIP_TRY(launch_fold_tail(mc->S2, cur, cs, n, mc->d2, mc->n0, bufs[flip], ns, ng, wl.st));
+      HIP_TRY(launch_fold_tail(mc->S2, cur, cs, n, mc->d2, mc->dq, mc->n0, bufs[flip], ns, ng, wl.st));
       cur = bufs[flip];
       flip ^= 1;
       n = ng;

@@ -77,7 +77,12 @@ __device__ __forceinline__ uint32_t grp_from_prev(uint32_t x) {
 }
 
 // ---- Montgomery product on a lane group --------------------------------------
-template <int S, int TPI, int W>
+// QP ("quotient pipelining" modulus): the caller passes N~ = N·n0 instead of N, so that
+// N~ ≡ -1 mod 2^W and the CIOS quotient is the low limb of t itself — no v_mul_lo on the
+// step's dependent chain. Products are then correct mod N~, hence mod N (N | N~), with values
+// < 2N~ (needs R > 4N~, i.e. W·S >= bits(N) + W + 2); a final product against N brings them
+// back below 2N. Used by the latency-bound tree levels.
+template <int S, int TPI, int W, bool QP = false>
 struct Mont {
   static_assert(S % TPI == 0, "S must divide into TPI lanes");
   static constexpr int L = S / TPI;
@@ -96,7 +101,7 @@ struct Mont {
     // (mul_lo -> and -> DPP) hides under the remaining L-1 mads.
 #ifndef DDSHE_AB_M_LATE
     t[0] = (uint64_t)a[0] * b + t[0];
-    const uint32_t m = grp_bcast0<TPI>(((uint32_t)t[0] * n0) & kMask);
+    const uint32_t m = grp_bcast0<TPI>((QP ? (uint32_t)t[0] : (uint32_t)t[0] * n0) & kMask);
 #pragma unroll
     for (int l = 1; l < L; ++l) t[l] = (uint64_t)a[l] * b + t[l];
 #else

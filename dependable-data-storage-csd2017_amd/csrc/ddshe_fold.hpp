@@ -84,12 +84,12 @@ struct Grp {
 // A group that folded c rows holds prod * R^(1-c). Requires 1 <= ngroups <= count (no empty
 // group: the launcher checks), which keeps the kernel body to load, MonPro loop, store.
 // ------------------------------------------------------------------------------
-template <int S, int TPI, int W>
+template <int S, int TPI, int W, bool QP = false>
 __global__ void __launch_bounds__(256, 2) k_fold(const uint32_t* __restrict__ X, size_t xstride, size_t count,
                                               const uint32_t* __restrict__ consts, uint32_t n0,
                                               uint32_t* __restrict__ P, size_t pstride, size_t ngroups) {
   using G = Grp<S, TPI, W>;
-  using M = Mont<S, TPI, W>;
+  using M = Mont<S, TPI, W, QP>;
   constexpr int L = G::L;
   G g;
   const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;

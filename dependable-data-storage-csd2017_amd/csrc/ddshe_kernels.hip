@@ -711,6 +711,13 @@ hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, c
 // Levels with more groups stay at TPI = 16 (fewer exchange instructions per mad). Same limb
 // layout and constants for both, so levels mix freely. DDSHE_TAIL32=0 disables (A/B timing).
 constexpr size_t kTail32MaxGroups = 2048;
+bool tail_qp(int S) {  // DDSHE_TAIL_QP=0 disables (A/B timing)
+  static const bool on = [] {
+    const char* e = getenv("DDSHE_TAIL_QP");
+    return !(e && e[0] == '0');
+  }();
+  return on && S == 160;
+}
 static bool use_tail32(int S, size_t ngroups) {
   static const bool on = [] {
     const char* e = getenv("DDSHE_TAIL32");
@@ -720,11 +727,16 @@ static bool use_tail32(int S, size_t ngroups) {
 }
 
 hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
-                            uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups, hipStream_t st) {
+                            const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups,
+                            hipStream_t st) {
   if (ngroups == 0 || ngroups > count) return hipErrorInvalidValue;
   if (use_tail32(S, ngroups)) {
-    hipLaunchKernelGGL((k_fold<160, 32, 28>), dim3(grid_for(ngroups * 32)), dim3(256), 0, st, X, xstride, count,
-                       consts, n0, P, pstride, ngroups);
+    if (qp_mod)  // N~ = N·n0 in place of N (Mont QP): the quotient needs no multiply
+      hipLaunchKernelGGL((k_fold<160, 32, 28, true>), dim3(grid_for(ngroups * 32)), dim3(256), 0, st, X, xstride,
+                         count, qp_mod, n0, P, pstride, ngroups);
+    else
+      hipLaunchKernelGGL((k_fold<160, 32, 28>), dim3(grid_for(ngroups * 32)), dim3(256), 0, st, X, xstride, count,
+                         consts, n0, P, pstride, ngroups);
     return hipGetLastError();
   }
   DDSHE_TAIL_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X,

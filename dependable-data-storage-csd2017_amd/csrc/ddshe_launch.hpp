@@ -28,8 +28,11 @@ hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, c
 hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts, uint32_t n0,
                        uint32_t* P, size_t pstride, size_t ngroups, int s_out, hipStream_t st);
 // tree levels / finalize in the tail shape (S = tail limb count, consts of the tail shape)
+// qp_mod (nullable): N~ = N·n0 in tail limbs, used by the latency-bound levels when tail_qp(S)
 hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
-                            uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups, hipStream_t st);
+                            const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups,
+                            hipStream_t st);
+bool tail_qp(int S);
 hipError_t launch_finalize_tail(int S, const uint32_t* P, size_t pstride, const uint32_t* consts, const uint32_t* Y,
                                 uint32_t n0, uint32_t* out, hipStream_t st);
 hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stride, size_t count,
