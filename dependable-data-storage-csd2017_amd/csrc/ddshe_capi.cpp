@@ -119,6 +119,7 @@ struct ModConsts {
   uint32_t* d = nullptr;         // device copies
   uint32_t* d2 = nullptr;
   uint32_t* dq = nullptr;        // N~ = N·n0 in tail limbs (tail_qp shapes), else null
+  uint32_t* dqm = nullptr;       // N~ in main limbs when R > 4N~ holds for the main shape, else null
   std::mutex ymu;
   std::map<int64_t, std::vector<uint32_t>> ycache;  // E -> 2^(W*S2 - E) mod N, tail limbs
   // decimal codec table (k_dec_parse), built on first use: Pt[l*jpad + j] = limb l of 10^(8j)
@@ -130,6 +131,7 @@ struct ModConsts {
     if (d) (void)hipFree(d);
     if (d2) (void)hipFree(d2);
     if (dq) (void)hipFree(dq);
+    if (dqm) (void)hipFree(dqm);
     if (dtab) (void)hipFree(dtab);
   }
   std::vector<uint32_t> rw(const bn::Limbs& v) const { return bn::to_rw(v, S, W); }
@@ -277,15 +279,21 @@ int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_p
   if (hipMemcpy(mc->d, mc->host.data(), mc->host.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(mc->d2, mc->host2.data(), mc->host2.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
     return fail(DDS_E_HIP, "const upload");
-  if (tail_qp(mc->S2)) {
-    // N~ = N·n0 ≡ -1 mod 2^W: R2 = 2^(W·S2) > 4N~ holds (W·S2 >= bits(N) + W + 2)
-    const bn::Limbs nq = bn::mul(N, bn::Limbs{mc->n0});
-    if ((size_t)mc->W * mc->S2 < bn::bit_length(nq) + 2) return fail(DDS_E_UNSUPPORTED, "tail shape too narrow");
-    const std::vector<uint32_t> q = bn::to_rw(nq, mc->S2, mc->W);
-    if (hipMalloc(&mc->dq, q.size() * 4) != hipSuccess) return fail(DDS_E_NOMEM, "const alloc");
-    if (hipMemcpy(mc->dq, q.data(), q.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+  // N~ = N·n0 ≡ -1 mod 2^W (Mont QP), for the shapes where R = 2^(W·S) > 4N~ holds
+  const bn::Limbs nq = bn::mul(N, bn::Limbs{mc->n0});
+  auto upload_qp = [&](int s, uint32_t** dst) -> int {
+    const std::vector<uint32_t> q = bn::to_rw(nq, s, mc->W);
+    if (hipMalloc(dst, q.size() * 4) != hipSuccess) return fail(DDS_E_NOMEM, "const alloc");
+    if (hipMemcpy(*dst, q.data(), q.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
       return fail(DDS_E_HIP, "const upload");
+    return DDS_OK;
+  };
+  if (tail_qp(mc->S2)) {
+    if ((size_t)mc->W * mc->S2 < bn::bit_length(nq) + 2) return fail(DDS_E_UNSUPPORTED, "tail shape too narrow");
+    if (int rc = upload_qp(mc->S2, &mc->dq)) return rc;
   }
+  if (fold_qp_enabled() && (size_t)mc->W * S >= bn::bit_length(nq) + 2)
+    if (int rc = upload_qp(S, &mc->dqm)) return rc;
   std::lock_guard<std::mutex> lk(ctx->mu);
   auto it = ctx->mods.find(N);
   if (it != ctx->mods.end()) {
@@ -329,7 +337,7 @@ int fold_partial_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, 
   HIP_TRY(w->p0.ensure((size_t)S2 * ps * 4));
   HIP_TRY(w->p1.ensure((size_t)S2 * round_up((G + 1) / 2, 64) * 4));
   record_time(ctx, w, st, true, 0);
-  HIP_TRY(launch_fold(S, X, xstride, count, mc.d, mc.n0, w->p0.as<uint32_t>(), ps, G, S2, st));
+  HIP_TRY(launch_fold(S, X, xstride, count, mc.d, mc.dqm, mc.n0, w->p0.as<uint32_t>(), ps, G, S2, st));
   record_time(ctx, w, st, false, 0);
   if (ctx->timing.load()) {
     w->timed_fold = true;

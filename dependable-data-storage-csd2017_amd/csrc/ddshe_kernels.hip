@@ -692,17 +692,30 @@ hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, c
   return hipGetLastError();
 }
 
-hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts, uint32_t n0,
-                       uint32_t* P, size_t pstride, size_t ngroups, int s_out, hipStream_t st) {
+hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
+                       const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups, int s_out, hipStream_t st) {
   if (ngroups == 0 || ngroups > count) return hipErrorInvalidValue;
   // limbs S..s_out of the partials (tail shape is wider): zero, contiguous in the limb-major layout
   if (s_out > S) {
     hipError_t e = hipMemsetAsync(P + (size_t)S * pstride, 0, (size_t)(s_out - S) * pstride * 4, st);
     if (e != hipSuccess) return e;
   }
-  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X, xstride,
-                                     count, consts, n0, P, pstride, ngroups));
+  if (qp_mod) {  // N~ = N·n0 in place of N (Mont QP): no v_mul_lo per CIOS step
+    DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W, true>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X,
+                                       xstride, count, qp_mod, n0, P, pstride, ngroups));
+  } else {
+    DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X,
+                                       xstride, count, consts, n0, P, pstride, ngroups));
+  }
   return hipGetLastError();
+}
+
+bool fold_qp_enabled() {  // DDSHE_FOLD_QP=0 disables (A/B timing)
+  static const bool on = [] {
+    const char* e = getenv("DDSHE_FOLD_QP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 // Latency-bound tree levels of the 4096-bit tail shape (S = 160, W = 28) run with 32 lanes per

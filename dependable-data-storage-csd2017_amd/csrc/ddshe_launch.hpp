@@ -25,8 +25,11 @@ hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S
 hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, const uint32_t* consts, uint32_t n0,
                               hipStream_t st);
 // main fold level (throughput shape); partial rows are zero-extended to s_out limbs
-hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts, uint32_t n0,
+// qp_mod (nullable): N~ = N·n0 in main limbs (when W·S >= bits(N~) + 2; see Mont QP)
+hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
+                       const uint32_t* qp_mod, uint32_t n0,
                        uint32_t* P, size_t pstride, size_t ngroups, int s_out, hipStream_t st);
+bool fold_qp_enabled();
 // tree levels / finalize in the tail shape (S = tail limb count, consts of the tail shape)
 // qp_mod (nullable): N~ = N·n0 in tail limbs, used by the latency-bound levels when tail_qp(S)
 hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
