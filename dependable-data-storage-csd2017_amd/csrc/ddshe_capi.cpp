@@ -1250,8 +1250,8 @@ int modexp_device(Worker* w, hipStream_t st, ModConsts& mc, const bn::Limbs& E, 
   HIP_TRY(w->tab.ensure((size_t)nodd * S * chunk * 4));
   for (size_t c0 = 0; c0 < count; c0 += chunk) {
     const size_t cc = std::min(chunk, count - c0);
-    HIP_TRY(launch_modexp_pre(S, d_x + c0, xstride, cc, mc.d, mc.n0, nodd, w->tab.as<uint32_t>(), chunk, st));
-    HIP_TRY(launch_modexp_ladder(S, w->tab.as<uint32_t>(), chunk, d_m ? d_m + c0 : nullptr, cc, mc.d, d_gr, d_sched,
+    HIP_TRY(launch_modexp_pre(S, d_x + c0, xstride, cc, mc.d, mc.dqm, mc.n0, nodd, w->tab.as<uint32_t>(), chunk, st));
+    HIP_TRY(launch_modexp_ladder(S, w->tab.as<uint32_t>(), chunk, d_m ? d_m + c0 : nullptr, cc, mc.d, mc.dqm, d_gr, d_sched,
                                  (int)sched.size(), mc.n0, d_out + c0, ostride, st));
   }
   HIP_TRY(hipStreamSynchronize(st));  // host vectors above must outlive the async copies

@@ -137,12 +137,14 @@ __device__ __forceinline__ void store_lds(uint32_t* dst, const uint32_t (&a)[S /
   for (int l = 0; l < S / TPI; ++l) dst[r * (S / TPI) + l] = a[l];
 }
 
-template <int S, int TPI, int W>
+// QP: products against N~ = N·n0 (qp_mod, see Mont QP); table entries are then < 2N~.
+template <int S, int TPI, int W, bool QP = false>
 __global__ void __launch_bounds__(256, 2) k_modexp_pre(const uint32_t* __restrict__ Xcol, size_t xstride,
-                                                    size_t count, const uint32_t* __restrict__ consts, uint32_t n0,
+                                                    size_t count, const uint32_t* __restrict__ consts,
+                                                    const uint32_t* __restrict__ qp_mod, uint32_t n0,
                                                     int nodd, uint32_t* __restrict__ Tab, size_t tstride) {
   using G = Grp<S, TPI, W>;
-  using M = Mont<S, TPI, W>;
+  using M = Mont<S, TPI, W, QP>;
   constexpr int L = G::L;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   G g;
@@ -151,7 +153,7 @@ __global__ void __launch_bounds__(256, 2) k_modexp_pre(const uint32_t* __restric
   uint32_t* x1 = lds + (size_t)(threadIdx.x / TPI) * 2 * S;  // group-private operand slots
   uint32_t* x2 = x1 + S;
   uint32_t n[L], acc[L];
-  g.load_vec(n, consts + kConstN * S);
+  g.load_vec(n, QP ? qp_mod : consts + kConstN * S);
   g.load_col(acc, Xcol, xstride, grp);
   M::mul_col(acc, n, consts + kConstR2 * S, 1, 0, n0, g.top, g.bottom);  // x*R
   M::normalize(acc, g.bottom);
@@ -172,15 +174,18 @@ __global__ void __launch_bounds__(256, 2) k_modexp_pre(const uint32_t* __restric
 
 // sched[0] = index of the leading window; sched[1..nsched) = (nsq << 16) | (idx + 1),
 // idx + 1 == 0: squarings only. nsched == 0: E == 0 (x^0 = 1).
-template <int S, int TPI, int W>
+// QP: every product but the last against N~ = N·n0 (values < 2N~); the last one, against N,
+// leaves the Montgomery form below 2N (R > 2N~) for the canonical reduction.
+template <int S, int TPI, int W, bool QP = false>
 __global__ void __launch_bounds__(256, 2) k_modexp_ladder(const uint32_t* __restrict__ Tab, size_t tstride,
                                                        const uint32_t* __restrict__ m, size_t count,
                                                        const uint32_t* __restrict__ consts,
+                                                       const uint32_t* __restrict__ qp_mod,
                                                        const uint32_t* __restrict__ gR,
                                                        const uint32_t* __restrict__ sched, int nsched, uint32_t n0,
                                                        uint32_t* __restrict__ O, size_t ostride) {
   using G = Grp<S, TPI, W>;
-  using M = Mont<S, TPI, W>;
+  using M = Mont<S, TPI, W, QP>;
   constexpr int L = G::L;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   G g;
@@ -189,7 +194,7 @@ __global__ void __launch_bounds__(256, 2) k_modexp_ladder(const uint32_t* __rest
   uint32_t* sq = lds + (size_t)(threadIdx.x / TPI) * 2 * S;  // group-private operand slots
   uint32_t* xs = sq + S;
   uint32_t n[L], acc[L];
-  g.load_vec(n, consts + kConstN * S);
+  g.load_vec(n, QP ? qp_mod : consts + kConstN * S);
   if (nsched > 0) g.load_col(acc, Tab + (size_t)sched[0] * S * tstride, tstride, grp);
   else g.load_vec(acc, consts + kConstRmod * S);  // 1*R
   for (int k = 1; k < nsched; ++k) {
@@ -224,7 +229,8 @@ __global__ void __launch_bounds__(256, 2) k_modexp_ladder(const uint32_t* __rest
     // acc = (g^m R) * (x^E R) * R^-1
     M::mul_lds(acc, n, xs, n0, g.top, g.bottom);
   }
-  M::mul_col(acc, n, consts + kConstOne * S, 1, 0, n0, g.top, g.bottom);  // leave Montgomery form
+  if constexpr (QP) g.load_vec(n, consts + kConstN * S);
+  Mont<S, TPI, W>::mul_col(acc, n, consts + kConstOne * S, 1, 0, n0, g.top, g.bottom);  // leave Montgomery form
   g.canon(acc, n);
   g.store_col(acc, O, ostride, grp);
 }
@@ -779,20 +785,35 @@ hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stri
 }
 
 hipError_t launch_modexp_pre(int S, const uint32_t* Xcol, size_t xstride, size_t count, const uint32_t* consts,
-                             uint32_t n0, int nodd, uint32_t* Tab, size_t tstride, hipStream_t st) {
+                             const uint32_t* qp_mod, uint32_t n0, int nodd, uint32_t* Tab, size_t tstride,
+                             hipStream_t st) {
   if (count == 0) return hipSuccess;
-  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_modexp_pre<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256),
-                                     (256 / TPI) * 2 * S * 4, st, Xcol, xstride, count, consts, n0, nodd, Tab, tstride));
+  if (qp_mod) {
+    DDSHE_SWITCH(S, hipLaunchKernelGGL((k_modexp_pre<S, TPI, W, true>), dim3(grid_for(count * TPI)), dim3(256),
+                                       (256 / TPI) * 2 * S * 4, st, Xcol, xstride, count, consts, qp_mod, n0, nodd,
+                                       Tab, tstride));
+  } else {
+    DDSHE_SWITCH(S, hipLaunchKernelGGL((k_modexp_pre<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256),
+                                       (256 / TPI) * 2 * S * 4, st, Xcol, xstride, count, consts, nullptr, n0, nodd,
+                                       Tab, tstride));
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_modexp_ladder(int S, const uint32_t* Tab, size_t tstride, const uint32_t* m, size_t count,
-                                const uint32_t* consts, const uint32_t* gR, const uint32_t* sched, int nsched,
-                                uint32_t n0, uint32_t* O, size_t ostride, hipStream_t st) {
+                                const uint32_t* consts, const uint32_t* qp_mod, const uint32_t* gR,
+                                const uint32_t* sched, int nsched, uint32_t n0, uint32_t* O, size_t ostride,
+                                hipStream_t st) {
   if (count == 0) return hipSuccess;
-  DDSHE_SWITCH(S, hipLaunchKernelGGL((k_modexp_ladder<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256),
-                                     (256 / TPI) * 2 * S * 4, st, Tab, tstride, m, count, consts, gR, sched, nsched,
-                                     n0, O, ostride));
+  if (qp_mod) {
+    DDSHE_SWITCH(S, hipLaunchKernelGGL((k_modexp_ladder<S, TPI, W, true>), dim3(grid_for(count * TPI)), dim3(256),
+                                       (256 / TPI) * 2 * S * 4, st, Tab, tstride, m, count, consts, qp_mod, gR, sched,
+                                       nsched, n0, O, ostride));
+  } else {
+    DDSHE_SWITCH(S, hipLaunchKernelGGL((k_modexp_ladder<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256),
+                                       (256 / TPI) * 2 * S * 4, st, Tab, tstride, m, count, consts, nullptr, gR, sched,
+                                       nsched, n0, O, ostride));
+  }
   return hipGetLastError();
 }
 

@@ -42,12 +42,14 @@ hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stri
                         const uint32_t* consts, uint32_t n0, uint32_t* O, hipStream_t st);
 // modexp table: Tab[j] = x^(2j+1)*R mod N (j < nodd), entry j at Tab + j*S*tstride
 hipError_t launch_modexp_pre(int S, const uint32_t* Xcol, size_t xstride, size_t count, const uint32_t* consts,
-                             uint32_t n0, int nodd, uint32_t* Tab, size_t tstride, hipStream_t st);
+                             const uint32_t* qp_mod, uint32_t n0, int nodd, uint32_t* Tab, size_t tstride,
+                             hipStream_t st);
 // O = g^m_i * x_i^E mod N (m == nullptr: x_i^E) from the table and the host-built window schedule;
 // gR = g*R mod N in rW limbs
 hipError_t launch_modexp_ladder(int S, const uint32_t* Tab, size_t tstride, const uint32_t* m, size_t count,
-                                const uint32_t* consts, const uint32_t* gR, const uint32_t* sched, int nsched,
-                                uint32_t n0, uint32_t* O, size_t ostride, hipStream_t st);
+                                const uint32_t* consts, const uint32_t* qp_mod, const uint32_t* gR,
+                                const uint32_t* sched, int nsched, uint32_t n0, uint32_t* O, size_t ostride,
+                                hipStream_t st);
 // CRT encryption pieces (see ddshe_kernels.hip): radix change between rW layouts (flags[0] |= 1 on
 // overflow), h = (y_p - y_q)(q^2)^-1 mod p^2 (c12 = c1R | c2R, 2*S limbs), c = h*q^2 + y_q
 hipError_t launch_repack(const uint32_t* src, size_t sstride, int Ss, int Ws, uint32_t* dst, size_t dstride, int Sd,
