@@ -758,8 +758,13 @@ hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t cou
                          consts, n0, P, pstride, ngroups);
     return hipGetLastError();
   }
-  DDSHE_TAIL_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X,
-                                          xstride, count, consts, n0, P, pstride, ngroups));
+  if (qp_mod) {
+    DDSHE_TAIL_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W, true>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st,
+                                            X, xstride, count, qp_mod, n0, P, pstride, ngroups));
+  } else {
+    DDSHE_TAIL_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X,
+                                            xstride, count, consts, n0, P, pstride, ngroups));
+  }
   return hipGetLastError();
 }
 
