@@ -89,6 +89,32 @@ def test_fold_random_moduli(eng, bits):
         assert eng.modmul_fold(N, xs) == homo.modmul_fold(xs, N), (bits, k)
 
 
+# Moduli on either side of the QP limit of each shape (Mont QP reduces against N~ = N·n0, which
+# needs W·S >= bits(N) + W + 2; above it the shape keeps n0), with worst-case operands (N-1 and
+# near it). k = 5000 runs the tree through 16-lane (> 2048 groups) and 32-lane (QP) levels.
+QP_EDGE_BITS = [1090, 1118, 2042, 2070, 3106, 3134, 4114, 4142, 6235, 6262]
+
+
+@pytest.mark.parametrize("bits", QP_EDGE_BITS)
+def test_fold_qp_shape_edges(eng, bits):
+    rng = random.Random(bits * 7)
+    N = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+    for k in (2, 3, 5000):
+        xs = [N - 1 - rng.randrange(4) for _ in range(k)]
+        assert eng.modmul_fold(N, xs) == homo.modmul_fold(xs, N), (bits, k)
+    xs = [rng.randrange(N) for _ in range(777)]
+    assert eng.modmul_fold(N, xs) == homo.modmul_fold(xs, N), bits
+
+
+@pytest.mark.parametrize("bits", [1090, 1118, 3106, 3134])
+def test_modexp_qp_shape_edges(eng, bits):
+    rng = random.Random(bits * 11)
+    N = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+    e = rng.getrandbits(bits) | 1
+    xs = [N - 1, N - 2, 1, 0] + [rng.randrange(N) for _ in range(60)]
+    assert eng.modexp_batch(N, e, xs) == [pow(x, e, N) for x in xs], bits
+
+
 @pytest.mark.parametrize("k", SIZES)
 def test_fold_sizes_committed_nsq(eng, keys, k):
     N = keys["paillier2048_committed"]["nsquare"]
