@@ -408,8 +408,8 @@ class ProductFilterWorkload(_Workload):
             if not ok:
                 print("VERIFY FAILED", file=sys.stderr)
         roof = self.fold_roofline(64)
-        roof["kernel"] = "k_fold<74,2,28> (first MultAll fold level, 2048-bit n)"
-        roof["traffic"] = pmc_traffic("product_filter", ("k_fold<74, 2, 28>",))
+        roof["kernel"] = "k_fold<76,2,28,QP> (first MultAll fold level, 2048-bit n)"
+        roof["traffic"] = pmc_traffic("product_filter", ("k_fold<76, 2, 28, true>",))
         roof["traffic_unit"] = "HBM bytes per launch (PMC, profiles/r01_pmc_filter_order.json)"
         _, _, filt_dev_ms, _ = self.eng.timing()  # HIP events around the filter launches (device time)
         filt_s = filt_dev_ms / 1e3 / (4 * a.steps)

@@ -664,9 +664,22 @@ __global__ void __launch_bounds__(256) k_bigmul_carry(const uint32_t* __restrict
 // ------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------
+// 2048-bit moduli (RSA n) use S = 76, not the minimal 74: 4-limb blocks (fewer loop instructions per
+// CIOS step) and room for the QP modulus (no v_mul_lo) outweigh the 5.5 % more mads: MultAll fold
+// 4.08-4.11 -> 4.01 ms over 10M rows (profiles/r01_rsa76_ab.txt). DDSHE_RSA76=0 keeps S = 74.
+static bool use_rsa76() {
+  static const bool on = [] {
+    const char* e = getenv("DDSHE_RSA76");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 Shape pick_shape(size_t mod_bits) {
-  for (const Shape& s : kShapes)
+  for (const Shape& s : kShapes) {
+    if (s.S == (use_rsa76() ? 74 : 76)) continue;
     if ((size_t)s.W * s.S >= mod_bits + 2) return s;
+  }
   return Shape{0, 0, 0};
 }
 

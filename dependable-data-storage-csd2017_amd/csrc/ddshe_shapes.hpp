@@ -16,15 +16,18 @@ namespace ddshe {
   switch (S_RT) {                                    \
     DDSHE_DISPATCH(40, 2, 28, __VA_ARGS__)           \
     DDSHE_DISPATCH(74, 2, 28, __VA_ARGS__)           \
+    DDSHE_DISPATCH(76, 2, 28, __VA_ARGS__)           \
     DDSHE_DISPATCH(112, 4, 28, __VA_ARGS__)          \
     DDSHE_DISPATCH(148, 4, 28, __VA_ARGS__)          \
     DDSHE_DISPATCH(232, 8, 27, __VA_ARGS__)          \
     default: return hipErrorInvalidValue;            \
   }
 
-inline constexpr Shape kShapes[] = {{40, 2, 28}, {74, 2, 28}, {112, 4, 28}, {148, 4, 28}, {232, 8, 27}};
+// {76, 2, 28} is the 2048-bit alternative to {74, 2, 28} (4-limb blocks, room for the QP modulus);
+// pick_shape uses 76 unless DDSHE_RSA76=0
+inline constexpr Shape kShapes[] = {{40, 2, 28}, {74, 2, 28}, {76, 2, 28}, {112, 4, 28}, {148, 4, 28}, {232, 8, 27}};
 // latency-oriented shapes for the reduction tree / finalize: 16 lanes per bignum
-inline constexpr Shape kTail[] = {{48, 16, 28}, {80, 16, 28}, {112, 16, 28}, {160, 16, 28}, {240, 16, 27}};
+inline constexpr Shape kTail[] = {{48, 16, 28}, {80, 16, 28}, {80, 16, 28}, {112, 16, 28}, {160, 16, 28}, {240, 16, 27}};
 
 #define DDSHE_TAIL_SWITCH(S_RT, ...)                 \
   switch (S_RT) {                                    \

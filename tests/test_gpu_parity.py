@@ -92,7 +92,7 @@ def test_fold_random_moduli(eng, bits):
 # Moduli on either side of the QP limit of each shape (Mont QP reduces against N~ = N·n0, which
 # needs W·S >= bits(N) + W + 2; above it the shape keeps n0), with worst-case operands (N-1 and
 # near it). k = 5000 runs the tree through 16-lane (> 2048 groups) and 32-lane (QP) levels.
-QP_EDGE_BITS = [1090, 1118, 2042, 2070, 3106, 3134, 4114, 4142, 6235, 6262]
+QP_EDGE_BITS = [1090, 1118, 2042, 2070, 2098, 2126, 3106, 3134, 4114, 4142, 6235, 6262]
 
 
 @pytest.mark.parametrize("bits", QP_EDGE_BITS)
