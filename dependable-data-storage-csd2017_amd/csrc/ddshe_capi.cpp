@@ -22,12 +22,13 @@
 #include <thread>
 #include <vector>
 
-#include "bn_host.hpp"
-#include "ddshe_launch.hpp"
+#include "ddshe_host.hpp"
 
 using namespace ddshe;
+using namespace ddshe::host;
 
-namespace {
+namespace ddshe {
+namespace host {
 
 thread_local std::string g_last_error;
 
@@ -36,203 +37,29 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
-#define HIP_TRY(expr)                                                                             \
-  do {                                                                                            \
-    hipError_t e_ = (expr);                                                                       \
-    if (e_ != hipSuccess) return fail(DDS_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
-  } while (0)
 
-struct DevBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
-  }
-  hipError_t ensure(size_t bytes) {
-    if (bytes <= cap) return hipSuccess;
-    if (p) {
-      (void)hipFree(p);
-      p = nullptr;
-      cap = 0;
-    }
-    size_t nb = std::max<size_t>(bytes, 256);
-    hipError_t e = hipMalloc(&p, nb);
-    if (e == hipSuccess) cap = nb;
-    return e;
-  }
-  template <class T>
-  T* as() const {
-    return (T*)p;
-  }
-};
 
-struct HostBuf {  // pinned staging (truly asynchronous H2D)
-  void* p = nullptr;
-  size_t cap = 0;
-  ~HostBuf() {
-    if (p) (void)hipHostFree(p);
-  }
-  hipError_t ensure(size_t bytes) {
-    if (bytes <= cap) return hipSuccess;
-    if (p) {
-      (void)hipHostFree(p);
-      p = nullptr;
-      cap = 0;
-    }
-    hipError_t e = hipHostMalloc(&p, bytes, 0);
-    if (e == hipSuccess) cap = bytes;
-    return e;
-  }
-};
 
-struct Worker {
-  hipStream_t stream = nullptr;
-  bool timed_fold = false;  // ev[0]/ev[1] bracket a first-level fold launch not yet accounted
-  DevBuf in, in2, x, x2, p0, p1, out, flags, y, misc, misc2, tab;
-  DevBuf crt[7];  // CRT encryption scratch (see encrypt_crt_device)
-  hipEvent_t ev[4] = {};
-  // decimal codec: double-buffered pinned chunks (chars, offsets), their device copies,
-  // per-row status bytes, and the event after each slot's last use
-  HostBuf hch[2], hoff[2];
-  DevBuf dch[2], doff[2], rflags;
-  hipEvent_t ev_dec[2] = {};
-  ~Worker() {
-    for (auto e : ev)
-      if (e) (void)hipEventDestroy(e);
-    for (auto e : ev_dec)
-      if (e) (void)hipEventDestroy(e);
-    if (stream) (void)hipStreamDestroy(stream);
-  }
-};
+// rows of one rW matrix of this modulus' shape must stay addressable by the kernels (max_stride)
+int check_rows(const ModConsts& mc, size_t rows) {
+  if (round_up(std::max<size_t>(rows, 1), 64) > max_stride(mc.S))
+    return fail(DDS_E_UNSUPPORTED, "row count " + std::to_string(rows) + " exceeds the " +
+                                       std::to_string(max_stride(mc.S)) + "-row limit of one column of this modulus");
+  return DDS_OK;
+}
 
-// Per-modulus constants for the two kernel shapes: the throughput shape (S limbs, TPI
-// lanes) of the first fold level, and the latency shape (S2 limbs, 16 lanes) of the
-// reduction tree and finalize. Both use radix 2^W, so R = 2^(W*S) and R2 = 2^(W*S2)
-// differ only by a power of two: every partial is tracked as prod * 2^E (E signed).
-struct ModConsts {
-  int S = 0, TPI = 0, W = 0, S2 = 0;
-  size_t bits = 0, bytes = 0;
-  uint32_t n0 = 0;
-  bn::Limbs N, Rmod, half;       // half = (N+1)/2 = 2^-1 mod N
-  std::vector<uint32_t> host;    // kConstCount * S  (throughput shape)
-  std::vector<uint32_t> host2;   // kConstCount * S2 (tail shape)
-  uint32_t* d = nullptr;         // device copies
-  uint32_t* d2 = nullptr;
-  uint32_t* dq = nullptr;        // N~ = N·n0 in tail limbs (tail_qp shapes), else null
-  uint32_t* dqm = nullptr;       // N~ in main limbs when R > 4N~ holds for the main shape, else null
-  std::mutex ymu;
-  std::map<int64_t, std::vector<uint32_t>> ycache;  // E -> 2^(W*S2 - E) mod N, tail limbs
-  // decimal codec table (k_dec_parse), built on first use: Pt[l*jpad + j] = limb l of 10^(8j)
-  // for the jfit powers below 2^(W*S), then jst[i] (first power reaching limb TPI*i, rounded down to 4)
-  std::mutex decmu;
-  uint32_t* dtab = nullptr;
-  int jfit = 0, jpad = 0;
-  ~ModConsts() {
-    if (d) (void)hipFree(d);
-    if (d2) (void)hipFree(d2);
-    if (dq) (void)hipFree(dq);
-    if (dqm) (void)hipFree(dqm);
-    if (dtab) (void)hipFree(dtab);
-  }
-  std::vector<uint32_t> rw(const bn::Limbs& v) const { return bn::to_rw(v, S, W); }
-  bn::Limbs value(const uint32_t* limbs) const { return bn::from_rw(limbs, S, W); }
-  bn::Limbs value2(const uint32_t* limbs) const { return bn::from_rw(limbs, S2, W); }
-  // 2^e mod N for a signed e
-  bn::Limbs pow2(int64_t e) const {
-    return e >= 0 ? bn::powmod_u64(bn::Limbs{2}, (uint64_t)e, N) : bn::powmod_u64(half, (uint64_t)(-e), N);
-  }
-  // finalize multiplier for a tail-shape partial holding prod * 2^E
-  const std::vector<uint32_t>& y_for(int64_t E) {
-    std::lock_guard<std::mutex> lk(ymu);
-    auto it = ycache.find(E);
-    if (it != ycache.end()) return it->second;
-    if (ycache.size() > 64) ycache.clear();
-    bn::Limbs y = pow2((int64_t)W * S2 - E);
-    return ycache.emplace(E, bn::to_rw(y, S2, W)).first->second;
-  }
-  // bits of 2 contributed by one Montgomery product of the main / tail shape
-  int64_t wS() const { return (int64_t)W * S; }
-  int64_t wS2() const { return (int64_t)W * S2; }
-};
-
-// partial exchanged between GPUs: S2 tail limbs + signed exponent E (two words)
-size_t partial_words_for(const ModConsts& mc) { return (size_t)mc.S2 + 2; }
-
-}  // namespace
-
-struct CrtKey;  // CRT form of a Paillier key (encrypt_crt_device)
-
-struct dds_ctx {
-  int device = 0;
-  int cus = 0;
-  std::mutex mu;
-  std::vector<std::unique_ptr<Worker>> workers;
-  std::vector<Worker*> idle;
-  std::map<bn::Limbs, std::shared_ptr<ModConsts>> mods;
-  std::map<std::pair<bn::Limbs, bn::Limbs>, std::shared_ptr<CrtKey>> crt_keys;
-  hipStream_t ext_stream = nullptr;
-  std::atomic<bool> timing{false};
-  std::mutex tmu;
-  double fold_ms = 0, total_ms = 0;
-  uint64_t fold_launches = 0, fold_modmuls = 0, pending_modmuls = 0;
-};
-
-struct dds_col {
-  dds_ctx* ctx = nullptr;
-  std::shared_ptr<ModConsts> mc;
-  size_t capacity = 0, count = 0, stride = 0;
-  uint32_t* d = nullptr;
-  std::mutex mu;
-  ~dds_col() {
-    if (d) (void)hipFree(d);
-  }
-};
-
-namespace {
-
-struct WorkerLease {
-  dds_ctx* ctx;
-  Worker* w = nullptr;
-  hipStream_t st = nullptr;
-  explicit WorkerLease(dds_ctx* c) : ctx(c) {}
-  int acquire() {
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    if (!ctx->idle.empty()) {
-      w = ctx->idle.back();
-      ctx->idle.pop_back();
-    } else {
-      auto nw = std::make_unique<Worker>();
-      if (hipSetDevice(ctx->device) != hipSuccess) return fail(DDS_E_HIP, "hipSetDevice");
-      if (hipStreamCreateWithFlags(&nw->stream, hipStreamNonBlocking) != hipSuccess)
-        return fail(DDS_E_HIP, "hipStreamCreate");
-      for (auto& e : nw->ev)
-        if (hipEventCreate(&e) != hipSuccess) return fail(DDS_E_HIP, "hipEventCreate");
-      for (auto& e : nw->ev_dec)
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(DDS_E_HIP, "hipEventCreate");
-      w = nw.get();
-      ctx->workers.push_back(std::move(nw));
-    }
-    st = ctx->ext_stream ? ctx->ext_stream : w->stream;
-    return DDS_OK;
-  }
-  ~WorkerLease() {
-    if (w) {
-      std::lock_guard<std::mutex> lk(ctx->mu);
-      ctx->idle.push_back(w);
-    }
-  }
-};
-
-size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-
-int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_ptr<ModConsts>* out) {
+int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_ptr<ModConsts>* out,
+            size_t min_bits) {
   if (!mod_be || mod_bytes == 0) return fail(DDS_E_ARG, "modulus missing");
   bn::Limbs N = bn::from_be(mod_be, mod_bytes);
   if (N.empty() || (N[0] & 1u) == 0 || bn::bit_length(N) < 2)
     return fail(DDS_E_ARG, "modulus must be odd and > 1 (Montgomery)");
+  const Shape sh = pick_shape(std::max(bn::bit_length(N), min_bits));
+  if (!sh.S) return fail(DDS_E_UNSUPPORTED, "modulus too large");
+  const auto key = std::make_pair(N, sh.S);
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
-    auto it = ctx->mods.find(N);
+    auto it = ctx->mods.find(key);
     if (it != ctx->mods.end()) {
       *out = it->second;
       return DDS_OK;
@@ -241,8 +68,6 @@ int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_p
   auto mc = std::make_shared<ModConsts>();
   mc->bits = bn::bit_length(N);
   mc->bytes = (mc->bits + 7) / 8;
-  const Shape sh = pick_shape(mc->bits);
-  if (!sh.S) return fail(DDS_E_UNSUPPORTED, "modulus too large");
   const Shape tail = tail_shape(sh);
   mc->S = sh.S;
   mc->TPI = sh.TPI;
@@ -288,19 +113,23 @@ int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_p
       return fail(DDS_E_HIP, "const upload");
     return DDS_OK;
   };
+  mc->qbound = N;
   if (tail_qp(mc->S2)) {
     if ((size_t)mc->W * mc->S2 < bn::bit_length(nq) + 2) return fail(DDS_E_UNSUPPORTED, "tail shape too narrow");
     if (int rc = upload_qp(mc->S2, &mc->dq)) return rc;
+    mc->qbound = nq;
   }
-  if (fold_qp_enabled() && (size_t)mc->W * S >= bn::bit_length(nq) + 2)
+  if (fold_qp_enabled() && (size_t)mc->W * S >= bn::bit_length(nq) + 2) {
     if (int rc = upload_qp(S, &mc->dqm)) return rc;
+    mc->qbound = nq;  // level-1 partials are then < 2N~ too
+  }
   std::lock_guard<std::mutex> lk(ctx->mu);
-  auto it = ctx->mods.find(N);
+  auto it = ctx->mods.find(key);
   if (it != ctx->mods.end()) {
     *out = it->second;
     return DDS_OK;
   }
-  ctx->mods.emplace(N, mc);
+  ctx->mods.emplace(key, mc);
   *out = mc;
   return DDS_OK;
 }
@@ -325,19 +154,18 @@ size_t max_fold_groups(dds_ctx* ctx, int S) {
   return (size_t)ctx->cus * bpc * (256 / pick_tpi(S));
 }
 
-// Fold `count` rows of an rW column into one un-finalised partial: tail-shape limbs
-// (row 0 of `*part`, stride `*part_stride`) holding prod(rows) * 2^(*E).
+// Partial of `count` rows (declared in ddshe_host.hpp):
 //   level 1 (throughput shape, G groups): group g holds prod_g * R^(1 - c_g)
 //   tree (tail shape, G-1 products):      multiplies by R2^-(G-1)
 int fold_partial_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
-                        size_t count, const uint32_t** part, size_t* part_stride, int64_t* E) {
+                        size_t count, const uint32_t** part, size_t* part_stride, int64_t* E, const uint32_t* d_ids) {
   const int S = mc.S, S2 = mc.S2;
   size_t G = std::min(max_fold_groups(ctx, S), std::max<size_t>(1, count / 2));
   size_t ps = round_up(G, 64);
   HIP_TRY(w->p0.ensure((size_t)S2 * ps * 4));
   HIP_TRY(w->p1.ensure((size_t)S2 * round_up((G + 1) / 2, 64) * 4));
   record_time(ctx, w, st, true, 0);
-  HIP_TRY(launch_fold(S, X, xstride, count, mc.d, mc.dqm, mc.n0, w->p0.as<uint32_t>(), ps, G, S2, st));
+  HIP_TRY(launch_fold(S, X, xstride, count, mc.d, mc.dqm, mc.n0, w->p0.as<uint32_t>(), ps, G, S2, st, d_ids));
   record_time(ctx, w, st, false, 0);
   if (ctx->timing.load()) {
     w->timed_fold = true;
@@ -378,7 +206,7 @@ void account_fold(dds_ctx* ctx, Worker* w) {
 int finalize_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* part, size_t pstride,
                     int64_t E, std::vector<uint32_t>* result_rw) {
   const int S2 = mc.S2;
-  const std::vector<uint32_t>& y = mc.y_for(E);
+  const std::vector<uint32_t> y = mc.y_for(E);  // local copy outlives the async H2D (synced below)
   HIP_TRY(w->y.ensure((size_t)S2 * 4));
   HIP_TRY(w->out.ensure((size_t)S2 * 4));
   HIP_TRY(hipMemcpyAsync(w->y.p, y.data(), (size_t)S2 * 4, hipMemcpyHostToDevice, st));
@@ -397,105 +225,26 @@ int emit_be(const bn::Limbs& v, size_t width, uint8_t* out, size_t out_cap, size
   return DDS_OK;
 }
 
-// Upload `count` big-endian operands into an rW column (X, stride) validated against mc.
-// Host worker pool for the boundary codecs: parallel copies of caller buffers into pinned staging
-// (one thread copies ~10-15 GB/s, below what PCIe moves). parallel_for(n, f) splits [0, n) into
-// one contiguous slice per thread, aligned to `align`, and calls f(begin, end) on each.
-class CopyPool {
- public:
-  static CopyPool& get() {
-    static CopyPool pool;
-    return pool;
-  }
-  template <class F>
-  void parallel_for(size_t n, size_t align, F&& f) {
-    // a forked child inherits the pool object but not its threads: run on the calling thread
-    if (th_.empty() || getpid() != owner_) {
-      f((size_t)0, n);
-      return;
-    }
-    std::lock_guard<std::mutex> job(job_mu_);
-    const size_t T = th_.size() + 1;
-    size_t piece = (n + T - 1) / T;
-    piece = (piece + align - 1) / align * align;
-    std::function<void(size_t, size_t)> fn = f;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      fn_ = &fn;
-      n_ = n;
-      piece_ = piece;
-      pending_ = (int)th_.size();
-      ++gen_;
-    }
-    cv_.notify_all();
-    f((size_t)0, std::min(piece, n));  // slice 0 on the calling thread
-    std::unique_lock<std::mutex> lk(mu_);
-    done_.wait(lk, [&] { return pending_ == 0; });
-  }
-  void copy(void* dst, const void* src, size_t n) {
-    if (n < ((size_t)4 << 20)) {
-      memcpy(dst, src, n);
-      return;
-    }
-    parallel_for(n, 4096, [&](size_t a, size_t e) { memcpy((char*)dst + a, (const char*)src + a, e - a); });
-  }
-  ~CopyPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
 
- private:
-  CopyPool() : owner_(getpid()) {
-    int n = 8;
-    if (const char* e = getenv("DDSHE_COPY_THREADS")) n = atoi(e);
-    n = std::max(1, std::min(n, 64));
-    for (int i = 1; i < n; ++i) th_.emplace_back([this, i] { run(i); });
-  }
-  void run(int id) {
-    uint64_t seen = 0;
-    for (;;) {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-      if (stop_) return;
-      seen = gen_;
-      const std::function<void(size_t, size_t)>* fn = fn_;
-      const size_t n = n_, a = (size_t)id * piece_;
-      const size_t e = a < n ? std::min(n, a + piece_) : a;
-      lk.unlock();
-      if (e > a) (*fn)(a, e);
-      lk.lock();
-      if (--pending_ == 0) done_.notify_one();
-    }
-  }
-  pid_t owner_;
-  std::vector<std::thread> th_;
-  std::mutex mu_, job_mu_;
-  std::condition_variable cv_, done_;
-  const std::function<void(size_t, size_t)>* fn_ = nullptr;
-  size_t n_ = 0, piece_ = 0;
-  uint64_t gen_ = 0;
-  int pending_ = 0;
-  bool stop_ = false;
-};
-
-constexpr size_t kIngestChunkBytes = (size_t)64 << 20;  // binary rows per pinned chunk
 
 int ingest(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint8_t* ops, size_t width, size_t count,
-           DevBuf& raw, uint32_t* X, size_t stride) {
+           DevBuf& raw, uint32_t* X, size_t stride, std::vector<size_t>* reduced) {
   (void)ctx;
   if (count == 0) return DDS_OK;
   HIP_TRY(w->flags.ensure(16));
   HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, st));
+  uint8_t* rowflags = nullptr;
+  if (reduced) {
+    HIP_TRY(w->rflags.ensure(count));
+    rowflags = w->rflags.as<uint8_t>();
+  }
   const uint32_t* n2x = mc.d + (size_t)kConstN2x * mc.S;
   const size_t crows = std::max<size_t>(1, kIngestChunkBytes / width);
   if (count <= crows) {
     HIP_TRY(raw.ensure(count * width));
     HIP_TRY(hipMemcpyAsync(raw.p, ops, count * width, hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_ingest_be(raw.as<uint8_t>(), width, count, mc.S, mc.W, n2x, X, stride, w->flags.as<uint32_t>(), st));
+    HIP_TRY(launch_ingest_be(raw.as<uint8_t>(), width, count, mc.S, mc.W, n2x, X, stride, w->flags.as<uint32_t>(), st,
+                             rowflags));
   } else {
     // chunked: the pool fills pinned slot s while the DMA + k_ingest_be of slot s^1 run
     bool used[2] = {false, false};
@@ -508,7 +257,8 @@ int ingest(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint8_t
       uint8_t* d = raw.as<uint8_t>() + slot * crows * width;
       HIP_TRY(hipMemcpyAsync(d, w->hch[slot].p, bytes, hipMemcpyHostToDevice, st));
       HIP_TRY(hipEventRecord(w->ev_dec[slot], st));
-      HIP_TRY(launch_ingest_be(d, width, nrows, mc.S, mc.W, n2x, X + b, stride, w->flags.as<uint32_t>(), st));
+      HIP_TRY(launch_ingest_be(d, width, nrows, mc.S, mc.W, n2x, X + b, stride, w->flags.as<uint32_t>(), st,
+                               rowflags ? rowflags + b : nullptr));
       used[slot] = true;
     }
   }
@@ -516,23 +266,20 @@ int ingest(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint8_t
   HIP_TRY(hipMemcpyAsync(&flags, w->flags.p, 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   if (flags & 2u) return fail(DDS_E_RANGE, "operand wider than the modulus limb width");
-  if (flags & 1u) HIP_TRY(launch_reduce_rows(mc.S, X, stride, count, mc.d, mc.n0, st));
+  if (flags & 1u) {
+    HIP_TRY(launch_reduce_rows(mc.S, X, stride, count, mc.d, mc.n0, st));
+    if (reduced) {
+      std::vector<uint8_t> f(count);
+      HIP_TRY(hipMemcpyAsync(f.data(), rowflags, count, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      for (size_t i = 0; i < count; ++i)
+        if (f[i]) reduced->push_back(i);
+    }
+  }
   return DDS_OK;
 }
 
-// ---- decimal codec (BigInteger.toString rows) ---------------------------------------------
-// The rows arrive either Arrow-style (chars + offsets[count+1]) or as NUL-terminated strings
-// (the JNA String[] of the route bodies, DDSRestServer.scala:417,419,422,513).
-struct DecRows {
-  const char* chars = nullptr;
-  const uint64_t* offs = nullptr;
-  const char* const* strs = nullptr;
-  size_t len(size_t i) const { return strs ? strlen(strs[i]) : (size_t)(offs[i + 1] - offs[i]); }
-  const char* row(size_t i) const { return strs ? strs[i] : chars + offs[i]; }
-};
 
-constexpr size_t kDecChunkBytes = (size_t)64 << 20;  // chars per pinned chunk
-constexpr size_t kDecChunkRows = (size_t)1 << 18;
 
 int dec_table(ModConsts& mc) {
   std::lock_guard<std::mutex> lk(mc.decmu);
@@ -674,7 +421,272 @@ int dec_rows_with(Worker* w, hipStream_t st, size_t count, uint32_t mask, std::v
   return DDS_OK;
 }
 
-}  // namespace
+int modmul_fold_be(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, size_t min_bits, const uint8_t* ops,
+                   size_t width, size_t count, uint8_t* out, size_t out_cap, size_t* out_len) {
+  std::shared_ptr<ModConsts> mc;
+  int rc = get_mod(ctx, mod_be, mod_bytes, &mc, min_bits);
+  if (rc) return rc;
+  if ((rc = check_rows(*mc, count))) return rc;
+  WorkerLease wl(ctx);
+  if ((rc = wl.acquire())) return rc;
+  Worker* w = wl.w;
+  const size_t stride = round_up(count, 64);
+  HIP_TRY(w->x.ensure((size_t)mc->S * stride * 4));
+  if ((rc = ingest(ctx, w, wl.st, *mc, ops, width, count, w->in, w->x.as<uint32_t>(), stride))) return rc;
+  const uint32_t* part;
+  size_t ps;
+  int64_t E;
+  if ((rc = fold_partial_device(ctx, w, wl.st, *mc, w->x.as<uint32_t>(), stride, count, &part, &ps, &E))) return rc;
+  std::vector<uint32_t> res;
+  if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, E, &res))) return rc;
+  return emit_be(mc->value2(res.data()), mod_bytes, out, out_cap, out_len);
+}
+
+// Product of `count` rows of radix-2^16 limbs (h: count x len u32 words, row-major) on the GPU product
+// tree (k_bigmul_*: one level multiplies row pairs, carry passes until every limb is < 2^16).
+// cap16 != 0: each level keeps only its low cap16 limbs, i.e. the product mod 2^(16 cap16).
+int product_tree(dds_ctx* ctx, const std::vector<uint32_t>& h, size_t count, size_t len, size_t cap16, bn::Limbs* out) {
+  WorkerLease wl(ctx);
+  int rc;
+  if ((rc = wl.acquire())) return rc;
+  Worker* w = wl.w;
+  HIP_TRY(w->x.ensure(h.size() * 4));
+  HIP_TRY(hipMemcpyAsync(w->x.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, wl.st));
+  HIP_TRY(w->flags.ensure(16));
+  uint32_t* cur = w->x.as<uint32_t>();
+  size_t n = count;
+  while (n > 1) {  // one tree level: n rows of len limbs -> ceil(n/2) rows of outlen limbs
+    const size_t pairs = (n + 1) / 2, outlen = cap16 ? std::min(2 * len, cap16) : 2 * len;
+    HIP_TRY(w->misc.ensure(pairs * outlen * 8));
+    HIP_TRY(w->x2.ensure(pairs * outlen * 4));
+    HIP_TRY(w->p0.ensure(pairs * outlen * 4));
+    HIP_TRY(launch_bigmul_level(cur, n, len, w->misc.as<uint64_t>(), w->x2.as<uint32_t>(), wl.st, cap16));
+    uint32_t* v = w->x2.as<uint32_t>();
+    uint32_t* u = w->p0.as<uint32_t>();
+    for (;;) {  // carry passes until every limb is < 2^16 (ripples are rare and short)
+      HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, wl.st));
+      HIP_TRY(launch_bigmul_carry(v, pairs, outlen, u, w->flags.as<uint32_t>(), wl.st));
+      uint32_t flag = 0;
+      HIP_TRY(hipMemcpyAsync(&flag, w->flags.p, 4, hipMemcpyDeviceToHost, wl.st));
+      HIP_TRY(hipStreamSynchronize(wl.st));
+      std::swap(u, v);
+      if (!flag) break;
+    }
+    // v holds the normalised level; move it to the level buffer
+    HIP_TRY(w->x.ensure(pairs * outlen * 4));
+    HIP_TRY(hipMemcpyAsync(w->x.p, v, pairs * outlen * 4, hipMemcpyDeviceToDevice, wl.st));
+    cur = w->x.as<uint32_t>();
+    n = pairs;
+    len = outlen;
+  }
+  std::vector<uint32_t> res(len);
+  HIP_TRY(hipMemcpyAsync(res.data(), cur, len * 4, hipMemcpyDeviceToHost, wl.st));
+  HIP_TRY(hipStreamSynchronize(wl.st));
+  bn::Limbs v((len + 1) / 2, 0);
+  for (size_t i = 0; i < len; ++i) v[i / 2] |= res[i] << (16 * (i % 2));
+  bn::trim(v);
+  *out = std::move(v);
+  return DDS_OK;
+}
+
+// x mod 2^t
+bn::Limbs low_bits(const bn::Limbs& x, size_t t) {
+  bn::Limbs r(x.begin(), x.begin() + std::min(x.size(), (t + 31) / 32));
+  if (t % 32 && r.size() == (t + 31) / 32) r.back() &= (1u << (t % 32)) - 1u;
+  bn::trim(r);
+  return r;
+}
+
+// Product of magnitudes xs[i] (signs negs[i]) mod an EVEN modulus M (or M == 1), count >= 2. A
+// Montgomery fold needs an odd modulus, so M = 2^t * Q (Q odd) is split: prod mod Q by the
+// Montgomery fold (in the shape of M's width, so operands as wide as M's capacity fit), prod mod 2^t
+// by the truncated product tree, both on the GPU; then CRT and the sign (-1)^#neg on the host —
+// BigInteger.mod semantics (DDSRestServer.scala:422-423, 515-518 send any modulus).
+int fold_even_modulus(dds_ctx* ctx, const bn::Limbs& M, const std::vector<bn::Limbs>& xs, const std::vector<bool>& negs,
+                      bn::Limbs* out) {
+  const size_t count = xs.size();
+  size_t t = 0;
+  while (!((M[t / 32] >> (t % 32)) & 1u)) ++t;
+  bn::Limbs Q = M;
+  for (size_t i = 0; i < t; ++i) (void)bn::divmod_small(Q, 2);
+  bn::trim(Q);
+  const size_t mbits = bn::bit_length(M);
+  // rows wider than M's limb capacity: pre-reduce mod M (consistent mod Q and mod 2^t)
+  const Shape sh = pick_shape(mbits);
+  if (!sh.S) return fail(DDS_E_UNSUPPORTED, "modulus too large");
+  const size_t capbits = (size_t)sh.W * sh.S - 2;
+  std::vector<bn::Limbs> ys(xs);
+  size_t width = 1;
+  for (auto& y : ys) {
+    if (bn::bit_length(y) > capbits) y = bn::mod(y, M);
+    width = std::max(width, bn::byte_length(y));
+  }
+  bn::Limbs rq;  // prod mod Q
+  if (bn::bit_length(Q) >= 2) {
+    std::vector<uint8_t> rows(count * width), qbe(bn::byte_length(Q));
+    for (size_t i = 0; i < count; ++i) bn::to_be(ys[i], rows.data() + i * width, width);
+    bn::to_be(Q, qbe.data(), qbe.size());
+    std::vector<uint8_t> r(qbe.size());
+    size_t rl = 0;
+    int rc = modmul_fold_be(ctx, qbe.data(), qbe.size(), mbits, rows.data(), width, count, r.data(), r.size(), &rl);
+    if (rc) return rc;
+    rq = bn::from_be(r.data(), rl);
+  }
+  bn::Limbs r2;  // prod mod 2^t
+  if (t > 0) {
+    const size_t cap16 = (t + 15) / 16;
+    std::vector<uint32_t> h(count * cap16, 0);
+    for (size_t i = 0; i < count; ++i) {
+      const bn::Limbs lo = low_bits(ys[i], t);
+      for (size_t k = 0; k < lo.size() && 2 * k < cap16; ++k) {
+        h[i * cap16 + 2 * k] = lo[k] & 0xFFFFu;
+        if (2 * k + 1 < cap16) h[i * cap16 + 2 * k + 1] = lo[k] >> 16;
+      }
+    }
+    int rc = product_tree(ctx, h, count, cap16, cap16, &r2);
+    if (rc) return rc;
+    r2 = low_bits(r2, t);
+  }
+  // CRT: r = rq + Q * ((r2 - rq) * Q^-1 mod 2^t)
+  bn::Limbs r = rq;
+  if (t > 0) {
+    const bn::Limbs two_t = bn::pow2(t);
+    bn::Limbs qinv{1};  // Newton: qinv <- qinv (2 - Q qinv) mod 2^t, doubling the correct bits
+    for (size_t bits = 1; bits < t; bits *= 2) {
+      const bn::Limbs qq = low_bits(bn::mul(Q, qinv), t);
+      qinv = low_bits(bn::mul(qinv, bn::sub(bn::add(two_t, bn::Limbs{2}), qq)), t);
+    }
+    const bn::Limbs rqt = low_bits(rq, t);
+    const bn::Limbs d = bn::cmp(r2, rqt) >= 0 ? bn::sub(r2, rqt) : bn::sub(bn::add(r2, two_t), rqt);
+    r = bn::add(rq, bn::mul(Q, low_bits(bn::mul(d, qinv), t)));
+  }
+  size_t nneg = 0;
+  for (bool b : negs) nneg += b;
+  bn::trim(r);
+  if ((nneg & 1) && !r.empty()) r = bn::sub(M, r);
+  *out = r;
+  return DDS_OK;
+}
+
+// Combine partials (dds_col_fold_partial layout: S2 limbs + exponent, back to back) given in host
+// memory (h_parts) or device memory of ctx's GPU (d_parts): validate them, one more tree, finalize.
+int combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint32_t* h_parts,
+                     const uint32_t* d_parts, const uint64_t* rows, size_t nparts, uint8_t* out, size_t out_cap,
+                     size_t* out_len) {
+  std::shared_ptr<ModConsts> mc;
+  int rc = get_mod(ctx, mod_be, mod_bytes, &mc);
+  if (rc) return rc;
+  uint64_t k = 0;
+  for (size_t i = 0; i < nparts; ++i) k += rows[i];
+  if (k == 0) return fail(DDS_E_EMPTY, "no operand");
+  const size_t S2 = (size_t)mc->S2, pw = partial_words_for(*mc);
+  WorkerLease wl(ctx);
+  if ((rc = wl.acquire())) return rc;
+  Worker* w = wl.w;
+  std::vector<uint32_t> hp;
+  if (d_parts) {  // limbs + exponents are a few hundred bytes per partial: read them back to check
+    hp.resize(nparts * pw);
+    HIP_TRY(hipMemcpyAsync(hp.data(), d_parts, hp.size() * 4, hipMemcpyDeviceToHost, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    h_parts = hp.data();
+  }
+  // the tree kernels' lazy-accumulation bound needs fully normalised limbs and a value below the
+  // bound the fold leaves its partials under (2N~ when a QP shape is used, else 2N): reject the rest
+  const bn::Limbs bound = bn::add(mc->qbound, mc->qbound);
+  int64_t E = -mc->wS2() * ((int64_t)nparts - 1);  // the tree below multiplies by R2^-(n-1)
+  for (size_t i = 0; i < nparts; ++i) {
+    const uint32_t* pl = h_parts + i * pw;
+    for (size_t l = 0; l < S2; ++l)
+      if (pl[l] >> mc->W) return fail(DDS_E_RANGE, "partial " + std::to_string(i) + ": limb not normalised");
+    if (bn::cmp(mc->value2(pl), bound) >= 0) return fail(DDS_E_RANGE, "partial " + std::to_string(i) + " out of range");
+    E += (int64_t)((uint64_t)pl[S2] | ((uint64_t)pl[S2 + 1] << 32));
+  }
+  const size_t stride = round_up(nparts, 64);
+  HIP_TRY(w->x.ensure(S2 * stride * 4));
+  HIP_TRY(w->p0.ensure(S2 * stride * 4));
+  HIP_TRY(w->p1.ensure(S2 * stride * 4));
+  std::vector<uint32_t> h;
+  if (d_parts) {
+    HIP_TRY(launch_strided_copy(d_parts, pw, 1, w->x.as<uint32_t>(), 1, stride, nparts, S2, wl.st));
+  } else {
+    h.assign(S2 * stride, 0);
+    for (size_t i = 0; i < nparts; ++i)
+      for (size_t l = 0; l < S2; ++l) h[l * stride + i] = h_parts[i * pw + l];
+    HIP_TRY(hipMemcpyAsync(w->x.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, wl.st));
+  }
+  const uint32_t* cur = w->x.as<uint32_t>();
+  size_t n = nparts, cs = stride;
+  uint32_t* bufs[2] = {w->p0.as<uint32_t>(), w->p1.as<uint32_t>()};
+  int flip = 0;
+  while (n > 1) {
+    size_t ng = (n + 1) / 2, ns = round_up(ng, 64);
+    HIP_TRY(launch_fold_tail(mc->S2, cur, cs, n, mc->d2, mc->dq, mc->n0, bufs[flip], ns, ng, wl.st));
+    cur = bufs[flip];
+    flip ^= 1;
+    n = ng;
+    cs = ns;
+  }
+  std::vector<uint32_t> res;
+  if ((rc = finalize_device(ctx, w, wl.st, *mc, cur, cs, E, &res))) return rc;  // syncs: h may go
+  return emit_be(mc->value2(res.data()), mod_bytes, out, out_cap, out_len);
+}
+
+// SumAll/MultAll over rows of a resident column (DDSRestServer.scala:412-430, 506-524): rows
+// row_ids[0..n) (nullptr: rows [first, first+n)). n == 0 -> DDS_E_EMPTY (404); n == 1 -> the operand
+// as appended, unreduced (:416-417); else the canonical product mod N.
+int col_fold_value(dds_col* col, const uint64_t* row_ids, size_t first, size_t n, bn::Limbs* v, bool* neg) {
+  *neg = false;
+  if (n == 0) return fail(DDS_E_EMPTY, "no operand");
+  ModConsts& mc = *col->mc;
+  const size_t rows = col->count;
+  if (row_ids) {
+    for (size_t i = 0; i < n; ++i)
+      if (row_ids[i] >= rows) return fail(DDS_E_ARG, "row id " + std::to_string(row_ids[i]) + " out of range");
+  } else if (first + n > rows) {
+    return fail(DDS_E_ARG, "rows out of range");
+  }
+  if (n == 1) {
+    const size_t r = row_ids ? (size_t)row_ids[0] : first;
+    {
+      std::lock_guard<std::mutex> lk(col->mu);
+      auto it = col->orig.find(r);
+      if (it != col->orig.end()) {
+        *v = it->second.mag;
+        *neg = it->second.neg;
+        return DDS_OK;
+      }
+    }
+    std::vector<uint32_t> h((size_t)mc.S);  // stored verbatim (< 2N): the raw limbs
+    HIP_TRY(hipMemcpy2D(h.data(), 4, col->d + r, col->stride * 4, 4, (size_t)mc.S, hipMemcpyDeviceToHost));
+    *v = mc.value(h.data());
+    return DDS_OK;
+  }
+  WorkerLease wl(col->ctx);
+  int rc;
+  if ((rc = wl.acquire())) return rc;
+  Worker* w = wl.w;
+  std::vector<uint32_t> ids32;
+  const uint32_t* d_ids = nullptr;
+  if (row_ids) {
+    ids32.assign(row_ids, row_ids + n);  // < count <= max_stride < 2^32
+    HIP_TRY(w->ids.ensure(n * 4));
+    HIP_TRY(hipMemcpyAsync(w->ids.p, ids32.data(), n * 4, hipMemcpyHostToDevice, wl.st));
+    d_ids = w->ids.as<uint32_t>();
+  }
+  const uint32_t* part;
+  size_t ps;
+  int64_t E;
+  if ((rc = fold_partial_device(col->ctx, w, wl.st, mc, col->d + (row_ids ? 0 : first), col->stride, n, &part, &ps,
+                                &E, d_ids)))
+    return rc;
+  std::vector<uint32_t> res;
+  if ((rc = finalize_device(col->ctx, w, wl.st, mc, part, ps, E, &res))) return rc;  // syncs: ids32 may go
+  *v = mc.value2(res.data());
+  return DDS_OK;
+}
+
+}  // namespace host
+}  // namespace ddshe
 
 // =============================================================================
 extern "C" {
@@ -778,22 +790,18 @@ int dds_modmul_fold(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const
       memcpy(out, ops, width);
       return DDS_OK;
     }
-    std::shared_ptr<ModConsts> mc;
-    int rc = get_mod(ctx, mod_be, mod_bytes, &mc);
-    if (rc) return rc;
-    WorkerLease wl(ctx);
-    if ((rc = wl.acquire())) return rc;
-    Worker* w = wl.w;
-    const size_t stride = round_up(count, 64);
-    HIP_TRY(w->x.ensure((size_t)mc->S * stride * 4));
-    if ((rc = ingest(ctx, w, wl.st, *mc, ops, width, count, w->in, w->x.as<uint32_t>(), stride))) return rc;
-    const uint32_t* part;
-    size_t ps;
-    int64_t E;
-    if ((rc = fold_partial_device(ctx, w, wl.st, *mc, w->x.as<uint32_t>(), stride, count, &part, &ps, &E))) return rc;
-    std::vector<uint32_t> res;
-    if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, E, &res))) return rc;
-    return emit_be(mc->value2(res.data()), mod_bytes, out, out_cap, out_len);
+    if (!mod_be || mod_bytes == 0) return fail(DDS_E_ARG, "modulus missing");
+    const bn::Limbs M = bn::from_be(mod_be, mod_bytes);
+    if (M.empty()) return fail(DDS_E_ARG, "modulus must be positive (BigInteger.mod)");
+    if (!(M[0] & 1u) || bn::bit_length(M) < 2) {  // even modulus or 1: CRT split (fold_even_modulus)
+      std::vector<bn::Limbs> xs(count);
+      for (size_t i = 0; i < count; ++i) xs[i] = bn::from_be(ops + i * width, width);
+      bn::Limbs r;
+      int rc = fold_even_modulus(ctx, M, xs, std::vector<bool>(count, false), &r);
+      if (rc) return rc;
+      return emit_be(r, mod_bytes, out, out_cap, out_len);
+    }
+    return modmul_fold_be(ctx, mod_be, mod_bytes, 0, ops, width, count, out, out_cap, out_len);
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");
   } catch (...) {
@@ -819,6 +827,7 @@ int dds_modmul_pairs(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, cons
     std::shared_ptr<ModConsts> mc;
     int rc = get_mod(ctx, mod_be, mod_bytes, &mc);
     if (rc) return rc;
+    if ((rc = check_rows(*mc, n))) return rc;
     WorkerLease wl(ctx);
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
@@ -902,10 +911,6 @@ int dds_bigint_product(dds_ctx* ctx, const uint8_t* ops, size_t width, size_t co
   try {
     if (!ctx || width == 0 || (count && !ops)) return fail(DDS_E_ARG, "bad arguments");
     if (count == 0) return fail(DDS_E_EMPTY, "no operand");
-    WorkerLease wl(ctx);
-    int rc;
-    if ((rc = wl.acquire())) return rc;
-    Worker* w = wl.w;
     // boundary format: big-endian bytes -> radix-2^16 limbs (one per u32 word), row-major
     size_t len = (width + 1) / 2;
     std::vector<uint32_t> h(count * len, 0);
@@ -914,41 +919,9 @@ int dds_bigint_product(dds_ctx* ctx, const uint8_t* ops, size_t width, size_t co
         const size_t bit = 8 * (width - 1 - i);
         h[r * len + bit / 16] |= (uint32_t)ops[r * width + i] << (bit % 16);
       }
-    HIP_TRY(w->x.ensure(h.size() * 4));
-    HIP_TRY(hipMemcpyAsync(w->x.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, wl.st));
-    HIP_TRY(w->flags.ensure(16));
-    uint32_t* cur = w->x.as<uint32_t>();
-    size_t n = count;
-    while (n > 1) {  // one tree level: n rows of len limbs -> ceil(n/2) rows of 2 len limbs
-      const size_t pairs = (n + 1) / 2, outlen = 2 * len;
-      HIP_TRY(w->misc.ensure(pairs * outlen * 8));
-      HIP_TRY(w->x2.ensure(pairs * outlen * 4));
-      HIP_TRY(w->p0.ensure(pairs * outlen * 4));
-      HIP_TRY(launch_bigmul_level(cur, n, len, w->misc.as<uint64_t>(), w->x2.as<uint32_t>(), wl.st));
-      uint32_t* v = w->x2.as<uint32_t>();
-      uint32_t* u = w->p0.as<uint32_t>();
-      for (;;) {  // carry passes until every limb is < 2^16 (ripples are rare and short)
-        HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, wl.st));
-        HIP_TRY(launch_bigmul_carry(v, pairs, outlen, u, w->flags.as<uint32_t>(), wl.st));
-        uint32_t flag = 0;
-        HIP_TRY(hipMemcpyAsync(&flag, w->flags.p, 4, hipMemcpyDeviceToHost, wl.st));
-        HIP_TRY(hipStreamSynchronize(wl.st));
-        std::swap(u, v);
-        if (!flag) break;
-      }
-      // v holds the normalised level; move it to the level buffer
-      HIP_TRY(w->x.ensure(pairs * outlen * 4));
-      HIP_TRY(hipMemcpyAsync(w->x.p, v, pairs * outlen * 4, hipMemcpyDeviceToDevice, wl.st));
-      cur = w->x.as<uint32_t>();
-      n = pairs;
-      len = outlen;
-    }
-    std::vector<uint32_t> res(len);
-    HIP_TRY(hipMemcpyAsync(res.data(), cur, len * 4, hipMemcpyDeviceToHost, wl.st));
-    HIP_TRY(hipStreamSynchronize(wl.st));
-    bn::Limbs v((len + 1) / 2, 0);
-    for (size_t i = 0; i < len; ++i) v[i / 2] |= res[i] << (16 * (i % 2));
-    bn::trim(v);
+    bn::Limbs v;
+    int rc = product_tree(ctx, h, count, len, 0, &v);
+    if (rc) return rc;
     return emit_be(v, std::max<size_t>(1, bn::byte_length(v)), out, out_cap, out_len);
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");
@@ -963,6 +936,7 @@ int dds_col_create(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, size_t
     std::shared_ptr<ModConsts> mc;
     int rc = get_mod(ctx, mod_be, mod_bytes, &mc);
     if (rc) return rc;
+    if ((rc = check_rows(*mc, capacity))) return rc;
     auto* c = new dds_col();
     c->ctx = ctx;
     c->mc = mc;
@@ -991,6 +965,7 @@ int dds_col_truncate(dds_col* col, size_t count) {
   std::lock_guard<std::mutex> lk(col->mu);
   if (count > col->count) return fail(DDS_E_ARG, "truncate beyond the row count");
   col->count = count;
+  col->orig.erase(col->orig.lower_bound(count), col->orig.end());
   return DDS_OK;
 }
 
@@ -1006,9 +981,12 @@ int dds_col_append(dds_col* col, const uint8_t* ops, size_t width, size_t count)
     int rc;
     if ((rc = wl.acquire())) return rc;
     // ingest writes with the column's stride starting at row `count`
-    if ((rc = ingest(col->ctx, wl.w, wl.st, *col->mc, ops, width, count, wl.w->in, col->d + col->count, col->stride)))
+    std::vector<size_t> reduced;
+    if ((rc = ingest(col->ctx, wl.w, wl.st, *col->mc, ops, width, count, wl.w->in, col->d + col->count, col->stride,
+                     &reduced)))
       return rc;
     HIP_TRY(hipStreamSynchronize(wl.st));
+    for (size_t i : reduced) col->orig[col->count + i] = dds_col::Orig{bn::from_be(ops + i * width, width), false};
     col->count += count;
     return DDS_OK;
   } catch (const std::bad_alloc&) {
@@ -1041,7 +1019,16 @@ int dds_col_append_dec(dds_col* col, const char* chars, const uint64_t* offsets,
       return fail(DDS_E_RANGE, "decimal row wider than the column limb capacity");
     }
     if (!longr.empty()) return fail(DDS_E_RANGE, "decimal row wider than the column limb capacity");
+    std::vector<size_t> changed;
+    if (fl & (kDecNeg | kDecReduce))
+      if ((rc = dec_rows_with(wl.w, wl.st, count, kDecNeg | kDecReduce, &changed))) return rc;
     HIP_TRY(hipStreamSynchronize(wl.st));
+    for (size_t i : changed) {
+      dds_col::Orig o;
+      if (!bn::from_dec(chars + offsets[i], (size_t)(offsets[i + 1] - offsets[i]), o.mag, &o.neg))
+        return fail(DDS_E_FORMAT, "row " + std::to_string(i) + ": NumberFormatException");
+      col->orig[col->count + i] = std::move(o);
+    }
     col->count += count;
     return DDS_OK;
   } catch (const std::bad_alloc&) {
@@ -1104,28 +1091,44 @@ int dds_col_fold_partial(dds_col* col, size_t first, size_t count, uint32_t* par
 int dds_col_fold(dds_col* col, size_t first, size_t count, uint8_t* out, size_t out_cap, size_t* out_len) {
   try {
     if (!col || first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
-    if (count == 0) return fail(DDS_E_EMPTY, "no operand");
-    ModConsts& mc = *col->mc;
-    if (count == 1) {
-      std::vector<uint8_t> tmp(mc.bytes);
-      int rc = dds_col_read(col, first, 1, tmp.data());
-      if (rc) return rc;
-      if (out_len) *out_len = mc.bytes;
-      if (!out || out_cap < mc.bytes) return fail(DDS_E_BUFSIZE, "output buffer too small");
-      memcpy(out, tmp.data(), mc.bytes);
-      return DDS_OK;
-    }
-    WorkerLease wl(col->ctx);
-    int rc;
-    if ((rc = wl.acquire())) return rc;
-    const uint32_t* part;
-    size_t ps;
-    int64_t E;
-    if ((rc = fold_partial_device(col->ctx, wl.w, wl.st, mc, col->d + first, col->stride, count, &part, &ps, &E)))
-      return rc;
-    std::vector<uint32_t> res;
-    if ((rc = finalize_device(col->ctx, wl.w, wl.st, mc, part, ps, E, &res))) return rc;
-    return emit_be(mc.value2(res.data()), mc.bytes, out, out_cap, out_len);
+    bn::Limbs v;
+    bool neg = false;
+    int rc = col_fold_value(col, nullptr, first, count, &v, &neg);
+    if (rc) return rc;
+    if (neg) return fail(DDS_E_RANGE, "the single operand is negative: use dds_col_fold_dec");
+    return emit_be(v, std::max(col->mc->bytes, bn::byte_length(v)), out, out_cap, out_len);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_col_fold_rows(dds_col* col, const uint64_t* row_ids, size_t n, uint8_t* out, size_t out_cap,
+                      size_t* out_len) {
+  try {
+    if (!col || (n && !row_ids)) return fail(DDS_E_ARG, "bad arguments");
+    bn::Limbs v;
+    bool neg = false;
+    int rc = col_fold_value(col, row_ids, 0, n, &v, &neg);
+    if (rc) return rc;
+    if (neg) return fail(DDS_E_RANGE, "the single operand is negative: use dds_col_fold_dec");
+    return emit_be(v, std::max(col->mc->bytes, bn::byte_length(v)), out, out_cap, out_len);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_col_fold_dec(dds_col* col, const uint64_t* row_ids, size_t n, char* out, size_t out_cap, size_t* out_len) {
+  try {
+    if (!col || (!row_ids && n > col->count)) return fail(DDS_E_ARG, "bad arguments");
+    bn::Limbs v;
+    bool neg = false;
+    int rc = col_fold_value(col, row_ids, 0, n, &v, &neg);
+    if (rc) return rc;
+    const std::string t = bn::to_dec(v, neg);
+    if (out_len) *out_len = t.size();
+    if (!out || out_cap < t.size() + 1) return fail(DDS_E_BUFSIZE, "output buffer too small");
+    memcpy(out, t.c_str(), t.size() + 1);
+    return DDS_OK;
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");
   }
@@ -1135,43 +1138,47 @@ int dds_combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, 
                          const uint64_t* rows, size_t nparts, uint8_t* out, size_t out_cap, size_t* out_len) {
   try {
     if (!ctx || !partials || !rows || nparts == 0) return fail(DDS_E_ARG, "bad arguments");
-    std::shared_ptr<ModConsts> mc;
-    int rc = get_mod(ctx, mod_be, mod_bytes, &mc);
-    if (rc) return rc;
-    uint64_t k = 0;
-    for (size_t i = 0; i < nparts; ++i) k += rows[i];
-    if (k == 0) return fail(DDS_E_EMPTY, "no operand");
-    const size_t S2 = (size_t)mc->S2, pw = partial_words_for(*mc);
-    WorkerLease wl(ctx);
+    return combine_partials(ctx, mod_be, mod_bytes, partials, nullptr, rows, nparts, out, out_cap, out_len);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_combine_partials_device(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint32_t* d_partials,
+                                const uint64_t* rows, size_t nparts, uint8_t* out, size_t out_cap, size_t* out_len) {
+  try {
+    if (!ctx || !d_partials || !rows || nparts == 0) return fail(DDS_E_ARG, "bad arguments");
+    return combine_partials(ctx, mod_be, mod_bytes, nullptr, d_partials, rows, nparts, out, out_cap, out_len);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_col_fold_partial_device(dds_col* col, size_t first, size_t count, uint32_t* d_partial) {
+  try {
+    if (!col || !d_partial || first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
+    ModConsts& mc = *col->mc;
+    const size_t S2 = (size_t)mc.S2;
+    WorkerLease wl(col->ctx);
+    int rc;
     if ((rc = wl.acquire())) return rc;
-    Worker* w = wl.w;
-    // the tree below multiplies by R2^-(n-1); each partial carries its own 2^E_i
-    int64_t E = -mc->wS2() * ((int64_t)nparts - 1);
-    const size_t stride = round_up(nparts, 64);
-    std::vector<uint32_t> h(S2 * stride, 0);
-    for (size_t i = 0; i < nparts; ++i) {
-      for (size_t l = 0; l < S2; ++l) h[l * stride + i] = partials[i * pw + l];
-      E += (int64_t)((uint64_t)partials[i * pw + S2] | ((uint64_t)partials[i * pw + S2 + 1] << 32));
+    int64_t E = 0;
+    if (count == 0) {  // empty partial: prod = 1, E = 0
+      HIP_TRY(hipMemsetAsync(d_partial, 0, S2 * 4, wl.st));
+      const uint32_t one = 1;
+      HIP_TRY(hipMemcpyAsync(d_partial, &one, 4, hipMemcpyHostToDevice, wl.st));
+    } else {
+      const uint32_t* part;
+      size_t ps;
+      if ((rc = fold_partial_device(col->ctx, wl.w, wl.st, mc, col->d + first, col->stride, count, &part, &ps, &E)))
+        return rc;
+      HIP_TRY(launch_strided_copy(part, 0, ps, d_partial, 0, 1, 1, S2, wl.st));
     }
-    HIP_TRY(w->x.ensure(h.size() * 4));
-    HIP_TRY(w->p0.ensure(h.size() * 4));
-    HIP_TRY(w->p1.ensure(h.size() * 4));
-    HIP_TRY(hipMemcpyAsync(w->x.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, wl.st));
-    const uint32_t* cur = w->x.as<uint32_t>();
-    size_t n = nparts, cs = stride;
-    uint32_t* bufs[2] = {w->p0.as<uint32_t>(), w->p1.as<uint32_t>()};
-    int flip = 0;
-    while (n > 1) {
-      size_t ng = (n + 1) / 2, ns = round_up(ng, 64);
-      HIP_TRY(launch_fold_tail(mc->S2, cur, cs, n, mc->d2, mc->dq, mc->n0, bufs[flip], ns, ng, wl.st));
-      cur = bufs[flip];
-      flip ^= 1;
-      n = ng;
-      cs = ns;
-    }
-    std::vector<uint32_t> res;
-    if ((rc = finalize_device(ctx, w, wl.st, *mc, cur, cs, E, &res))) return rc;
-    return emit_be(mc->value2(res.data()), mod_bytes, out, out_cap, out_len);
+    const uint32_t ew[2] = {(uint32_t)(uint64_t)E, (uint32_t)((uint64_t)E >> 32)};
+    HIP_TRY(hipMemcpyAsync(d_partial + S2, ew, 8, hipMemcpyHostToDevice, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    account_fold(col->ctx, wl.w);
+    return DDS_OK;
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");
   }
@@ -1384,6 +1391,7 @@ int dds_paillier_encrypt_batch(dds_ctx* ctx, const uint8_t* n_be, size_t n_bytes
     int rc = get_mod(ctx, nsq_be.data(), nsq_be.size(), &mc);
     if (rc) return rc;
     bn::Limbs g = bn::from_be(g_be, g_bytes);
+    if ((rc = check_rows(*mc, count))) return rc;
     WorkerLease wl(ctx);
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
@@ -1420,6 +1428,7 @@ int dds_modexp_batch(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, cons
     int rc = get_mod(ctx, mod_be, mod_bytes, &mc);
     if (rc) return rc;
     bn::Limbs e = bn::from_be(exp_be, exp_bytes);
+    if ((rc = check_rows(*mc, count))) return rc;
     WorkerLease wl(ctx);
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
@@ -1455,8 +1464,18 @@ static uint64_t splitmix64_host(uint64_t x) {
 
 int dds_col_fill_paillier_synth(dds_col* col, const uint8_t* n_be, size_t n_bytes, const uint8_t* g_be,
                                 size_t g_bytes, uint64_t seed, uint64_t row0, size_t count, uint32_t pool_size) {
+  return ddshe::host::col_fill_paillier_synth(col, n_be, n_bytes, g_be, g_bytes, seed, row0, count, pool_size, 1, 0);
+}
+
+}  // extern "C"
+
+namespace ddshe {
+namespace host {
+int col_fill_paillier_synth(dds_col* col, const uint8_t* n_be, size_t n_bytes, const uint8_t* g_be, size_t g_bytes,
+                            uint64_t seed, uint64_t row0, size_t count, uint32_t pool_size, uint32_t shards,
+                            uint32_t shard) {
   try {
-    if (!col || !n_be || !g_be || pool_size == 0) return fail(DDS_E_ARG, "bad arguments");
+    if (!col || !n_be || !g_be || pool_size == 0 || shards == 0 || shard >= shards) return fail(DDS_E_ARG, "bad arguments");
     std::lock_guard<std::mutex> lk(col->mu);
     if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
     ModConsts& mc = *col->mc;
@@ -1509,7 +1528,7 @@ int dds_col_fill_paillier_synth(dds_col* col, const uint8_t* n_be, size_t n_byte
     HIP_TRY(hipMemcpyAsync(w->x.p, rmod_col.data(), rmod_col.size() * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(launch_pairs(S, pool_plain, w->x.as<uint32_t>(), ps, pool_size, mc.d, mc.n0, pool_mont, st));
     HIP_TRY(launch_synth_rows(S, w->misc.as<uint32_t>(), ts, tcount, pool_mont, ps, pool_size, seed, row0, count, mc.d,
-                              mc.n0, col->d + col->count, col->stride, st));
+                              mc.n0, col->d + col->count, col->stride, st, shards, shard));
     HIP_TRY(hipStreamSynchronize(st));
     col->count += count;
     return DDS_OK;
@@ -1517,6 +1536,10 @@ int dds_col_fill_paillier_synth(dds_col* col, const uint8_t* n_be, size_t n_byte
     return fail(DDS_E_NOMEM, "host allocation");
   }
 }
+}  // namespace host
+}  // namespace ddshe
+
+extern "C" {
 
 int dds_paillier_encrypt_batch_crt(dds_ctx* ctx, const uint8_t* p_be, size_t p_bytes, const uint8_t* q_be,
                                    size_t q_bytes, const uint8_t* g_be, size_t g_bytes, const uint32_t* m,
@@ -1535,6 +1558,7 @@ int dds_paillier_encrypt_batch_crt(dds_ctx* ctx, const uint8_t* p_be, size_t p_b
       if (r.empty() || bn::cmp(r, k->n) >= 0) return fail(DDS_E_RANGE, "r must be in [1, n)");
     }
     const bn::Limbs g = bn::from_be(g_be, g_bytes);
+    if ((rc = check_rows(mn, count))) return rc;
     WorkerLease wl(ctx);
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
@@ -1961,12 +1985,22 @@ int fold_dec_mod(dds_ctx* ctx, const char* const* values, size_t count, const ch
   bool mneg = false;
   if (!bn::from_dec(mod_dec, strlen(mod_dec), M, &mneg) || mneg || M.empty())
     return fail(DDS_E_FORMAT, "modulus: NumberFormatException / non-positive");
+  if (!(M[0] & 1u) || bn::bit_length(M) < 2) {  // even modulus or 1 (BigInteger.mod accepts any m > 0)
+    std::vector<bn::Limbs> mags;
+    std::vector<bool> negs;
+    int rc = parse_values(values, count, &mags, &negs);
+    if (rc) return rc;
+    bn::Limbs r;
+    if ((rc = fold_even_modulus(ctx, M, mags, negs, &r))) return rc;
+    return write_dec(bn::to_dec(r), out, out_cap, out_len);
+  }
   const size_t mb = bn::byte_length(M);
   std::vector<uint8_t> mbe(mb);
   bn::to_be(M, mbe.data(), mb);
   std::shared_ptr<ModConsts> mc;
   int rc = get_mod(ctx, mbe.data(), mb, &mc);
   if (rc) return rc;
+  if ((rc = check_rows(*mc, count))) return rc;
   WorkerLease wl(ctx);
   if ((rc = wl.acquire())) return rc;
   Worker* w = wl.w;

@@ -84,25 +84,32 @@ struct Grp {
 // A group that folded c rows holds prod * R^(1-c). Requires 1 <= ngroups <= count (no empty
 // group: the launcher checks), which keeps the kernel body to load, MonPro loop, store.
 // ------------------------------------------------------------------------------
-template <int S, int TPI, int W, bool QP = false>
+// Idx: the fold runs over the rows ids[0..count) of X instead of rows [0, count) (row-subset folds:
+// the rows that pass a route's guard / dedup, DDSRestServer.scala:401-415). Sorted ids keep the
+// lanes of a wave on nearby rows, so the limb loads stay mostly coalesced.
+template <int S, int TPI, int W, bool QP = false, bool Idx = false>
 __global__ void __launch_bounds__(256, 2) k_fold(const uint32_t* __restrict__ X, size_t xstride, size_t count,
                                               const uint32_t* __restrict__ consts, uint32_t n0,
-                                              uint32_t* __restrict__ P, size_t pstride, size_t ngroups) {
+                                              uint32_t* __restrict__ P, size_t pstride, size_t ngroups,
+                                              const uint32_t* __restrict__ ids = nullptr) {
   using G = Grp<S, TPI, W>;
   using M = Mont<S, TPI, W, QP>;
   constexpr int L = G::L;
   G g;
   const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
   if (grp >= ngroups) return;
+  auto rowat = [&](size_t pos) -> uint32_t { return Idx ? ids[pos] : (uint32_t)pos; };
   uint32_t n[L], a[L];
   g.load_vec(n, consts + kConstN * S);
-  g.load_col(a, X, xstride, grp);
+  g.load_col(a, X, xstride, rowat(grp));
   if (grp + ngroups < count) {
     uint32_t pre[2][M::kPF];  // first limb blocks of the next row, requested one row ahead
-    M::load_blocks2(pre, X, xstride, (uint32_t)(grp + ngroups));
-    for (size_t row = grp + ngroups; row < count; row += ngroups) {
-      const size_t nxt = row + ngroups < count ? row + ngroups : row;  // last row: a harmless re-read
-      M::mul_col_chain(a, n, X, xstride, (uint32_t)row, (uint32_t)nxt, pre, n0, g.top, g.bottom);
+    uint32_t row = rowat(grp + ngroups);
+    M::load_blocks2(pre, X, xstride, row);
+    for (size_t pos = grp + ngroups; pos < count; pos += ngroups) {
+      const uint32_t nxt = pos + ngroups < count ? rowat(pos + ngroups) : row;  // last row: a harmless re-read
+      M::mul_col_chain(a, n, X, xstride, row, nxt, pre, n0, g.top, g.bottom);
+      row = nxt;
     }
   }
   M::normalize(a, g.bottom);

@@ -14,6 +14,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "ddshe_device.hpp"
 #include "ddshe_fold.hpp"
 #include "ddshe_launch.hpp"
@@ -24,11 +26,14 @@ namespace ddshe {
 // ------------------------------------------------------------------------------
 // ingest: big-endian fixed-width rows -> rW column (+ range classification)
 // ------------------------------------------------------------------------------
-// flags[0] |= 1 if some row is >= 2N (needs k_reduce_rows), flags[0] |= 2 if some
-// row does not fit in S rW limbs (boundary error DDS_E_RANGE).
+// flags[0] |= 1 if some row is >= 2N (needs k_reduce_rows), flags[0] |= 2 if some row does not fit
+// in S rW limbs (boundary error DDS_E_RANGE). rowflags (nullable): per row, 1 if it is >= 2N (it is
+// stored as its residue, so the column remembers which rows differ from what the caller passed).
+// One thread per row, least-significant end first; rows of a multiple of 4 bytes at 4-byte
+// alignment are read as big-endian dwords (a 4096-bit row: 128 loads instead of 512).
 __global__ void k_ingest_be(const uint8_t* __restrict__ in, size_t width, size_t count, int S, int W,
                             const uint32_t* __restrict__ n2x /* 2N in rW, S+1 limbs */, uint32_t* __restrict__ X,
-                            size_t stride, uint32_t* __restrict__ flags) {
+                            size_t stride, uint32_t* __restrict__ flags, uint8_t* __restrict__ rowflags) {
   const size_t row = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= count) return;
   const uint8_t* p = in + row * width;
@@ -36,39 +41,53 @@ __global__ void k_ingest_be(const uint8_t* __restrict__ in, size_t width, size_t
   int nbits = 0, l = 0, cmpv = 0;
   bool overflow = false;
   const uint32_t kMask = (1u << W) - 1u;
-  for (size_t i = 0; i < width; ++i) {
-    bitbuf |= (uint64_t)p[width - 1 - i] << nbits;
-    nbits += 8;
+  auto emit = [&]() {
     while (nbits >= W) {
-      uint32_t limb = (uint32_t)bitbuf & kMask;
+      const uint32_t limb = (uint32_t)bitbuf & kMask;
       bitbuf >>= W;
       nbits -= W;
       if (l < S) {
         X[(size_t)l * stride + row] = limb;
-        uint32_t nl = n2x[l];
+        const uint32_t nl = n2x[l];
         cmpv = limb > nl ? 1 : (limb < nl ? -1 : cmpv);
       } else if (limb) {
         overflow = true;
       }
       ++l;
     }
+  };
+  const bool words = (width % 4 == 0) && (((uintptr_t)in) % 4 == 0);
+  if (words) {
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(p);
+    for (size_t i = width / 4; i-- > 0;) {
+      bitbuf |= (uint64_t)__builtin_bswap32(pw[i]) << nbits;  // nbits < W <= 28: fits 64 bits
+      nbits += 32;
+      emit();
+    }
+  } else {
+    for (size_t i = 0; i < width; ++i) {
+      bitbuf |= (uint64_t)p[width - 1 - i] << nbits;
+      nbits += 8;
+      emit();
+    }
   }
   while (l < S || bitbuf != 0) {  // flush: zero-pad to S limbs, any leftover bit beyond S overflows
-    uint32_t limb = (uint32_t)bitbuf & kMask;
+    const uint32_t limb = (uint32_t)bitbuf & kMask;
     bitbuf >>= W;
     if (l < S) {
       X[(size_t)l * stride + row] = limb;
-      uint32_t nl = n2x[l];
+      const uint32_t nl = n2x[l];
       cmpv = limb > nl ? 1 : (limb < nl ? -1 : cmpv);
     } else if (limb) {
       overflow = true;
     }
     ++l;
   }
-  // 2N may need limb S (if 2N >= 2^(27S)); row limbs beyond S are zero here
+  // 2N may need limb S (if 2N >= 2^(W*S)); row limbs beyond S are zero here
   if (n2x[S] != 0) cmpv = -1;
   if (overflow) atomicOr(flags, 2u);
   else if (cmpv >= 0) atomicOr(flags, 1u);
+  if (rowflags) rowflags[row] = (!overflow && cmpv >= 0) ? 1 : 0;
 }
 
 // rows >= 2N: x <- MonPro(MonPro(x, R^2 mod N), 1) = x mod N
@@ -252,14 +271,19 @@ __global__ void __launch_bounds__(256, 2) k_synth_rows(const uint32_t* __restric
                                                     const uint32_t* __restrict__ P, size_t pstride, uint32_t pcount,
                                                     uint64_t seed, uint64_t row0, size_t count,
                                                     const uint32_t* __restrict__ consts, uint32_t n0,
-                                                    uint32_t* __restrict__ X, size_t xstride) {
+                                                    uint32_t* __restrict__ X, size_t xstride, uint32_t shards,
+                                                    uint32_t shard) {
   using G = Grp<S, TPI, W>;
   using M = Mont<S, TPI, W>;
   constexpr int L = G::L;
   G g;
   const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
   if (grp >= count) return;
-  const uint64_t h = splitmix64(seed ^ splitmix64(row0 + grp));
+  // local row l of shard `shard` of a column sharded in 64-row blocks round-robin over `shards`
+  // holds global row ((l/64)*shards + shard)*64 + l%64 (shards == 1: l itself)
+  const uint64_t l = row0 + grp;
+  const uint64_t grow = (((l >> 6) * shards + shard) << 6) | (l & 63u);
+  const uint64_t h = splitmix64(seed ^ splitmix64(grow));
   const uint32_t mi = (uint32_t)(h % tcount);
   const uint32_t ai = (uint32_t)((h >> 20) % pcount);
   const uint32_t bi = (uint32_t)((h >> 42) % pcount);
@@ -414,9 +438,12 @@ constexpr size_t kOpeTile = (size_t)kOpeBlock * kOpeItems;
 // issued before any predicate so they are in flight together.
 constexpr int kOpeGroups = kOpeItems / 4;
 
+// A row qualifies iff its valid byte v has (v & vmask) != 0 and (v & vbad) == 0 (raw arrays:
+// vmask 0xFF, vbad 0 — valid != 0; a resident OPE column: its searchable bit, minus wide rows).
 template <bool HasValid>
 __device__ __forceinline__ uint32_t ope_thread_mask(const int64_t* __restrict__ col, const uint8_t* __restrict__ valid,
-                                                    size_t n, int64_t bound, int op, size_t tile, bool vec) {
+                                                    size_t n, int64_t bound, int op, size_t tile, bool vec,
+                                                    uint32_t vmask, uint32_t vbad) {
   const size_t t0 = tile * kOpeTile + 4 * (size_t)threadIdx.x;
   int64_t c[kOpeItems];
   uint32_t v[kOpeGroups];
@@ -454,7 +481,8 @@ __device__ __forceinline__ uint32_t ope_thread_mask(const int64_t* __restrict__ 
   for (int k = 0; k < kOpeGroups; ++k)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if (((v[k] >> (8 * j)) & 0xFFu) && ope_pred(c[4 * k + j], bound, op)) mask |= 1u << (4 * k + j);
+      if ((((v[k] >> (8 * j)) & vmask) != 0u) && (((v[k] >> (8 * j)) & vbad) == 0u) && ope_pred(c[4 * k + j], bound, op))
+        mask |= 1u << (4 * k + j);
   return mask;
 }
 
@@ -468,12 +496,12 @@ __device__ __forceinline__ uint32_t ope_thread_mask(const int64_t* __restrict__ 
 template <bool HasValid>
 __global__ void __launch_bounds__(kOpeBlock) k_ope_count(const int64_t* __restrict__ col,
                                                          const uint8_t* __restrict__ valid, size_t n, int64_t bound,
-                                                         int op, uint32_t* __restrict__ masks,
-                                                         uint32_t* __restrict__ counts) {
+                                                         int op, uint32_t vmask, uint32_t vbad,
+                                                         uint32_t* __restrict__ masks, uint32_t* __restrict__ counts) {
   __shared__ uint32_t wsum[kOpeBlock / 64];
   const size_t t = (size_t)blockIdx.x * kOpeBlock + threadIdx.x;
   const bool vec = ((uintptr_t)col % 16 == 0) && (!HasValid || (uintptr_t)valid % 4 == 0);
-  const uint32_t m = ope_thread_mask<HasValid>(col, valid, n, bound, op, blockIdx.x, vec);
+  const uint32_t m = ope_thread_mask<HasValid>(col, valid, n, bound, op, blockIdx.x, vec, vmask, vbad);
   masks[t] = m;
   uint32_t s = __builtin_popcount(m);
   for (int off = 32; off >= 1; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off);
@@ -616,9 +644,10 @@ __global__ void __launch_bounds__(256) k_plain_sum_reduce(const uint64_t* __rest
 // multiplies rows (2p, 2p+1) of a [count][len] matrix into row p of [count/2][2 len].
 // ------------------------------------------------------------------------------
 // column sums: S[p][k] = sum_{i+j=k} A[2p][i] * A[2p+1][j]  (< len * 2^32, 64-bit)
+// outlen <= 2 len: columns [outlen, 2 len) are not computed (a product mod 2^(16 outlen), the
+// truncated tree of an even modulus' power-of-two part)
 __global__ void __launch_bounds__(256) k_bigmul_cols(const uint32_t* __restrict__ A, size_t count, size_t len,
-                                                     uint64_t* __restrict__ Sk) {
-  const size_t outlen = 2 * len;
+                                                     uint64_t* __restrict__ Sk, size_t outlen) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t p = blockIdx.y;
   if (k >= outlen) return;
@@ -696,10 +725,10 @@ size_t max_modulus_bits() {
 }
 
 hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, int W, const uint32_t* n2x,
-                            uint32_t* X, size_t stride, uint32_t* flags, hipStream_t st) {
+                            uint32_t* X, size_t stride, uint32_t* flags, hipStream_t st, uint8_t* rowflags) {
   if (count == 0) return hipSuccess;
   hipLaunchKernelGGL(k_ingest_be, dim3(grid_for(count)), dim3(256), 0, st, in, width, count, S, W, n2x, X, stride,
-                     flags);
+                     flags, rowflags);
   return hipGetLastError();
 }
 
@@ -712,19 +741,27 @@ hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, c
 }
 
 hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
-                       const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups, int s_out, hipStream_t st) {
+                       const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups, int s_out,
+                       hipStream_t st, const uint32_t* ids) {
   if (ngroups == 0 || ngroups > count) return hipErrorInvalidValue;
   // limbs S..s_out of the partials (tail shape is wider): zero, contiguous in the limb-major layout
   if (s_out > S) {
     hipError_t e = hipMemsetAsync(P + (size_t)S * pstride, 0, (size_t)(s_out - S) * pstride * 4, st);
     if (e != hipSuccess) return e;
   }
-  if (qp_mod) {  // N~ = N·n0 in place of N (Mont QP): no v_mul_lo per CIOS step
-    DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W, true>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X,
-                                       xstride, count, qp_mod, n0, P, pstride, ngroups));
+  const uint32_t* c = qp_mod ? qp_mod : consts;  // N~ = N·n0 in place of N (Mont QP): no v_mul_lo per CIOS step
+  if (qp_mod && ids) {
+    DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W, true, true>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X, xstride, count, c,
+                                       n0, P, pstride, ngroups, ids));
+  } else if (qp_mod) {
+    DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W, true>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X, xstride, count, c, n0, P,
+                                       pstride, ngroups, nullptr));
+  } else if (ids) {
+    DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W, false, true>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X, xstride, count, c,
+                                       n0, P, pstride, ngroups, ids));
   } else {
-    DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X,
-                                       xstride, count, consts, n0, P, pstride, ngroups));
+    DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X, xstride, count, c, n0, P,
+                                       pstride, ngroups, nullptr));
   }
   return hipGetLastError();
 }
@@ -837,10 +874,12 @@ hipError_t launch_modexp_ladder(int S, const uint32_t* Tab, size_t tstride, cons
 
 hipError_t launch_synth_rows(int S, const uint32_t* T, size_t tstride, uint32_t tcount, const uint32_t* P,
                              size_t pstride, uint32_t pcount, uint64_t seed, uint64_t row0, size_t count,
-                             const uint32_t* consts, uint32_t n0, uint32_t* X, size_t xstride, hipStream_t st) {
+                             const uint32_t* consts, uint32_t n0, uint32_t* X, size_t xstride, hipStream_t st,
+                             uint32_t shards, uint32_t shard) {
   if (count == 0) return hipSuccess;
   DDSHE_SWITCH(S, hipLaunchKernelGGL((k_synth_rows<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), 0, st, T, tstride,
-                                     tcount, P, pstride, pcount, seed, row0, count, consts, n0, X, xstride));
+                                     tcount, P, pstride, pcount, seed, row0, count, consts, n0, X, xstride, shards,
+                                     shard));
   return hipGetLastError();
 }
 
@@ -900,17 +939,17 @@ hipError_t launch_flag_compact(const uint32_t* flags, size_t n, uint32_t req, vo
 }
 
 hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
-                             uint64_t* total, uint32_t* out, hipStream_t st) {
+                             uint64_t* total, uint32_t* out, hipStream_t st, uint32_t vmask, uint32_t vbad) {
   const size_t nb = ope_blocks(n);
   if (nb == 0) return hipSuccess;
   uint32_t* counts = (uint32_t*)scratch;
   uint32_t* masks = counts + nb;
   if (valid)
-    hipLaunchKernelGGL(k_ope_count<true>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, bound, op, masks,
-                       counts);
+    hipLaunchKernelGGL(k_ope_count<true>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, bound, op, vmask,
+                       vbad, masks, counts);
   else
-    hipLaunchKernelGGL(k_ope_count<false>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, bound, op, masks,
-                       counts);
+    hipLaunchKernelGGL(k_ope_count<false>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, bound, op, vmask,
+                       vbad, masks, counts);
   hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, masks, counts, out, total);
   return hipGetLastError();
 }
@@ -922,10 +961,11 @@ hipError_t launch_plain_sum(const uint32_t* X, size_t stride, size_t count, int 
   return hipGetLastError();
 }
 
-hipError_t launch_bigmul_level(const uint32_t* A, size_t count, size_t len, uint64_t* Sk, uint32_t* V, hipStream_t st) {
-  const size_t pairs = (count + 1) / 2, outlen = 2 * len;
+hipError_t launch_bigmul_level(const uint32_t* A, size_t count, size_t len, uint64_t* Sk, uint32_t* V, hipStream_t st,
+                               size_t cap) {
+  const size_t pairs = (count + 1) / 2, outlen = cap ? std::min(2 * len, cap) : 2 * len;
   dim3 grid((unsigned)((outlen + 255) / 256), (unsigned)pairs);
-  hipLaunchKernelGGL(k_bigmul_cols, grid, dim3(256), 0, st, A, count, len, Sk);
+  hipLaunchKernelGGL(k_bigmul_cols, grid, dim3(256), 0, st, A, count, len, Sk, outlen);
   hipLaunchKernelGGL(k_bigmul_spread, grid, dim3(256), 0, st, Sk, outlen, V);
   return hipGetLastError();
 }
@@ -934,6 +974,23 @@ hipError_t launch_bigmul_carry(const uint32_t* V, size_t pairs, size_t outlen, u
                                hipStream_t st) {
   dim3 grid((unsigned)((outlen + 255) / 256), (unsigned)pairs);
   hipLaunchKernelGGL(k_bigmul_carry, grid, dim3(256), 0, st, V, outlen, Wout, flag);
+  return hipGetLastError();
+}
+
+// dst[r*drs + c*dcs] = src[r*srs + c*scs]: partials between the limb-major tree layout and packed rows
+__global__ void k_strided_copy(const uint32_t* __restrict__ src, size_t srs, size_t scs, uint32_t* __restrict__ dst,
+                               size_t drs, size_t dcs, size_t rows, size_t cols) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * cols) return;
+  const size_t r = i / cols, c = i % cols;
+  dst[r * drs + c * dcs] = src[r * srs + c * scs];
+}
+
+hipError_t launch_strided_copy(const uint32_t* src, size_t srs, size_t scs, uint32_t* dst, size_t drs, size_t dcs,
+                               size_t rows, size_t cols, hipStream_t st) {
+  if (rows * cols == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_strided_copy, dim3(grid_for(rows * cols)), dim3(256), 0, st, src, srs, scs, dst, drs, dcs, rows,
+                     cols);
   return hipGetLastError();
 }
 

@@ -16,19 +16,28 @@ struct Shape {
   int TPI;  // lanes per bignum
   int W;    // radix bits
 };
+// Largest column stride (rows, multiple of 64) the Montgomery kernels can address: mul_col reads a
+// block of PF limbs through one buffer descriptor with num_records = PF*stride*4 and per-limb
+// soffsets q*stride*4, all 32-bit (PF = 4 when S % 4 == 0, else 2). Beyond it the loads would wrap.
+inline size_t max_stride(int S) {
+  const size_t pf = (S % 4 == 0) ? 4 : 2;
+  return (((size_t)1 << 32) / (4 * pf) - 1) / 64 * 64;
+}
 Shape pick_shape(size_t mod_bits);  // S == 0: unsupported
 Shape tail_shape(const Shape& main);  // TPI = 16 shape (more limbs, same W) for tree levels + finalize
 size_t max_modulus_bits();
 
 hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, int W, const uint32_t* n2x,
-                            uint32_t* X, size_t stride, uint32_t* flags, hipStream_t st);
+                            uint32_t* X, size_t stride, uint32_t* flags, hipStream_t st,
+                            uint8_t* rowflags = nullptr);  // rowflags[i] = 1: row i >= 2N (stored reduced)
 hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, const uint32_t* consts, uint32_t n0,
                               hipStream_t st);
 // main fold level (throughput shape); partial rows are zero-extended to s_out limbs
 // qp_mod (nullable): N~ = N·n0 in main limbs (when W·S >= bits(N~) + 2; see Mont QP)
 hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
                        const uint32_t* qp_mod, uint32_t n0,
-                       uint32_t* P, size_t pstride, size_t ngroups, int s_out, hipStream_t st);
+                       uint32_t* P, size_t pstride, size_t ngroups, int s_out, hipStream_t st,
+                       const uint32_t* ids = nullptr);  // ids: fold rows ids[0..count) (device, u32)
 bool fold_qp_enabled();
 // tree levels / finalize in the tail shape (S = tail limb count, consts of the tail shape)
 // qp_mod (nullable): N~ = N·n0 in tail limbs, used by the latency-bound levels when tail_qp(S)
@@ -65,14 +74,18 @@ hipError_t launch_gather_rows(const uint32_t* T, size_t tstride, uint32_t tcount
                               size_t count, uint32_t* X, size_t xstride, hipStream_t st);
 hipError_t launch_synth_rows(int S, const uint32_t* T, size_t tstride, uint32_t tcount, const uint32_t* P,
                              size_t pstride, uint32_t pcount, uint64_t seed, uint64_t row0, size_t count,
-                             const uint32_t* consts, uint32_t n0, uint32_t* X, size_t xstride, hipStream_t st);
+                             const uint32_t* consts, uint32_t n0, uint32_t* X, size_t xstride, hipStream_t st,
+                             uint32_t shards = 1, uint32_t shard = 0);  // row mapping of a sharded column
 size_t ope_blocks(size_t n);
 size_t ope_scratch_bytes(size_t n);  // per-tile match counts + per-thread match masks
 // rows with flags[r] != 0 (req == 0) or (flags[r] & req) == req -> ascending ids; scratch as above
 hipError_t launch_flag_compact(const uint32_t* flags, size_t n, uint32_t req, void* scratch, uint64_t* total,
                                uint32_t* out, hipStream_t st);
+// rows i with (valid[i] & vmask) != 0 and (valid[i] & vbad) == 0 (valid == nullptr: every row) and
+// col[i] <op> bound -> ascending ids in out, count in *total (device)
 hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
-                             uint64_t* total, uint32_t* out, hipStream_t st);
+                             uint64_t* total, uint32_t* out, hipStream_t st, uint32_t vmask = 0xFFu,
+                             uint32_t vbad = 0u);
 // OPE ordering (ddshe_sort.hip): stable radix sort of the int64 column -> row ids
 size_t rs_scratch_bytes(size_t n);
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
@@ -110,10 +123,15 @@ hipError_t launch_plain_sum(const uint32_t* X, size_t stride, size_t count, int 
                             uint64_t* out, hipStream_t st);
 // unbounded product tree level: rows (2p, 2p+1) of A[count][len] (radix 2^16 in u32)
 // -> V[pairs][2 len] (limbs < 2^18, carries resolved by launch_bigmul_carry passes)
-hipError_t launch_bigmul_level(const uint32_t* A, size_t count, size_t len, uint64_t* Sk, uint32_t* V, hipStream_t st);
+// cap != 0: keep only the low min(2 len, cap) limbs of each product (products mod 2^(16 cap))
+hipError_t launch_bigmul_level(const uint32_t* A, size_t count, size_t len, uint64_t* Sk, uint32_t* V, hipStream_t st,
+                               size_t cap = 0);
 hipError_t launch_bigmul_carry(const uint32_t* V, size_t pairs, size_t outlen, uint32_t* Wout, uint32_t* flag,
                                hipStream_t st);
 hipError_t fold_occupancy(int S, int* blocks_per_cu);
+// dst[r*drs + c*dcs] = src[r*srs + c*scs] for r < rows, c < cols (u32 words, one device)
+hipError_t launch_strided_copy(const uint32_t* src, size_t srs, size_t scs, uint32_t* dst, size_t drs, size_t dcs,
+                               size_t rows, size_t cols, hipStream_t st);
 
 // decimal codec (ddshe_codec.hip): per-row status bits
 enum : uint32_t { kDecNeg = 1, kDecReduce = 2, kDecWide = 4, kDecFormat = 8 };

@@ -20,14 +20,21 @@ namespace ddshe {
     DDSHE_DISPATCH(112, 4, 28, __VA_ARGS__)          \
     DDSHE_DISPATCH(148, 4, 28, __VA_ARGS__)          \
     DDSHE_DISPATCH(232, 8, 27, __VA_ARGS__)          \
+    DDSHE_DISPATCH(320, 16, 27, __VA_ARGS__)         \
+    DDSHE_DISPATCH(640, 32, 27, __VA_ARGS__)         \
     default: return hipErrorInvalidValue;            \
   }
 
+// 320 x 27 bits: an 8192-bit modulus (n^2 of a 4096-bit Paillier key, QP-capable); 640 x 27: up to
+// 17278 bits (the JDK's largest RSA modulus, 16384 bits, for MultAll's pubkey). Wide shapes keep
+// L = S/TPI = 20 limbs per lane (register budget) and serve as their own tail shapes.
 // {76, 2, 28} is the 2048-bit alternative to {74, 2, 28} (4-limb blocks, room for the QP modulus);
 // pick_shape uses 76 unless DDSHE_RSA76=0
-inline constexpr Shape kShapes[] = {{40, 2, 28}, {74, 2, 28}, {76, 2, 28}, {112, 4, 28}, {148, 4, 28}, {232, 8, 27}};
-// latency-oriented shapes for the reduction tree / finalize: 16 lanes per bignum
-inline constexpr Shape kTail[] = {{48, 16, 28}, {80, 16, 28}, {80, 16, 28}, {112, 16, 28}, {160, 16, 28}, {240, 16, 27}};
+inline constexpr Shape kShapes[] = {{40, 2, 28},  {74, 2, 28},   {76, 2, 28},   {112, 4, 28},
+                                    {148, 4, 28}, {232, 8, 27},  {320, 16, 27}, {640, 32, 27}};
+// latency-oriented shapes for the reduction tree / finalize: 16 lanes per bignum (32 for the widest)
+inline constexpr Shape kTail[] = {{48, 16, 28},  {80, 16, 28},  {80, 16, 28},   {112, 16, 28},
+                                  {160, 16, 28}, {240, 16, 27}, {320, 16, 27}, {640, 32, 27}};
 
 #define DDSHE_TAIL_SWITCH(S_RT, ...)                 \
   switch (S_RT) {                                    \
@@ -36,6 +43,8 @@ inline constexpr Shape kTail[] = {{48, 16, 28}, {80, 16, 28}, {80, 16, 28}, {112
     DDSHE_DISPATCH(112, 16, 28, __VA_ARGS__)         \
     DDSHE_DISPATCH(160, 16, 28, __VA_ARGS__)         \
     DDSHE_DISPATCH(240, 16, 27, __VA_ARGS__)         \
+    DDSHE_DISPATCH(320, 16, 27, __VA_ARGS__)         \
+    DDSHE_DISPATCH(640, 32, 27, __VA_ARGS__)         \
     default: return hipErrorInvalidValue;            \
   }
 

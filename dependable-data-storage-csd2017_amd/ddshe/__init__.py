@@ -48,6 +48,12 @@ EXPORTS = [
     "dds_col_fill_table_synth", "dds_col_truncate",
     "dds_ope_order", "dds_ope_order_device", "dds_strtab_create", "dds_strtab_destroy", "dds_search_eq",
     "dds_search_entry", "dds_is_element",
+    "dds_col_fold_rows", "dds_col_fold_dec", "dds_col_fold_partial_device", "dds_combine_partials_device",
+    "dds_opecol_create", "dds_opecol_destroy", "dds_opecol_count", "dds_opecol_truncate", "dds_opecol_append",
+    "dds_opecol_append_dec", "dds_opecol_search", "dds_opecol_order",
+    "dds_mctx_create", "dds_mctx_create_devices", "dds_mctx_destroy", "dds_mctx_shards", "dds_mcol_create",
+    "dds_mcol_destroy", "dds_mcol_count", "dds_mcol_append", "dds_mcol_append_dec", "dds_mcol_fill_paillier_synth",
+    "dds_mcol_fold", "dds_mcol_fold_rows", "dds_mcol_fold_dec",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -112,6 +118,33 @@ _sig("dds_col_encrypt_paillier", C.c_int, C.c_void_p, C.c_void_p, _sz, C.c_void_
 _sig("dds_modexp_batch", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, C.c_char_p, _sz, _sz, _u8p)
 for _n in ("dds_sum_all_dec", "dds_mult_all_dec"):
     _sig(_n, C.c_int, C.c_void_p, C.POINTER(C.c_char_p), _sz, C.c_char_p, C.c_char_p, _sz, _szp)
+_u64p = C.POINTER(C.c_uint64)
+_sig("dds_col_fold_rows", C.c_int, C.c_void_p, _u64p, _sz, _u8p, _sz, _szp)
+_sig("dds_col_fold_dec", C.c_int, C.c_void_p, _u64p, _sz, C.c_char_p, _sz, _szp)
+_sig("dds_col_fold_partial_device", C.c_int, C.c_void_p, _sz, _sz, C.c_void_p)
+_sig("dds_combine_partials_device", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_void_p, _u64p, _sz, _u8p, _sz, _szp)
+_sig("dds_opecol_create", C.c_int, C.c_void_p, _sz, C.POINTER(C.c_void_p))
+_sig("dds_opecol_destroy", C.c_int, C.c_void_p)
+_sig("dds_opecol_count", _sz, C.c_void_p)
+_sig("dds_opecol_truncate", C.c_int, C.c_void_p, _sz)
+_sig("dds_opecol_append", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz)
+_sig("dds_opecol_append_dec", C.c_int, C.c_void_p, C.POINTER(C.c_char_p), C.c_void_p, C.c_void_p, _sz)
+_sig("dds_opecol_search", C.c_int, C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, _szp)
+_sig("dds_opecol_order", C.c_int, C.c_void_p, C.c_int, C.c_void_p)
+_sig("dds_mctx_create", C.c_int, C.c_uint64, C.POINTER(C.c_void_p))
+_sig("dds_mctx_create_devices", C.c_int, C.POINTER(C.c_int), _sz, C.POINTER(C.c_void_p))
+_sig("dds_mctx_destroy", C.c_int, C.c_void_p)
+_sig("dds_mctx_shards", _sz, C.c_void_p)
+_sig("dds_mcol_create", C.c_int, C.c_void_p, C.c_char_p, _sz, _sz, C.POINTER(C.c_void_p))
+_sig("dds_mcol_destroy", C.c_int, C.c_void_p)
+_sig("dds_mcol_count", _sz, C.c_void_p)
+_sig("dds_mcol_append", C.c_int, C.c_void_p, C.c_void_p, _sz, _sz)
+_sig("dds_mcol_append_dec", C.c_int, C.c_void_p, C.c_char_p, _u64p, _sz)
+_sig("dds_mcol_fill_paillier_synth", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, C.c_uint64, _sz,
+     C.c_uint32)
+_sig("dds_mcol_fold", C.c_int, C.c_void_p, _u8p, _sz, _szp)
+_sig("dds_mcol_fold_rows", C.c_int, C.c_void_p, _u64p, _sz, _u8p, _sz, _szp)
+_sig("dds_mcol_fold_dec", C.c_int, C.c_void_p, _u64p, _sz, C.c_char_p, _sz, _szp)
 
 
 class DDSError(RuntimeError):
@@ -335,6 +368,20 @@ class Engine:
     def column(self, modulus: int, capacity: int) -> "Column":
         return Column(self, modulus, capacity)
 
+    def opecol(self, capacity: int) -> "OpeColumn":
+        return OpeColumn(self, capacity)
+
+    def combine_partials_device(self, modulus: int, d_partials: int, rows) -> int:
+        """dds_combine_partials_device: partials back to back in device memory (d_partials pointer)."""
+        rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        mb = nbytes(modulus)
+        out = (C.c_uint8 * mb)()
+        olen = C.c_size_t()
+        _check(_lib.dds_combine_partials_device(self._h, int_to_be(modulus, mb), mb, C.c_void_p(d_partials),
+                                                rows.ctypes.data_as(_u64p), len(rows), out, mb, C.byref(olen)),
+               "dds_combine_partials_device")
+        return int.from_bytes(bytes(out[: olen.value]), "big")
+
     def combine_partials(self, modulus: int, partials: np.ndarray, rows) -> int:
         partials = np.ascontiguousarray(partials, dtype=np.uint32)
         rows = np.ascontiguousarray(rows, dtype=np.uint64)
@@ -411,10 +458,40 @@ class Column:
 
     def fold(self, first: int = 0, count: int | None = None) -> int:
         count = len(self) - first if count is None else count
-        out = (C.c_uint8 * self.mb)()
+        out = (C.c_uint8 * (self.mb + 4096))()  # a one-row fold returns the operand, which may be wider
         olen = C.c_size_t()
-        _check(_lib.dds_col_fold(self._h, first, count, out, self.mb, C.byref(olen)), "dds_col_fold")
+        _check(_lib.dds_col_fold(self._h, first, count, out, len(out), C.byref(olen)), "dds_col_fold")
         return int.from_bytes(bytes(out[: olen.value]), "big")
+
+    def fold_rows(self, row_ids) -> int:
+        """dds_col_fold_rows: SumAll/MultAll over the rows row_ids (a one-row fold returns the operand
+        as appended, unreduced)."""
+        ids = np.ascontiguousarray(row_ids, dtype=np.uint64)
+        out = (C.c_uint8 * (self.mb + 4096))()
+        olen = C.c_size_t()
+        _check(_lib.dds_col_fold_rows(self._h, ids.ctypes.data_as(_u64p), len(ids), out, len(out), C.byref(olen)),
+               "dds_col_fold_rows")
+        return int.from_bytes(bytes(out[: olen.value]), "big")
+
+    def fold_dec(self, row_ids=None, count: int | None = None) -> str:
+        """dds_col_fold_dec: the route's decimal reply over row_ids (or rows [0, count))."""
+        if row_ids is None:
+            ids, n = None, len(self) if count is None else count
+        else:
+            ids = np.ascontiguousarray(row_ids, dtype=np.uint64)
+            n = len(ids)
+        cap = 4 * self.mb + 8192
+        out = C.create_string_buffer(cap)
+        olen = C.c_size_t()
+        _check(_lib.dds_col_fold_dec(self._h, None if ids is None else ids.ctypes.data_as(_u64p), n, out, cap,
+                                     C.byref(olen)), "dds_col_fold_dec")
+        return out.value.decode()
+
+    def fold_partial_device(self, d_partial: int, first: int = 0, count: int | None = None):
+        """dds_col_fold_partial_device: the partial (partial_words u32) into device memory at d_partial."""
+        count = len(self) - first if count is None else count
+        _check(_lib.dds_col_fold_partial_device(self._h, first, count, C.c_void_p(d_partial)),
+               "dds_col_fold_partial_device")
 
     def fold_partial(self, first: int = 0, count: int | None = None):
         count = len(self) - first if count is None else count
@@ -451,6 +528,165 @@ class Column:
                                              int_to_be(n, nbytes(n)), nbytes(n), int_to_be(g, nbytes(g)), nbytes(g),
                                              pb, nbytes(p) if p else 0, qb, nbytes(q) if q else 0),
                "dds_col_encrypt_paillier")
+
+
+OPE_CLS_LACKS, OPE_CLS_LAST, OPE_CLS_INNER = 0, 1, 2
+
+
+class OpeColumn:
+    """Resident OPE column (dds_opecol): Search{Gt,GtEq,Lt,LtEq} and OrderLS/OrderSL over it."""
+
+    def __init__(self, eng: Engine, capacity: int):
+        self.eng = eng
+        h = C.c_void_p()
+        _check(_lib.dds_opecol_create(eng._h, capacity, C.byref(h)), "dds_opecol_create")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            _lib.dds_opecol_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return _lib.dds_opecol_count(self._h)
+
+    def truncate(self, count: int = 0):
+        _check(_lib.dds_opecol_truncate(self._h, count), "dds_opecol_truncate")
+
+    def append(self, values, cls=None):
+        v = np.ascontiguousarray(values, dtype=np.int64)
+        c = None if cls is None else np.ascontiguousarray(cls, dtype=np.uint8)
+        _check(_lib.dds_opecol_append(self._h, v.ctypes.data_as(C.c_void_p),
+                                      None if c is None else c.ctypes.data_as(C.c_void_p), len(v)),
+               "dds_opecol_append")
+
+    def append_dec(self, values, cls=None, is_string=None):
+        """values: element texts (str, or None where the row lacks the position)."""
+        n = len(values)
+        arr = (C.c_char_p * max(1, n))(*[None if v is None else str(v).encode() for v in values])
+        c = None if cls is None else np.ascontiguousarray(cls, dtype=np.uint8)
+        st = None if is_string is None else np.ascontiguousarray(is_string, dtype=np.uint8)
+        _check(_lib.dds_opecol_append_dec(self._h, arr, None if c is None else c.ctypes.data_as(C.c_void_p),
+                                          None if st is None else st.ctypes.data_as(C.c_void_p), n),
+               "dds_opecol_append_dec")
+
+    def search(self, bound, op: str) -> np.ndarray:
+        out = np.empty(max(1, len(self)), dtype=np.uint32)
+        got = C.c_size_t()
+        _check(_lib.dds_opecol_search(self._h, None if bound is None else str(bound).encode(), OPE_OPS[op],
+                                      out.ctypes.data_as(C.c_void_p), C.byref(got)), "dds_opecol_search")
+        return out[: got.value].copy()
+
+    def order(self, descending: bool) -> np.ndarray:
+        out = np.empty(max(1, len(self)), dtype=np.uint32)
+        _check(_lib.dds_opecol_order(self._h, int(descending), out.ctypes.data_as(C.c_void_p)), "dds_opecol_order")
+        return out[: len(self)].copy()
+
+
+class MultiEngine:
+    """dds_mctx: one caller driving several GPUs (devices may repeat: several shards on one GPU)."""
+
+    def __init__(self, devices=None, mask: int | None = None):
+        h = C.c_void_p()
+        if mask is not None:
+            _check(_lib.dds_mctx_create(int(mask), C.byref(h)), "dds_mctx_create")
+        else:
+            devs = (C.c_int * len(devices))(*devices)
+            _check(_lib.dds_mctx_create_devices(devs, len(devices), C.byref(h)), "dds_mctx_create_devices")
+        self._h = h
+
+    @property
+    def shards(self) -> int:
+        return _lib.dds_mctx_shards(self._h)
+
+    def close(self):
+        if self._h:
+            _lib.dds_mctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def column(self, modulus: int, capacity: int) -> "MColumn":
+        return MColumn(self, modulus, capacity)
+
+
+class MColumn:
+    """dds_mcol: a column sharded over the devices of a MultiEngine (64-row blocks, round-robin)."""
+
+    def __init__(self, m: MultiEngine, modulus: int, capacity: int):
+        self.m, self.modulus, self.mb = m, int(modulus), nbytes(modulus)
+        h = C.c_void_p()
+        _check(_lib.dds_mcol_create(m._h, int_to_be(modulus, self.mb), self.mb, capacity, C.byref(h)),
+               "dds_mcol_create")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            _lib.dds_mcol_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return _lib.dds_mcol_count(self._h)
+
+    def append(self, ops):
+        ops = [int(x) for x in ops]
+        width = max([self.mb] + [nbytes(x) for x in ops])
+        buf = ints_to_be(ops, width)
+        _check(_lib.dds_mcol_append(self._h, buf, width, len(ops)), "dds_mcol_append")
+
+    def append_buffer(self, buf: np.ndarray):
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        _check(_lib.dds_mcol_append(self._h, buf.ctypes.data, buf.shape[1], buf.shape[0]), "dds_mcol_append")
+
+    def append_dec(self, rows):
+        enc = [r.encode() if isinstance(r, str) else bytes(r) for r in rows]
+        chars = b"".join(enc)
+        offs = np.zeros(len(enc) + 1, dtype=np.uint64)
+        np.cumsum([len(e) for e in enc], out=offs[1:])
+        _check(_lib.dds_mcol_append_dec(self._h, chars, offs.ctypes.data_as(_u64p), len(enc)), "dds_mcol_append_dec")
+
+    def fill_paillier_synth(self, n: int, g: int, seed: int, count: int, pool: int = 1024):
+        _check(_lib.dds_mcol_fill_paillier_synth(self._h, int_to_be(n, nbytes(n)), nbytes(n), int_to_be(g, nbytes(g)),
+                                                 nbytes(g), seed, count, pool), "dds_mcol_fill_paillier_synth")
+
+    def fold(self) -> int:
+        out = (C.c_uint8 * (self.mb + 4096))()
+        olen = C.c_size_t()
+        _check(_lib.dds_mcol_fold(self._h, out, len(out), C.byref(olen)), "dds_mcol_fold")
+        return int.from_bytes(bytes(out[: olen.value]), "big")
+
+    def fold_rows(self, row_ids) -> int:
+        ids = np.ascontiguousarray(row_ids, dtype=np.uint64)
+        out = (C.c_uint8 * (self.mb + 4096))()
+        olen = C.c_size_t()
+        _check(_lib.dds_mcol_fold_rows(self._h, ids.ctypes.data_as(_u64p), len(ids), out, len(out), C.byref(olen)),
+               "dds_mcol_fold_rows")
+        return int.from_bytes(bytes(out[: olen.value]), "big")
+
+    def fold_dec(self, row_ids=None) -> str:
+        ids = None if row_ids is None else np.ascontiguousarray(row_ids, dtype=np.uint64)
+        cap = 4 * self.mb + 8192
+        out = C.create_string_buffer(cap)
+        olen = C.c_size_t()
+        _check(_lib.dds_mcol_fold_dec(self._h, None if ids is None else ids.ctypes.data_as(_u64p),
+                                      0 if ids is None else len(ids), out, cap, C.byref(olen)), "dds_mcol_fold_dec")
+        return out.value.decode()
 
 
 class StrTable:

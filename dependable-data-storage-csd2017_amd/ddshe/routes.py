@@ -6,15 +6,17 @@ rows (``DDSSet.contents`` lists, ``None`` for a missing set) — applies the rou
 own guard/dedup logic exactly as the Scala code does, and hands the whole loop to
 ONE batched C-ABI call. Errors follow the route: :class:`NotFound` is the 404
 branch, :class:`ServerError` the 500 branch.
+
+Element values are Python objects standing for what ``AnyJsonFormat`` reads
+(``DDSJsonProtocol.scala:22-28``): ``str`` (JsString), ``int`` (JsNumber → Int), ``bool``,
+``None`` (JsNull). A route that parses an element uses its ``toString``.
 """
 from __future__ import annotations
 
-import numpy as np
-
 from . import DDSError, Engine
 from . import NotFound as _EngineNotFound
-
-INT64_MIN, INT64_MAX = -(1 << 63), (1 << 63) - 1
+from . import OPE_CLS_INNER, OPE_CLS_LACKS, OPE_CLS_LAST
+from .x509 import rsa_modulus
 
 
 class NotFound(Exception):
@@ -25,23 +27,57 @@ class ServerError(Exception):
     """complete(StatusCodes.InternalServerError)"""
 
 
+def _value_key(v):
+    # Scala equality of a contents element: runtime type + value (Int 5 != String "5", true != 1)
+    if v is None:
+        return ("None",)
+    if isinstance(v, bool):
+        return ("Boolean", v)
+    if isinstance(v, int):
+        return ("Int", v)
+    return ("String", str(v))
+
+
 def _dedup(rows):
     # storedKeys.map(fetchSet) + Future.sequence over a Set collapses equal DDSSets
-    # (DDSRestServer.scala:401-403); filter(nonEmpty) drops missing ones (:408).
+    # (DDSRestServer.scala:401-403; DDSSet(contents: List[Any]) case-class equality, DDSSet.scala:3);
+    # filter(nonEmpty) drops missing ones (:408).
     seen, out = set(), []
     for r in rows:
         if r is None:
             continue
-        key = tuple(str(v) for v in r)
+        key = tuple(_value_key(v) for v in r)
         if key not in seen:
             seen.add(key)
             out.append(r)
     return out
 
 
+def _to_string(v) -> str:
+    """``toString`` of a contents element, as the text the engine parses. Scala prints booleans in
+    lower case and JsNull reads as ``None``; neither parses as an integer, like here."""
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    return str(v)
+
+
+def _dec_text(v) -> str:
+    """The element text for the engine's ASCII decimal parser. ``new BigInteger(String)`` and
+    ``Long.parseLong`` map digits with ``Character.digit`` (any Unicode Nd digit); non-ASCII text
+    that is such a number is rewritten as its ASCII decimal, anything else is passed through for the
+    engine to reject."""
+    s = _to_string(v)
+    if s.isascii():
+        return s
+    body = s[1:] if s[:1] in "+-" else s
+    if body and body.isdecimal():
+        return ("-" if s[:1] == "-" else "") + str(int(body))
+    return s
+
+
 def _column(rows, position):
     # guard `contents.length-1 > position` (DDSRestServer.scala:415 / :509)
-    return [str(r[position]) for r in rows if len(r) - 1 > position]
+    return [_dec_text(r[position]) for r in rows if len(r) - 1 > position]
 
 
 def _call(fn, *args):
@@ -54,112 +90,120 @@ def _call(fn, *args):
 
 
 def sum_all(eng: Engine, rows, position: int, nsqr: str | None = None) -> str:
-    """GET /SumAll?position&nsqr — DDSRestServer.scala:397-446."""
+    """GET /SumAll?position&nsqr — DDSRestServer.scala:397-446. nsqr is parsed only in the
+    later-operand branch (:422): the engine ignores it when one operand qualifies."""
     rows = _dedup(rows)
     if not rows:
         raise NotFound()
     vals = _column(rows, position)
     if not vals:
         raise NotFound()
-    return _call(eng.sum_all_dec, vals, nsqr)
+    return _call(eng.sum_all_dec, vals, None if nsqr is None else _dec_text(nsqr))
 
 
-def mult_all(eng: Engine, rows, position: int, n: str | None = None) -> str:
-    """GET /MultAll?position&pubkey — DDSRestServer.scala:491-539. ``n`` is the
-    modulus of the X.509 pubkey (decoded by the caller, :515-517)."""
+def _pubkey_modulus(pubkey: str) -> str:
+    try:
+        return str(rsa_modulus(pubkey))
+    except ValueError as e:
+        raise ServerError(f"InvalidKeySpecException: {e}") from e
+
+
+def mult_all(eng: Engine, rows, position: int, n: str | None = None, pubkey: str | None = None) -> str:
+    """GET /MultAll?position&pubkey — DDSRestServer.scala:491-539. ``pubkey`` (hex X.509) is decoded
+    only in the later-operand branch (:515-517), i.e. when two or more operands qualify; ``n`` may
+    be given instead (the modulus, already decoded). Neither: the plain product (:520)."""
     rows = _dedup(rows)
     if not rows:
         raise NotFound()
     vals = _column(rows, position)
     if not vals:
         raise NotFound()
-    return _call(eng.mult_all_dec, vals, n)
+    if pubkey is not None and len(vals) >= 2:
+        n = _pubkey_modulus(pubkey)
+    return _call(eng.mult_all_dec, vals, None if n is None else _dec_text(n))
 
 
-def _pair(rows, position):
-    set1, set2 = rows
+def _pair(set1, set2, position):
     if set1 is None or set2 is None:
         raise NotFound()
-    if len(set1) - 1 < position or len(set2) - 1 < position:  # :376 / :468
+    if len(set1) - 1 < position or len(set2) - 1 < position:  # :376 / :468 (not strict)
         raise NotFound()
-    return [str(set1[position]), str(set2[position])]
+    return [_dec_text(set1[position]), _dec_text(set2[position])]
 
 
 def pair_sum(eng: Engine, set1, set2, position: int, nsqr: str | None = None) -> str:
-    """GET /Sum?key1&key2&position&nsqr — DDSRestServer.scala:355-395 (HomoAdd.sum, :385)."""
-    return _call(eng.sum_all_dec, _pair((set1, set2), position), nsqr)
+    """GET /Sum?key1&key2&position&nsqr — DDSRestServer.scala:355-395 (HomoAdd.sum, :385).
+    Two keys, two operands: no dedup (the same set twice is folded twice)."""
+    return _call(eng.sum_all_dec, _pair(set1, set2, position), None if nsqr is None else _dec_text(nsqr))
 
 
-def pair_mult(eng: Engine, set1, set2, position: int, n: str | None = None) -> str:
+def pair_mult(eng: Engine, set1, set2, position: int, n: str | None = None, pubkey: str | None = None) -> str:
     """GET /Mult?key1&key2&position&pubkey — DDSRestServer.scala:447-490 (HomoMult.multiply, :479)."""
-    return _call(eng.mult_all_dec, _pair((set1, set2), position), n)
+    vals = _pair(set1, set2, position)
+    if pubkey is not None:
+        n = _pubkey_modulus(pubkey)
+    return _call(eng.mult_all_dec, vals, None if n is None else _dec_text(n))
 
 
 _ROUTE_OP = {"SearchGt": "gt", "SearchGtEq": "ge", "SearchLt": "lt", "SearchLtEq": "le"}
 
 
-def _parse_int(s) -> int:
-    s = str(s)
-    body = s[1:] if s[:1] in "+-" else s
-    if not body or not body.isascii() or not body.isdigit():
-        raise ServerError(f"NumberFormatException: {s!r}")
-    return int(s)
-
-
-def _clamp_bound(op: str, item: int):
-    """Map a BigInteger bound outside int64 to an equivalent int64 predicate."""
-    if INT64_MIN <= item <= INT64_MAX:
-        return op, item
-    if item > INT64_MAX:   # col > item / col >= item never; col < item / col <= item always
-        return ("gt", INT64_MAX) if op in ("gt", "ge") else ("le", INT64_MAX)
-    return ("ge", INT64_MIN) if op in ("gt", "ge") else ("lt", INT64_MIN)
+def _ope_rows(keyed_rows, position: int, dedup_keys: bool):
+    """keys, element texts, row classes and String flags of the live rows for a dds_opecol."""
+    keys, vals, cls, isstr, seen = [], [], [], [], set()
+    for key, row in keyed_rows:
+        if row is None or (dedup_keys and key in seen):
+            continue
+        seen.add(key)
+        last = len(row) - 1
+        c = OPE_CLS_INNER if last > position else OPE_CLS_LAST if last == position else OPE_CLS_LACKS
+        keys.append(key)
+        cls.append(c)
+        if c == OPE_CLS_LACKS:
+            vals.append(None)
+            isstr.append(0)
+        else:
+            v = row[position]
+            vals.append(_dec_text(v))
+            isstr.append(1 if isinstance(v, str) else 0)
+    return keys, vals, cls, isstr
 
 
 def search(eng: Engine, route: str, keyed_rows, position: int, value) -> list:
-    """POST /Search{Gt,GtEq,Lt,LtEq}?position — DDSRestServer.scala:682-830.
-    Returns the matching keys (the reference's key order is unspecified: it
-    prepends, :705; the engine returns them in row order)."""
+    """POST /Search{Gt,GtEq,Lt,LtEq}?position — DDSRestServer.scala:682-830 over a resident OPE
+    column (dds_opecol). The bound (``item.value.toString``) is parsed only when a row passes the
+    strict guard (:702-704); rows and bound compare as BigIntegers (values outside Long included).
+    Returns the matching keys in row order (the reference prepends, :705: order unspecified)."""
     op = _ROUTE_OP[route]
-    item = _parse_int(value)
-    keys, col, valid, seen = [], [], [], set()
-    for key, row in keyed_rows:
-        if row is None or key in seen:
-            continue
-        seen.add(key)
-        ok = len(row) - 1 > position
-        v = _parse_int(row[position]) if ok else 0
-        if ok and not (INT64_MIN <= v <= INT64_MAX):
-            raise ServerError("OPE value outside int64 (OPE ciphertexts are Java Long)")
-        keys.append(key)
-        col.append(v)
-        valid.append(1 if ok else 0)
+    keys, vals, cls, isstr = _ope_rows(keyed_rows, position, True)
     if not keys:
         return []
-    op, bound = _clamp_bound(op, item)
-    idx = _call(eng.ope_filter, np.array(col, dtype=np.int64), np.array(valid, dtype=np.uint8), bound, op)
+    col = eng.opecol(len(keys))
+    try:
+        _call(col.append_dec, vals, cls, isstr)
+        idx = _call(col.search, _dec_text(value), op)
+    finally:
+        col.close()
     return [keys[i] for i in idx]
 
 
 def order(eng: Engine, route: str, keyed_rows, position: int) -> list:
-    """GET /OrderLS|/OrderSL?position — DDSRestServer.scala:541-606: keys of the non-empty
-    rows, holders of the position (length-1 >= position) by contents(position).toLong
-    descending (OrderLS, others last) or ascending (OrderSL, others first); stable for ties."""
+    """GET /OrderLS|/OrderSL?position — DDSRestServer.scala:541-606 over a resident OPE column: keys
+    of the non-empty rows, holders of the position (length-1 >= position) by
+    contents(position).asInstanceOf[String].toLong descending (OrderLS, others last) or ascending
+    (OrderSL, others first); stable for ties. With two or more holders every holder is parsed (a
+    non-String or non-Long holder → 500); a lone holder is never parsed."""
     if route not in ("OrderLS", "OrderSL"):
         raise ValueError(route)
-    keys, col, valid = [], [], []
-    for key, row in keyed_rows:
-        if row is None:
-            continue
-        ok = len(row) - 1 >= position
-        v = _parse_int(row[position]) if ok else 0
-        if ok and not (INT64_MIN <= v <= INT64_MAX):
-            raise ServerError("NumberFormatException: value outside Long (String.toLong)")
-        keys.append(key)
-        col.append(v)
-        valid.append(1 if ok else 0)
+    keys, vals, cls, isstr = _ope_rows(keyed_rows, position, False)
     if not keys:
         return []
-    idx = _call(eng.ope_order, np.array(col, dtype=np.int64), np.array(valid, dtype=np.uint8), route == "OrderLS")
+    col = eng.opecol(len(keys))
+    try:
+        _call(col.append_dec, vals, cls, isstr)
+        idx = _call(col.order, route == "OrderLS")
+    finally:
+        col.close()
     return [keys[i] for i in idx]
 
 

@@ -126,17 +126,64 @@ size_t dds_col_count(const dds_col* col);
 int dds_col_truncate(dds_col* col, size_t count);
 /* download rows [first, first+count) as canonical residues (x mod N), big-endian, mod_bytes each */
 int dds_col_read(dds_col* col, size_t first, size_t count, uint8_t* out);
-/* fold rows [first, first+count) (SumAll/MultAll semantics as dds_modmul_fold; a column holds
- * residues, so a one-row fold returns that row's canonical residue) */
+/* fold rows [first, first+count) (SumAll/MultAll semantics as dds_modmul_fold). A one-row fold returns
+ * that row's operand as appended, unreduced (DDSRestServer.scala:416-417: the column remembers the
+ * operands it had to store as residues); *out_len = max(modulus bytes, operand bytes). A negative
+ * operand (decimal rows) has no big-endian magnitude form: DDS_E_RANGE, use dds_col_fold_dec. */
 int dds_col_fold(dds_col* col, size_t first, size_t count, uint8_t* out, size_t out_cap, size_t* out_len);
+/* Row-subset fold: the rows row_ids[0..n) of the column (ids < dds_col_count; duplicates fold twice),
+ * i.e. the sets a SumAll / MultAll route keeps after its dedup and strict guard
+ * (DDSRestServer.scala:401-415, 505-509) without re-uploading them. Same result rules as dds_col_fold. */
+int dds_col_fold_rows(dds_col* col, const uint64_t* row_ids, size_t n, uint8_t* out, size_t out_cap,
+                      size_t* out_len);
+/* Same fold with the route's decimal reply (DDSValueResult(acc.toString), :435/:529): rows row_ids[0..n),
+ * or rows [0, n) when row_ids is NULL. out receives NUL-terminated text, *out_len its length. */
+int dds_col_fold_dec(dds_col* col, const uint64_t* row_ids, size_t n, char* out, size_t out_cap, size_t* out_len);
 /* fold rows to one un-finalised partial for multi-GPU combination:
  * partial_r27 receives limbs() words, *rows the row count it covers. */
 int dds_col_fold_partial(dds_col* col, size_t first, size_t count, uint32_t* partial_r27, uint64_t* rows);
 /* number of 32-bit words in a partial of this column's modulus */
 size_t dds_col_partial_words(const dds_col* col);
-/* combine partials from several GPUs (same modulus): result = prod of all rows mod N */
+/* combine partials from several GPUs (same modulus): result = prod of all rows mod N. Each partial must
+ * be what dds_col_fold_partial produced (normalised limbs, value in range): DDS_E_RANGE otherwise. */
 int dds_combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint32_t* partials_r27,
                          const uint64_t* rows, size_t nparts, uint8_t* out, size_t out_cap, size_t* out_len);
+/* Device-resident forms for a multi-process (one rank per GPU) gather that never stages the partial
+ * limbs through the host: dds_col_fold_partial_device writes the partial (dds_col_partial_words u32,
+ * the last two words the exponent) to DEVICE memory of the column's GPU and synchronises before
+ * returning; dds_combine_partials_device combines nparts such partials laid out back to back in device
+ * memory of ctx's GPU (e.g. the output of an RCCL all_gather). */
+int dds_col_fold_partial_device(dds_col* col, size_t first, size_t count, uint32_t* d_partial);
+int dds_combine_partials_device(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint32_t* d_partials,
+                                const uint64_t* rows, size_t nparts, uint8_t* out, size_t out_cap, size_t* out_len);
+
+/* ---- one caller, several GPUs (SURVEY.md §8b device_mask) ----------------------------------
+ * A dds_mctx owns one context per shard; shard 0's device combines. dds_mctx_create takes a device
+ * bit mask (bit d = HIP device d); dds_mctx_create_devices an explicit list, where a device may repeat
+ * (several shards on one GPU). A dds_mcol spreads its rows over the shards in 64-row blocks,
+ * round-robin (global row r on shard (r/64) % G). dds_mcol_fold* fold every shard on its own device
+ * concurrently, move the shard partials device-to-device (xGMI peer copies) to the combining device
+ * and combine there: same results and result rules as dds_col_fold / dds_col_fold_rows /
+ * dds_col_fold_dec, row ids being global. Appends split the batch per shard and upload concurrently;
+ * a failed append leaves the column unchanged. */
+typedef struct dds_mctx dds_mctx;
+typedef struct dds_mcol dds_mcol;
+int dds_mctx_create(uint64_t device_mask, dds_mctx** out);
+int dds_mctx_create_devices(const int* devices, size_t ndevices, dds_mctx** out);
+int dds_mctx_destroy(dds_mctx* m);
+size_t dds_mctx_shards(const dds_mctx* m);
+int dds_mcol_create(dds_mctx* m, const uint8_t* mod_be, size_t mod_bytes, size_t capacity, dds_mcol** out);
+int dds_mcol_destroy(dds_mcol* col);
+size_t dds_mcol_count(const dds_mcol* col);
+int dds_mcol_append(dds_mcol* col, const uint8_t* operands_be, size_t width, size_t count);
+int dds_mcol_append_dec(dds_mcol* col, const char* chars, const uint64_t* offsets, size_t count);
+/* synthetic rows as dds_col_fill_paillier_synth with row0 = the current global row count */
+int dds_mcol_fill_paillier_synth(dds_mcol* col, const uint8_t* n_be, size_t n_bytes, const uint8_t* g_be,
+                                 size_t g_bytes, uint64_t seed, size_t count, uint32_t pool_size);
+int dds_mcol_fold(dds_mcol* col, uint8_t* out, size_t out_cap, size_t* out_len);
+int dds_mcol_fold_rows(dds_mcol* col, const uint64_t* row_ids, size_t n, uint8_t* out, size_t out_cap,
+                       size_t* out_len);
+int dds_mcol_fold_dec(dds_mcol* col, const uint64_t* row_ids, size_t n, char* out, size_t out_cap, size_t* out_len);
 /* Synthetic Paillier rows for benchmarks/tests (config 2 of BASELINE.json):
  * c_i = g^m_i * r_a^n * r_b^n mod n^2 with m_i, a, b from splitmix64(seed, row0+i);
  * m_i = splitmix64(seed ^ splitmix64(row0+i)) % 10000 (DDSDataGenerator.scala:274).
@@ -154,6 +201,36 @@ int dds_ope_filter(dds_ctx* ctx, const int64_t* col, const uint8_t* valid, size_
 /* same on device-resident arrays (pointers are device pointers) */
 int dds_ope_filter_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_valid, size_t n, int64_t bound, int op,
                           uint32_t* d_out_idx, size_t* out_n);
+
+/* ---- resident OPE column (Search{Gt,GtEq,Lt,LtEq} :682-830, OrderLS/OrderSL :541-606) ----
+ * The OPE ciphertexts of one column position stay in HBM across requests. Per row the caller gives
+ * the element's text (contents(position).toString, ASCII decimal) and its class:
+ *   cls 0: the row lacks the position (contents.length-1 < position)
+ *   cls 1: the position is the row's last element (length-1 == position: an Order holder that
+ *          Search's strict guard `length-1 > position` skips, :702)
+ *   cls 2: elements follow it (both routes read it); cls == NULL: every row is class 2.
+ * is_string (NULL: all) flags elements that are Strings: Order reads contents(position).asInstanceOf
+ * [String].toLong (:562/:595), which throws on an Int element; Search's BigInteger(toString) does not.
+ * Values outside int64 are kept exactly (Search compares BigIntegers); malformed ones are kept as
+ * such and fail a request only when the reference's loop would parse them:
+ *   dds_opecol_search: the bound (item.value.toString) is parsed only when some row passes the guard
+ *     (:702-704): no class-2 row -> 0 matches, any bound; a malformed bound or class-2 element -> 
+ *     DDS_E_FORMAT (500). out_idx (capacity dds_opecol_count) receives ascending row ids.
+ *   dds_opecol_order: a permutation of all rows, as dds_ope_order with valid = cls != 0; with two or
+ *     more holders every holder is parsed by the comparator: a holder that is not a Long String ->
+ *     DDS_E_FORMAT; a lone holder is never parsed. */
+typedef struct dds_opecol dds_opecol;
+int dds_opecol_create(dds_ctx* ctx, size_t capacity, dds_opecol** out);
+int dds_opecol_destroy(dds_opecol* col);
+size_t dds_opecol_count(const dds_opecol* col);
+int dds_opecol_truncate(dds_opecol* col, size_t count);
+/* rows already as Java Longs (values) */
+int dds_opecol_append(dds_opecol* col, const int64_t* values, const uint8_t* cls, size_t count);
+/* rows as the element text the route parses (values[i] may be NULL when cls[i] == 0) */
+int dds_opecol_append_dec(dds_opecol* col, const char* const* values, const uint8_t* cls, const uint8_t* is_string,
+                          size_t count);
+int dds_opecol_search(dds_opecol* col, const char* bound_dec, int op, uint32_t* out_idx, size_t* out_n);
+int dds_opecol_order(dds_opecol* col, int descending, uint32_t* out_idx);
 
 /* ---- OPE ordering (OrderLS / OrderSL, DDSRestServer.scala:541-606) ------------
  * out_idx receives a permutation of [0, n): rows with valid[i] != 0 (the row holds the

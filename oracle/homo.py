@@ -78,23 +78,48 @@ class ServerError(Exception):
 
 
 def java_biginteger(s) -> int:
-    """``new BigInteger(String)``: optional sign, decimal digits only."""
+    """``new BigInteger(String)`` (radix 10): an optional '+' or '-', then one or more digits,
+    each mapped by ``Character.digit(c, 10)`` — any Unicode decimal digit (category Nd), not only
+    ASCII; nothing else (no blanks, no '_'). Anything else is a NumberFormatException (→ 500)."""
     s = str(s)
     body = s[1:] if s[:1] in "+-" else s
-    if not body or not body.isdigit() or not body.isascii():
+    if not body or not body.isdecimal():
         raise ServerError(f"NumberFormatException: {s!r}")
-    return int(s)
+    v = int(body)
+    return -v if s[:1] == "-" else v
+
+
+def java_mod(x: int, m: int) -> int:
+    """``BigInteger.mod(m)``: the non-negative residue; ``ArithmeticException`` (→ 500) for m <= 0."""
+    if m <= 0:
+        raise ServerError("ArithmeticException: BigInteger: modulus not positive")
+    return x % m
+
+
+def value_key(v):
+    """Equality of one ``DDSSet.contents`` element as Scala sees it: values of different runtime
+    types never compare equal (``AnyJsonFormat`` reads JSON numbers as Int, strings as String,
+    booleans as Boolean, null as None — ``DDSJsonProtocol.scala:22-28``), so Int 5 != String "5" and
+    true != 1 (Python's ``True == 1`` must not merge them)."""
+    if v is None:
+        return ("None",)
+    if isinstance(v, bool):
+        return ("Boolean", v)
+    if isinstance(v, int):
+        return ("Int", v)
+    return ("String", str(v))
 
 
 def dedup_rows(rows):
     """``storedKeys.map(fetchSet)`` + ``Future.sequence`` over a Set collapses equal
-    DDSSets (``DDSRestServer.scala:401-403``) and ``filter(nonEmpty)`` drops
+    DDSSets (``DDSRestServer.scala:401-403``; case-class equality of ``contents: List[Any]``,
+    element by element with its runtime type, ``DDSSet.scala:3``) and ``filter(nonEmpty)`` drops
     missing ones (``:408``). Rows are lists of column values; None = missing."""
     seen, out = set(), []
     for r in rows:
         if r is None:
             continue
-        key = tuple(str(v) for v in r)
+        key = tuple(value_key(v) for v in r)
         if key in seen:
             continue
         seen.add(key)
@@ -106,19 +131,19 @@ def sum_all(rows, position: int, nsqr=None) -> str:
     """``GET /SumAll?position&nsqr`` — ``DDSRestServer.scala:397-446``.
     Strict guard ``contents.length-1 > position`` (``:415``); first operand is
     taken unreduced (``:416-417``); each later one is folded with HomoAdd.sum
-    (``:422-423``) or plain ``add`` when nsqr is absent (``:425``)."""
+    (``:422-423``) or plain ``add`` when nsqr is absent (``:425``). ``nsqr`` is parsed only
+    inside that later-operand branch (``:422``), i.e. never when one operand qualifies."""
     rows = dedup_rows(rows)
     if not rows:
         raise NotFound()
     acc = None
-    nsq = java_biginteger(nsqr) if nsqr is not None else None
     for r in rows:
         if len(r) - 1 > position:
             x = java_biginteger(r[position])
             if acc is None:
                 acc = x
-            elif nsq is not None:
-                acc = homo_add_sum(acc, x, nsq)
+            elif nsqr is not None:
+                acc = homo_add_sum_checked(acc, x, java_biginteger(nsqr))
             else:
                 acc = acc + x
     if acc is None:
@@ -126,9 +151,55 @@ def sum_all(rows, position: int, nsqr=None) -> str:
     return str(acc)
 
 
-def mult_all(rows, position: int, n=None) -> str:
+def rsa_modulus_from_pubkey_hex(pubkey: str) -> int:
+    """``KeyFactory.getInstance("RSA").generatePublic(new X509EncodedKeySpec(
+    DatatypeConverter.parseHexBinary(pubkey)))`` (``DDSRestServer.scala:476-478,515-517``) → its
+    modulus. parseHexBinary needs an even number of hex digits; the DER must be an X.509
+    SubjectPublicKeyInfo of rsaEncryption; the JDK's RSA key factory refuses moduli outside
+    [512, 16384] bits (``RSAKeyFactory.checkRSAProviderKeyLengths``). Failures → 500."""
+    h = str(pubkey)
+    if len(h) % 2 or any(c not in "0123456789abcdefABCDEF" for c in h):
+        raise ServerError("IllegalArgumentException: parseHexBinary")
+    der = bytes.fromhex(h)
+
+    def tlv(buf, i):  # (tag, value, next) with the declared length fully present
+        if i + 2 > len(buf):
+            raise ServerError("InvalidKeySpecException: truncated DER")
+        tag, ln, i = buf[i], buf[i + 1], i + 2
+        if ln & 0x80:
+            nb = ln & 0x7F
+            ln, i = int.from_bytes(buf[i:i + nb], "big"), i + nb
+        if i + ln > len(buf):
+            raise ServerError("InvalidKeySpecException: truncated DER")
+        return tag, buf[i:i + ln], i + ln
+
+    tag, spki, end = tlv(der, 0)
+    if tag != 0x30 or end != len(der):
+        raise ServerError("InvalidKeySpecException: not one SubjectPublicKeyInfo")
+    tag, alg, i = tlv(spki, 0)
+    tag2, oid, _ = tlv(alg, 0)
+    if tag != 0x30 or tag2 != 0x06 or oid != bytes.fromhex("2a864886f70d010101"):
+        raise ServerError("InvalidKeySpecException: not rsaEncryption")
+    tag, bits, i = tlv(spki, i)
+    if tag != 0x03 or i != len(spki) or bits[:1] != b"\0":
+        raise ServerError("InvalidKeySpecException: bad subjectPublicKey")
+    tag, key, j = tlv(bits, 1)
+    if tag != 0x30 or j != len(bits):
+        raise ServerError("InvalidKeySpecException: bad RSAPublicKey")
+    tag, nb, j = tlv(key, 0)
+    tag2, eb, j = tlv(key, j)
+    if tag != 0x02 or tag2 != 0x02 or j != len(key):
+        raise ServerError("InvalidKeySpecException: bad RSAPublicKey")
+    n = int.from_bytes(nb, "big", signed=True)
+    if not 512 <= n.bit_length() <= 16384 or n <= 0:
+        raise ServerError("InvalidKeyException: RSA modulus length")
+    return n
+
+
+def mult_all(rows, position: int, n=None, pubkey=None) -> str:
     """``GET /MultAll?position&pubkey`` — ``DDSRestServer.scala:491-539``.
-    ``n`` is the modulus of the X.509 pubkey (``:515-517``); None = plain product (``:520``)."""
+    ``pubkey`` is the hex X.509 key, decoded only inside the later-operand branch (``:515-517``);
+    ``n`` may be given instead (its modulus, already decoded). Neither = plain product (``:520``)."""
     rows = dedup_rows(rows)
     if not rows:
         raise NotFound()
@@ -138,6 +209,8 @@ def mult_all(rows, position: int, n=None) -> str:
             x = java_biginteger(r[position])
             if acc is None:
                 acc = x
+            elif pubkey is not None:
+                acc = homo_mult_multiply(acc, x, rsa_modulus_from_pubkey_hex(pubkey))
             elif n is not None:
                 acc = homo_mult_multiply(acc, x, n)
             else:
@@ -147,26 +220,33 @@ def mult_all(rows, position: int, n=None) -> str:
     return str(acc)
 
 
+def homo_add_sum_checked(c1: int, c2: int, nsquare: int) -> int:
+    """HomoAdd.sum with BigInteger.mod's exception on a non-positive modulus (→ 500)."""
+    return java_mod(c1 * c2, nsquare)
+
+
 def pair_sum(set1, set2, position: int, nsqr=None) -> str:
     """``GET /Sum?key1&key2&position&nsqr`` — ``DDSRestServer.scala:355-395``
-    (guard ``length-1 < position`` → 404 at ``:376``)."""
+    (guard ``length-1 < position`` → 404 at ``:376``; no dedup: two keys, two operands)."""
     if set1 is None or set2 is None:
         raise NotFound()
     if len(set1) - 1 < position or len(set2) - 1 < position:
         raise NotFound()
     a, b = java_biginteger(set1[position]), java_biginteger(set2[position])
     if nsqr is not None:
-        return str(homo_add_sum(a, b, java_biginteger(nsqr)))
+        return str(homo_add_sum_checked(a, b, java_biginteger(nsqr)))
     return str(a + b)
 
 
-def pair_mult(set1, set2, position: int, n=None) -> str:
+def pair_mult(set1, set2, position: int, n=None, pubkey=None) -> str:
     """``GET /Mult?key1&key2&position&pubkey`` — ``DDSRestServer.scala:447-490``."""
     if set1 is None or set2 is None:
         raise NotFound()
     if len(set1) - 1 < position or len(set2) - 1 < position:
         raise NotFound()
     a, b = java_biginteger(set1[position]), java_biginteger(set2[position])
+    if pubkey is not None:
+        return str(homo_mult_multiply(a, b, rsa_modulus_from_pubkey_hex(pubkey)))
     if n is not None:
         return str(homo_mult_multiply(a, b, n))
     return str(a * b)
@@ -185,29 +265,37 @@ OPS = {
 def search(route: str, keyed_rows, position: int, value) -> set:
     """``POST /Search{Gt,GtEq,Lt,LtEq}?position`` — ``DDSRestServer.scala:682-830``.
     ``keyed_rows`` = list of (key, row). Returns the matching key SET (the
-    reference prepends into a list, so order is unspecified: ``:705``)."""
+    reference prepends into a list, so order is unspecified: ``:705``). The bound is parsed with
+    ``new BigInteger(item.value.toString)`` inside the per-row condition, after the strict guard
+    (``:702-704``): only when some row qualifies. Both sides are arbitrary-size BigIntegers."""
     pred = OPS[route]
-    item = java_biginteger(value)
     out = set()
     seen = set()
     for key, row in keyed_rows:
         if row is None or key in seen:
             continue
         seen.add(key)
-        if len(row) - 1 > position and pred(java_biginteger(row[position]), item):
-            out.add(key)
+        if len(row) - 1 > position:
+            item = java_biginteger(value)
+            if pred(java_biginteger(row[position]), item):
+                out.add(key)
     return out
 
 
 def java_long(s) -> int:
-    """``String.toLong`` (java.lang.Long.parseLong): optional sign, decimal digits, int64 range."""
-    s = str(s)
+    """``contents(position).asInstanceOf[String].toLong`` (``DDSRestServer.scala:562,595``): the
+    element must be a String (an Int element is a ClassCastException), then
+    ``java.lang.Long.parseLong``: optional sign, ``Character.digit`` decimal digits, int64 range.
+    Failures → 500."""
+    if not isinstance(s, str):
+        raise ServerError(f"ClassCastException: {type(s).__name__} is not a String")
     body = s[1:] if s[:1] in "+-" else s
-    if not body or not body.isascii() or not body.isdigit():
-        raise ValueError(f"NumberFormatException: {s!r}")
-    v = int(s)
+    if not body or not body.isdecimal():
+        raise ServerError(f"NumberFormatException: {s!r}")
+    v = int(body)
+    v = -v if s[:1] == "-" else v
     if not -(1 << 63) <= v < (1 << 63):
-        raise ValueError(f"NumberFormatException: {s!r} (out of Long range)")
+        raise ServerError(f"NumberFormatException: {s!r} (out of Long range)")
     return v
 
 
@@ -218,9 +306,16 @@ def order(route: str, keyed_rows, position: int) -> list:
     OrderLS puts holders first, by ``contents(position).toLong`` descending; OrderSL puts the
     others first, then holders ascending. ``sortWith`` is stable, so equal keys keep the input
     order. (OrderSL's comparator is not strict between two non-holders — ``lt`` is true both
-    ways — so the JVM's order among them is an artefact of TimSort; unpinned, kept stable here.)"""
+    ways — so the JVM's order among them is an artefact of TimSort; unpinned, kept stable here.)
+    The comparator parses only when both operands hold the position, and a sort compares every
+    pair of holders that end up adjacent: with two or more holders every holder's element is
+    parsed (one bad element → 500); a lone holder is never parsed."""
     rows = [(k, r) for k, r in keyed_rows if r is not None]
-    hold = [(k, java_long(r[position])) for k, r in rows if len(r) - 1 >= position]
+    holders = [(k, r) for k, r in rows if len(r) - 1 >= position]
+    if len(holders) >= 2:
+        hold = [(k, java_long(r[position])) for k, r in holders]
+    else:
+        hold = [(k, 0) for k, _ in holders]
     rest = [k for k, r in rows if len(r) - 1 < position]
     if route == "OrderLS":
         return [k for k, _ in sorted(hold, key=lambda kv: -kv[1])] + rest

@@ -141,6 +141,79 @@ def route_vectors(pk, rsa, rng):
     return out
 
 
+def _outcome(fn, *args, **kw):
+    """Route result as a fixture: the reply text / key list, or {"status": 404 | 500}."""
+    try:
+        r = fn(*args, **kw)
+    except homo.NotFound:
+        return {"status": 404}
+    except homo.ServerError:
+        return {"status": 500}
+    return sorted(r) if isinstance(r, set) else r
+
+
+def route_edge_vectors(pk, rsa):
+    """Route-level edge cases (VERDICT r01 "What's weak" 1): lazy nsqr / pubkey / bound parsing, out-of-
+    Long OPE rows, typed dedup, pairwise guards, even and tiny moduli, Unicode digits, Order's lazy
+    parse. Each case names its route and arguments; expected = the oracle's reply or status."""
+    nsq, n, xh = pk["nsquare"], rsa["n"], rsa["x509_hex"]
+    c = [homo.paillier_encrypt(m, r, pk) for m, r in ((5, 11), (7, 13), (9, 17))]
+    rc = [homo.rsa_encrypt(m, rsa) for m in (3, 5, 7)]
+    cases = []
+
+    def add(rname, args, fn, **kw):
+        cases.append({"route": rname, "args": args, "expected": _outcome(fn, **kw)})
+
+    one = [["0", str(c[0]), "z"]]
+    two = [["0", str(c[0]), "z"], ["1", str(c[1]), "z"]]
+    for rows, nsqr in ((one, "12x"), (two, "12x"), (two, "1"), (two, "0"), (two, "-77"), (two, "+" + str(nsq)),
+                       (two, str(nsq * 4)), (two, str(2 ** 128 * 3)), (two, "1" + "0" * 40)):
+        add("SumAll", {"rows": rows, "position": 1, "nsqr": nsqr}, homo.sum_all, rows=rows, position=1, nsqr=nsqr)
+    typed = [["a", 5, "z"], ["a", "5", "z"], ["a", 5, "z"], [True, "3", "z"], [1, "3", "z"]]
+    for pos in (1, 0):
+        add("SumAll", {"rows": typed, "position": pos, "nsqr": None}, homo.sum_all, rows=typed, position=pos, nsqr=None)
+        add("MultAll", {"rows": typed, "position": pos, "pubkey": None}, homo.mult_all, rows=typed, position=pos)
+    uni = [["x", "\u0663\u0661", "z"], ["y", "+\u0664", "z"], ["w", "-\uff15", "z"]]  # Arabic-Indic 31, 4; fullwidth 5
+    add("SumAll", {"rows": uni, "position": 1, "nsqr": None}, homo.sum_all, rows=uni, position=1, nsqr=None)
+    add("SumAll", {"rows": uni, "position": 1, "nsqr": "1000"}, homo.sum_all, rows=uni, position=1, nsqr="1000")
+    add("SumAll", {"rows": [["x", "\u00b2", "z"]], "position": 1, "nsqr": None}, homo.sum_all,
+        rows=[["x", "\u00b2", "z"]], position=1, nsqr=None)  # superscript two: isdigit, not a decimal digit
+    mrows1 = [["0", str(rc[0]), "z"]]
+    mrows = [["0", str(rc[0]), "z"], ["1", str(rc[1]), "z"], ["2", str(rc[2]), "z"]]
+    for rows, key in ((mrows, xh), (mrows1, "zz"), (mrows, "zz"), (mrows, xh[:-2]), (mrows, xh.upper()), (mrows1, None)):
+        add("MultAll", {"rows": rows, "position": 1, "pubkey": key}, homo.mult_all, rows=rows, position=1, pubkey=key)
+    s1, s2, s3 = ["0", str(c[0])], ["1", str(c[1]), "q"], ["2"]
+    for a_, b_, pos, nsqr in ((s1, s2, 1, str(nsq)), (s1, s2, 1, None), (s1, s3, 1, str(nsq)), (None, s2, 1, None),
+                              (s1, s1, 1, str(nsq)), (s2, s2, 2, None), (s1, s2, 1, "0")):
+        add("Sum", {"set1": a_, "set2": b_, "position": pos, "nsqr": nsqr}, homo.pair_sum, set1=a_, set2=b_,
+            position=pos, nsqr=nsqr)
+    r1, r2 = ["0", str(rc[0])], ["1", str(rc[1]), "q"]
+    for a_, b_, key in ((r1, r2, xh), (r1, r2, None), (r1, r2, "0g"), (r1, ["1"], xh)):
+        add("Mult", {"set1": a_, "set2": b_, "position": 1, "pubkey": key}, homo.pair_mult, set1=a_, set2=b_,
+            position=1, pubkey=key)
+    big = 2 ** 70 + 12345
+    srows = [("k0", [str(-big), "x"]), ("k1", [str(big), "x"]), ("k2", ["17", "x"]), ("k3", ["-17", "x"]),
+             ("k4", [str(2 ** 63 - 1), "x"]), ("k5", [str(-2 ** 63), "x"]), ("k6", ["5"]), ("k7", [42, "x"]),
+             ("k8", ["+0017", "x"]), ("k9", None)]
+    for route in ("SearchGt", "SearchGtEq", "SearchLt", "SearchLtEq"):
+        for bound in ("17", str(big), str(-big), str(2 ** 80), str(-2 ** 80), str(2 ** 63), str(-2 ** 63 - 1), "0"):
+            add(route, {"rows": srows, "position": 0, "value": bound}, homo.search, route=route, keyed_rows=srows,
+                position=0, value=bound)
+    lone = [("a", ["zz"]), ("b", [])]
+    bad = [("a", ["zz", "q"]), ("b", ["1", "q"])]
+    for route in ("SearchGt", "SearchLtEq"):
+        for rows, bound in ((lone, "bad"), (lone, "3"), (bad, "3"), ([("a", ["1", "q"])], "bad"), ([], "bad")):
+            add(route, {"rows": rows, "position": 0, "value": bound}, homo.search, route=route, keyed_rows=rows,
+                position=0, value=bound)
+    orows = [("a", ["5"]), ("b", []), ("c", ["-3"]), ("d", ["5"]), ("e", None), ("g", ["+7"])]
+    for route in ("OrderLS", "OrderSL"):
+        for rows, pos in ((orows, 0), ([("a", ["x"]), ("b", [])], 0), ([("a", [5]), ("b", ["6"])], 0),
+                          ([("a", [5]), ("b", [])], 0), ([("a", [str(2 ** 64)]), ("b", ["1"])], 0),
+                          ([("a", ["1", "2"]), ("b", ["3"])], 1)):
+            add(route, {"rows": rows, "position": pos}, homo.order, route=route, keyed_rows=rows, position=pos)
+    return cases
+
+
 def main():
     os.makedirs(GOLDEN, exist_ok=True)
     kpath = os.path.join(GOLDEN, "keys.json")
@@ -164,6 +237,7 @@ def main():
         "edges_n1024": edge_vectors(rsa1024["n"], rng),
         "edges_nsq3072": edge_vectors(pk3072["nsquare"], rng),
         "routes": route_vectors(pk2048, rsa1024, rng),
+        "route_edges": route_edge_vectors(pk2048, rsa1024),
     }
     json.dump(vec, open(os.path.join(GOLDEN, "vectors.json"), "w"), indent=1)
     print("wrote", kpath, os.path.join(GOLDEN, "vectors.json"))

@@ -36,7 +36,7 @@ def test_strerror_and_limits():
     lib = ddshe._lib
     assert lib.dds_strerror(0) == b"ok"
     assert lib.dds_strerror(ddshe.DDS_E_EMPTY).startswith(b"no operand")
-    assert lib.dds_max_modulus_bits() >= 6146  # 3072-bit Paillier n^2 (BASELINE.json config 4)
+    assert lib.dds_max_modulus_bits() >= 16384  # JDK RSA limit; 8192-bit n^2 of a 4096-bit Paillier key
 
 
 def test_ctx_create_without_gpu_fails_cleanly():

@@ -141,11 +141,10 @@ def test_fold_operand_too_wide_is_range_error(eng):
     assert ei.value.status == ddshe.DDS_E_RANGE
 
 
-def test_even_modulus_rejected(eng):
-    import ddshe
-    with pytest.raises(ddshe.DDSError) as ei:
-        eng.modmul_fold(1 << 100, [3, 5])
-    assert ei.value.status == ddshe.DDS_E_ARG
+def test_even_modulus_folds_like_biginteger(eng):
+    """Round 1 refused even moduli; BigInteger.mod takes any positive modulus (see test_gpu_moduli.py)."""
+    assert eng.modmul_fold(1 << 100, [3, 5]) == 15
+    assert eng.modmul_fold(1 << 100, [1 << 99, 6]) == 0
 
 
 def test_pairs_random(eng, keys):

@@ -204,8 +204,11 @@ def test_order_route_semantics():
     assert homo.order("OrderLS", [r for r in rows if r[0] != "f"], 0) == ["g", "a", "d", "c", "b"]
     assert homo.order("OrderSL", [r for r in rows if r[0] != "f"], 0) == ["b", "c", "a", "d", "g"]
     assert homo.order("OrderSL", rows, 1) == ["a", "b", "c", "d", "g", "f"]  # only f holds position 1
-    with pytest.raises(ValueError):
+    with pytest.raises(homo.ServerError):
         homo.order("OrderLS", rows, 0)                                   # "x".toLong
+    assert homo.order("OrderLS", [("a", ["x"]), ("b", [])], 0) == ["a", "b"]  # lone holder: never parsed
+    with pytest.raises(homo.ServerError):
+        homo.order("OrderSL", [("a", [5]), ("b", ["6"])], 0)             # Int element: ClassCastException
 
 
 def test_openssl_baselines_match_oracle(keys):
@@ -225,3 +228,74 @@ def test_openssl_baselines_match_oracle(keys):
     ms = [rng.randrange(10000) for _ in range(6)]
     rs = [rng.randrange(1, k["n"]) for _ in ms]
     assert cref.bn_paillier_encrypt(k["n"], k["g"], ms, rs, 2) == [homo.paillier_encrypt(m, r, k) for m, r in zip(ms, rs)]
+
+
+def _oracle_outcome(c):
+    a, r = c["args"], c["route"]
+    try:
+        if r == "SumAll":
+            out = homo.sum_all(a["rows"], a["position"], a["nsqr"])
+        elif r == "MultAll":
+            out = homo.mult_all(a["rows"], a["position"], pubkey=a["pubkey"])
+        elif r == "Sum":
+            out = homo.pair_sum(a["set1"], a["set2"], a["position"], a["nsqr"])
+        elif r == "Mult":
+            out = homo.pair_mult(a["set1"], a["set2"], a["position"], pubkey=a["pubkey"])
+        elif r.startswith("Search"):
+            out = sorted(homo.search(r, [(k, row) for k, row in a["rows"]], a["position"], a["value"]))
+        else:
+            out = homo.order(r, [(k, row) for k, row in a["rows"]], a["position"])
+    except homo.NotFound:
+        return {"status": 404}
+    except homo.ServerError:
+        return {"status": 500}
+    return out
+
+
+def test_route_edge_vectors_recompute(vectors):
+    """The route edge fixtures are what the oracle answers (guards against fixture/oracle drift)."""
+    for c in vectors["route_edges"]:
+        assert _oracle_outcome(c) == c["expected"], (c["route"], str(c["args"])[:120])
+
+
+def test_route_edge_semantics_unit(keys):
+    """Hand-checked reference behaviours behind the fixtures (DDSRestServer.scala line cited)."""
+    # nsqr parsed only for the second and later operands (:416-422)
+    assert homo.sum_all([["0", "77", "z"]], 1, "not-a-number") == "77"
+    with pytest.raises(homo.ServerError):
+        homo.sum_all([["0", "77", "z"], ["1", "5", "z"]], 1, "not-a-number")
+    # any positive modulus: BigInteger.mod (:423); m <= 0 -> ArithmeticException (500)
+    assert homo.sum_all([["0", "77", "z"], ["1", "5", "z"]], 1, "64") == str(77 * 5 % 64)
+    assert homo.sum_all([["0", "77", "z"], ["1", "5", "z"]], 1, "1") == "0"
+    with pytest.raises(homo.ServerError):
+        homo.sum_all([["0", "77", "z"], ["1", "5", "z"]], 1, "0")
+    # the Search bound is parsed only for a row that passes the strict guard (:702-704)
+    assert homo.search("SearchGt", [("a", ["5"])], 0, "junk") == set()
+    with pytest.raises(homo.ServerError):
+        homo.search("SearchGt", [("a", ["5", "x"])], 0, "junk")
+    # rows outside Long compare as BigIntegers (:704)
+    assert homo.search("SearchGt", [("a", [str(2 ** 80), "x"]), ("b", ["3", "x"])], 0, "4") == {"a"}
+    # typed dedup: Int 5 and String "5" are different DDSSets (:401-403, DDSJsonProtocol.scala:22-28)
+    assert homo.sum_all([["a", 5, "z"], ["a", "5", "z"]], 1, None) == "10"
+    assert homo.sum_all([["a", "5", "z"], ["a", "5", "z"]], 1, None) == "5"
+    # Unicode decimal digits (Character.digit); a superscript two is not one
+    assert homo.java_biginteger("\u0664\u0662") == 42
+    with pytest.raises(homo.ServerError):
+        homo.java_biginteger("\u00b2")
+    # pubkey decoded only when a second operand exists (:515-517)
+    assert homo.mult_all([["0", "9", "z"]], 1, pubkey="zz") == "9"
+    n = keys["rsa1024_committed"]["n"]
+    assert homo.rsa_modulus_from_pubkey_hex(keys["rsa1024_committed"]["x509_hex"]) == n
+
+
+def test_x509_product_decoder_matches_oracle(keys):
+    """ddshe.x509 (product) and the oracle decode the same pubkeys and reject the same junk."""
+    from ddshe import x509
+    xh = keys["rsa1024_committed"]["x509_hex"]
+    assert x509.rsa_modulus(xh) == homo.rsa_modulus_from_pubkey_hex(xh) == keys["rsa1024_committed"]["n"]
+    assert x509.rsa_modulus(xh.upper()) == keys["rsa1024_committed"]["n"]
+    for junk in ("", "0", "zz", xh[:-2], xh[:40], "3000", xh[:2] + "ff" + xh[4:]):
+        with pytest.raises(ValueError):
+            x509.rsa_modulus(junk)
+        with pytest.raises(homo.ServerError):
+            homo.rsa_modulus_from_pubkey_hex(junk)
