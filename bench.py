@@ -87,6 +87,10 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="sum: skip the host-boundary (PCIe/decimal) rates")
     ap.add_argument("--e2e-dec-rows", type=int, default=1_000_000, help="sum: decimal-route sample rows")
     ap.add_argument("--verify", type=int, default=1, help="check the result on rank 0")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="sum: skip the extra lines (configs 3 and 4, latency, strong scaling, one-process multi-GPU)")
+    ap.add_argument("--strong-rows", type=int, default=10_000_000,
+                    help="rows of the strong-scaling and one-process multi-GPU lines (the north-star config)")
     args = ap.parse_args()
     dflt = {"sum": (10_000_000, 20, 3, 2), "product_filter": (10_000_000, 10, 2, 3),
             "encrypt_sum": (1_000_000, 2, 1, 4), "order": (10_000_000, 10, 2, 3),
@@ -155,15 +159,24 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
+    # extra lines measured by every rank together (collectives inside), before rank 0 reports
+    extra = wl.extra_distributed() if not args.no_extras else {}
     out = None
     if rank == 0:
         out = wl.report(res, elapsed)
         out["fill_s"] = t_fill
+        out.update(extra)
+    wl.close()
+    if not args.no_extras:
+        if rank == 0:
+            out.update(wl.extra_rank0())
+        if world > 1:
+            dist.barrier()
+    if rank == 0:
         print(json.dumps(out))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    wl.close()
     eng.close()
     return out
 
@@ -175,15 +188,45 @@ class _Workload:
     def reset_timers(self):
         pass
 
-    def fold_or_combine(self, col, modulus):
-        """One SumAll/MultAll fold over this rank's rows; N > 1: partial, RCCL gather, combine on rank 0."""
+    def extra_distributed(self):
+        return {}
+
+    def extra_rank0(self):
+        return {}
+
+    def fold_or_combine(self, col, modulus, count=None, rows_all=None):
+        """One SumAll/MultAll fold over this rank's rows [0, count); N > 1: the partial is folded into a
+        device tensor, all-gathered device-to-device (RCCL over xGMI) and combined on rank 0's GPU."""
+        count = len(col) if count is None else count
         if self.world == 1:
-            return col.fold()
-        part, rows = col.fold_partial()
-        parts, rows_all = self.ddist.gather_partials(part, rows, device=self.coll_dev)
+            return col.fold(0, count)
+        gathered = self.ddist.gather_partials_device(col, 0, count, self.coll_dev)
         if self.rank != 0:
             return None
-        return self.eng.combine_partials(modulus, parts, rows_all)
+        rows_all = rows_all if rows_all is not None else [self.per] * self.world
+        return self.eng.combine_partials_device(modulus, gathered.data_ptr(), rows_all)
+
+    def timed(self, step, steps, warmup):
+        """warmup + `steps` timed calls of step() bracketed by barrier + sync; max over ranks."""
+        torch = self.torch
+        import torch.distributed as dist
+        for _ in range(warmup):
+            res = step()
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            res = step()
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if self.world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device=self.coll_dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return res, el
 
     def fold_roofline(self, s32):
         """Dominant kernel (first fold level) from HIP events on its launch stream."""
@@ -221,6 +264,7 @@ class SumWorkload(_Workload):
         if self.mine:
             self.col.fill_paillier_synth(self.key["n"], self.key["g"], self.args.seed, self.row0, self.mine,
                                          self.args.pool)
+        self.col_sample = self.col.read(0, min(self.mine, 256)) if self.mine else []
 
     def step(self):
         return self.fold_or_combine(self.col, self.nsq)
@@ -259,8 +303,130 @@ class SumWorkload(_Workload):
                           "paillier_sumall_fold_10M_2048bit",
                           {"key_bits": key["n"].bit_length(), "modulus_bits": nsq.bit_length()})
         out.update(data="synthetic (seeded Paillier ciphertexts, committed key)", roofline=roof, cpu_baseline=cpu,
-                   end_to_end=e2e, verified=ok)
+                   end_to_end=e2e, verified=ok,
+                   fold_tail_ms=elapsed / a.steps * 1e3 - roof["avg_launch_ms"] if roof["achieved"] else None)
         return out
+
+    def extra_distributed(self):
+        """N > 1: the strong-scaling line of the north-star config — args.strong_rows rows over all
+        ranks (each folds the first shard_range rows of its resident column), partials moved
+        device-to-device and combined on rank 0's GPU."""
+        if self.world == 1:
+            return {}
+        a = self.args
+        cnts = [self.ddist.shard_range(a.strong_rows, self.world, r)[1] for r in range(self.world)]
+        if max(cnts) > self.mine:
+            return {"strong": {"skipped": "fewer resident rows per rank than the strong shard"}}
+        res, el = self.timed(lambda: self.fold_or_combine(self.col, self.nsq, cnts[self.rank], cnts), a.steps,
+                             a.warmup)
+        if self.rank != 0:
+            return {}
+        ok = None
+        if a.verify:
+            from oracle import homo  # checker only
+            ms = sum(int(self.ddshe.synth_plaintexts(a.seed, r * self.per, c).astype("int64").sum())
+                     for r, c in enumerate(cnts))
+            ok = homo.paillier_decrypt(res, self.key) == ms % self.key["n"]
+        return {"strong": {"metric": "Paillier homomorphic adds/sec (2048-bit key, mod n^2), strong scaling",
+                           "value": (a.strong_rows - 1) * a.steps / el, "unit": "HomoAdd/s", "n_gpus": self.world,
+                           "rows": a.strong_rows, "steps": a.steps, "ms_per_step": el / a.steps * 1e3,
+                           "scaling": "strong", "verified": ok,
+                           "partials": "device-to-device: dds_col_fold_partial_device -> RCCL all_gather_into_tensor"
+                                       " -> dds_combine_partials_device"}}
+
+    def extra_rank0(self):
+        out = {"single_process_multi_gpu": self.single_process_line()}
+        if self.world == 1:
+            out["latency"] = self.latency_lines()
+            out["configs"] = run_extra_configs(self)
+        return out
+
+    def single_process_line(self):
+        """One process drives all N GPUs through the C-ABI's multi-device context (dds_mctx: the form
+        a JNA caller uses): args.strong_rows rows sharded in 64-row blocks, every shard folded on its
+        own GPU, partials copied device-to-device (xGMI peer copies) and combined on GPU 0."""
+        a, torch = self.args, self.torch
+        if torch.cuda.device_count() < self.world:
+            return {"skipped": f"{torch.cuda.device_count()} visible devices < {self.world}"}
+        k, rows = self.key, a.strong_rows
+        m = self.ddshe.MultiEngine(list(range(self.world)))
+        col = m.column(self.nsq, rows)
+        col.fill_paillier_synth(k["n"], k["g"], a.seed, rows, a.pool)
+        for _ in range(a.warmup):
+            res = col.fold()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            res = col.fold()
+        el = time.perf_counter() - t0
+        ok = None
+        if a.verify:
+            from oracle import homo  # checker only
+            ms = self.ddshe.synth_plaintexts(a.seed, 0, rows)
+            ok = homo.paillier_decrypt(res, k) == int(ms.astype("int64").sum()) % k["n"]
+        col.close()
+        m.close()
+        return {"metric": "Paillier homomorphic adds/sec (2048-bit key, mod n^2), one process, all GPUs",
+                "value": (rows - 1) * a.steps / el, "unit": "HomoAdd/s", "n_gpus": self.world, "rows": rows,
+                "steps": a.steps, "ms_per_step": el / a.steps * 1e3, "scaling": "strong", "verified": ok,
+                "path": "dds_mcol_fold: shard folds on their GPUs, hipMemcpyPeerAsync of the partials, combine on GPU 0"}
+
+    def latency_lines(self):
+        """Request latency (host wall clock per call, inputs resident / as the route holds them):
+        BASELINE.json config 1 (SumAll over 10k ciphertexts, 1024-bit key) through the resident column
+        and the decimal route entry point, the reference path (OpenSSL BN_mod_mul fold, 1 core) on the
+        same rows, and the pairwise /Sum route (DDSRestServer.scala:355-395) on the committed key."""
+        import numpy as np
+        from oracle import cref  # CPU reference timing only
+        eng = self.eng
+        k1 = load_keyset("paillier1024_seed1")
+        nsq1 = k1["nsquare"]
+        col = eng.column(nsq1, 10000)
+        col.fill_paillier_synth(k1["n"], k1["g"], 1, 0, 10000, 64)
+
+        def med(fn, reps):
+            ts = []
+            for _ in range(reps):
+                t = time.perf_counter()
+                r = fn()
+                ts.append(time.perf_counter() - t)
+            ts.sort()
+            return r, ts[len(ts) // 2] * 1e3, ts[int(len(ts) * 0.99)] * 1e3
+
+        eng.set_stream(None)  # latency of the engine's own streams (no torch stream sync in the call)
+        col.fold()
+        gpu, fold_ms, fold_p99 = med(col.fold, 50)
+        rows = [str(x) for x in col.read(0, 10000)]
+        dec, dec_ms, _ = med(lambda: eng.sum_all_dec(rows, str(nsq1)), 10)
+        mb = (nsq1.bit_length() + 7) // 8
+        buf = col.read_buffer(0, 10000).tobytes()
+        t = time.perf_counter()
+        ref = int.from_bytes(cref.bn_fold_be(nsq1.to_bytes(mb, "big"), buf, mb, 10000), "big")
+        cpu_ms = (time.perf_counter() - t) * 1e3
+        col.close()
+        k2 = self.key
+        a, b = (str(x) for x in (self.col_sample[0], self.col_sample[1]))
+        pair, pair_ms, pair_p99 = med(lambda: eng.sum_all_dec([a, b], str(k2["nsquare"])), 200)
+        rng = np.random.default_rng(5)
+        n_pairs = 65536
+        xa = [self.col_sample[i % len(self.col_sample)] for i in range(n_pairs)]
+        xb = [self.col_sample[(i * 7 + 3) % len(self.col_sample)] for i in range(n_pairs)]
+        eng.modmul_pairs(k2["nsquare"], xa[:64], xb[:64])
+        t = time.perf_counter()
+        pr = eng.modmul_pairs(k2["nsquare"], xa, xb)
+        pairs_s = n_pairs / (time.perf_counter() - t)
+        del rng
+        eng.set_stream(self.torch.cuda.current_stream().cuda_stream)
+        return {"config1_sumall_10k_1024bit": {
+                    "resident_fold_ms": fold_ms, "resident_fold_p99_ms": fold_p99, "decimal_route_ms": dec_ms,
+                    "cpu_reference_ms": cpu_ms, "cpu_kind": "OpenSSL BN_mod_mul fold, 1 core (oracle/csrc/bn_baseline.c)",
+                    "speedup_resident_vs_cpu": cpu_ms / fold_ms,
+                    "matches": gpu == ref and dec == str(ref)},
+                "pair_sum_route_2048bit": {"median_ms": pair_ms, "p99_ms": pair_p99,
+                                           "path": "dds_sum_all_dec with two operands (the /Sum route body)",
+                                           "matches": pair == str(int(a) * int(b) % k2["nsquare"])},
+                "pairs_batched_2048bit": {"pairs": n_pairs, "pairs_per_s": pairs_s,
+                                          "path": "dds_modmul_pairs (k_pairs), host buffers in and out",
+                                          "matches": pr[:4] == [x * y % k2["nsquare"] for x, y in zip(xa[:4], xb[:4])]}}
 
     def end_to_end(self, res):
         """Host-boundary rates, outside the timed region (never `value`): (1) the binary boundary
@@ -326,6 +492,38 @@ class SumWorkload(_Workload):
         self.col.close()
 
 
+def run_extra_configs(main_wl):
+    """BASELINE.json configs 3 and 4 in the default run (rank 0, N = 1): each workload with its own
+    defaults, its own warmup and timed steps, roofline and CPU baseline, reported as an extra key of the
+    headline line so the driver's BENCH record carries them."""
+    import copy
+    out = {}
+    for name, cls, rows, steps, warmup, seed in (("config3_product_filter", ProductFilterWorkload, 10_000_000, 10, 2, 3),
+                                                 ("config4_encrypt_sum", EncryptSumWorkload, 1_000_000, 2, 1, 4)):
+        a = copy.copy(main_wl.args)
+        a.rows, a.steps, a.warmup, a.seed, a.strong = rows, steps, warmup, seed, False
+        ctx = {k: getattr(main_wl, k) for k in ("coll_dev", "eng", "world", "rank", "local", "torch", "ddshe", "ddist")}
+        ctx.update(args=a, total=rows, row0=0, mine=rows, per=rows)
+        wl = cls(ctx)
+        wl.setup()
+        main_wl.torch.cuda.synchronize()
+        for _ in range(warmup):
+            res = wl.step()
+        main_wl.eng.set_timing(True)
+        main_wl.eng.reset_timing()
+        wl.reset_timers()
+        main_wl.torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            res = wl.step()
+        main_wl.torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        main_wl.eng.set_timing(False)
+        out[name] = wl.report(res, el)
+        wl.close()
+    return out
+
+
 def pmc_traffic(workload, kernels, per_step=False):
     """HBM bytes per call from the committed rocprofv3 PMC passes (10M rows): the sum over `kernels`
     of bytes per dispatch (times dispatches per call when per_step: the PMC run did one call)."""
@@ -370,6 +568,10 @@ class ProductFilterWorkload(_Workload):
         self.d_valid = torch.ones(max(1, self.mine), dtype=torch.uint8, device="cuda")
         self.d_out = torch.empty(max(1, self.mine), dtype=torch.int32, device="cuda")
         self.bound = int(self.ope_map[5000])
+        # the same OPE values as a resident column behind the C-ABI (dds_opecol: what a JNA caller holds)
+        self.opecol = self.eng.opecol(max(1, self.mine))
+        if self.mine:
+            self.opecol.append(self.ope_host)
         self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         self.fold_ms = self.filter_ms = 0.0
 
@@ -430,6 +632,19 @@ class ProductFilterWorkload(_Workload):
         out = self.common("RSA HomoMult product + OPE range filter rows/sec (2048-bit key)",
                           self.total * a.steps / elapsed, "rows/s", elapsed, "rsa_multall_plus_ope_filter_10M_2048bit",
                           {"key_bits": key["n"].bit_length(), "filters_per_step": 4})
+        # Search through the resident OPE column with host output (the JNA-shaped call: bound as text, row
+        # ids back in host memory), outside the timed region
+        res_ms, res_ok = [], True
+        for op, f in (("gt", np.greater), ("ge", np.greater_equal), ("lt", np.less), ("le", np.less_equal)):
+            for _ in range(3):
+                t = time.perf_counter()
+                ids = self.opecol.search(str(self.bound), op)
+                res_ms.append((time.perf_counter() - t) * 1e3)
+            if self.world == 1:
+                res_ok = res_ok and len(ids) == counts[op] and (len(ids) == 0 or bool(f(self.ope_host[ids], self.bound).all()))
+        res_ms.sort()
+        filt["resident_opecol_search"] = {"median_ms": res_ms[len(res_ms) // 2], "matches": res_ok,
+                                          "path": "dds_opecol_search (device filter + D2H of the matching row ids)"}
         out.update(data="synthetic (seeded RSA ciphertexts of U[1,10^4) plaintexts, seeded OPE map)",
                    roofline=roof, filter_roofline=filt, cpu_baseline=cpu, verified=ok,
                    fold_ms_per_step=self.fold_ms / a.steps, filter_ms_per_step=self.filter_ms / a.steps,
@@ -438,6 +653,7 @@ class ProductFilterWorkload(_Workload):
 
     def close(self):
         self.col.close()
+        self.opecol.close()
 
 
 class EncryptSumWorkload(_Workload):

@@ -119,6 +119,30 @@ int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_p
     if (int rc = upload_qp(mc->S2, &mc->dq)) return rc;
     mc->qbound = nq;
   }
+  // reduction-tree constants (ddshe_tree.hip), the class of the main shape's capacity
+  {
+    const Shape t3 = tree_shape((size_t)mc->W * S - 2);
+    if (!t3.S) return fail(DDS_E_UNSUPPORTED, "no tree shape");
+    mc->S3 = t3.S;
+    mc->W3 = t3.W;
+    const size_t k3 = (size_t)mc->W3 * mc->S3;
+    bn::Limbs inv{1};  // N^-1 mod 2^k3 by Newton: inv <- inv (2 - N inv), doubling the correct bits
+    const bn::Limbs two{2};
+    for (size_t ok = 1; ok < k3; ok *= 2) {
+      const bn::Limbs t = low_bits(bn::mul(N, inv), k3);
+      inv = low_bits(bn::mul(inv, low_bits(bn::sub(bn::add(bn::pow2(k3), two), t), k3)), k3);
+    }
+    bn::trim(inv);
+    const bn::Limbs np = bn::sub(bn::pow2(k3), inv);  // -N^-1 mod R3 (inv != 0: N odd)
+    std::vector<uint32_t> h3;
+    for (const bn::Limbs& v : {N, np, N, bn::add(N, N), bn::add(bn::add(N, N), N)}) {
+      const std::vector<uint32_t> r = bn::to_rw(v, mc->S3, mc->W3);
+      h3.insert(h3.end(), r.begin(), r.end());
+    }
+    if (hipMalloc(&mc->d3, h3.size() * 4) != hipSuccess) return fail(DDS_E_NOMEM, "const alloc");
+    if (hipMemcpy(mc->d3, h3.data(), h3.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(DDS_E_HIP, "const upload");
+  }
   if (fold_qp_enabled() && (size_t)mc->W * S >= bn::bit_length(nq) + 2) {
     if (int rc = upload_qp(S, &mc->dqm)) return rc;
     mc->qbound = nq;  // level-1 partials are then < 2N~ too
@@ -154,16 +178,37 @@ size_t max_fold_groups(dds_ctx* ctx, int S) {
   return (size_t)ctx->cus * bpc * (256 / pick_tpi(S));
 }
 
-// Partial of `count` rows (declared in ddshe_host.hpp):
-//   level 1 (throughput shape, G groups): group g holds prod_g * R^(1 - c_g)
-//   tree (tail shape, G-1 products):      multiplies by R2^-(G-1)
-int fold_partial_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
-                        size_t count, const uint32_t** part, size_t* part_stride, int64_t* E, const uint32_t* d_ids) {
+// The reduction tree after the first fold level (ddshe_tree.hip: one launch, workgroup-cooperative
+// Montgomery products). DDSHE_TREE=0 selects round 1's per-level launches (k_fold in the tail shape +
+// k_finalize), DDSHE_TREE=1 the tree, for A/B timing. DDSHE_TREE_DIRECT (rows, default 8192): folds up to that many rows skip
+// the first level and run the tree over the rows themselves.
+bool use_tree() {  // off until it measures faster than the per-level launches (tools/tree_ab.py)
+  static const bool on = [] {
+    const char* e = getenv("DDSHE_TREE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+size_t tree_direct_rows() {
+  static const size_t n = [] {
+    const char* e = getenv("DDSHE_TREE_DIRECT");
+    return e ? (size_t)atoll(e) : (size_t)8192;
+  }();
+  return n;
+}
+
+// Level 1 (throughput shape, G groups: group g holds prod_g * R^(1 - c_g)) over `count` rows of X (or
+// rows d_ids[0..count)), unless the fold is small enough for the tree alone.
+int fold_level1(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
+                size_t count, const uint32_t* d_ids, Leaves* lv) {
   const int S = mc.S, S2 = mc.S2;
+  if (use_tree() && count <= tree_direct_rows()) {
+    *lv = Leaves{X, xstride, S, mc.W, count, 0, d_ids};
+    return DDS_OK;
+  }
   size_t G = std::min(max_fold_groups(ctx, S), std::max<size_t>(1, count / 2));
   size_t ps = round_up(G, 64);
   HIP_TRY(w->p0.ensure((size_t)S2 * ps * 4));
-  HIP_TRY(w->p1.ensure((size_t)S2 * round_up((G + 1) / 2, 64) * 4));
   record_time(ctx, w, st, true, 0);
   HIP_TRY(launch_fold(S, X, xstride, count, mc.d, mc.dqm, mc.n0, w->p0.as<uint32_t>(), ps, G, S2, st, d_ids));
   record_time(ctx, w, st, false, 0);
@@ -173,20 +218,94 @@ int fold_partial_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, 
     std::lock_guard<std::mutex> lk(ctx->tmu);
     ctx->pending_modmuls = count > G ? count - G : 0;
   }
-  uint32_t* cur = w->p0.as<uint32_t>();
-  uint32_t* nxt = w->p1.as<uint32_t>();
-  size_t n = G, cs = ps;
-  while (n > 1) {
-    size_t ng = (n + 1) / 2, ns = round_up(ng, 64);
-    HIP_TRY(launch_fold_tail(S2, cur, cs, n, mc.d2, mc.dq, mc.n0, nxt, ns, ng, st));
-    std::swap(cur, nxt);
-    n = ng;
-    cs = ns;
-  }
-  *part = cur;
-  *part_stride = cs;
-  *E = mc.wS() * ((int64_t)G - (int64_t)count) - mc.wS2() * ((int64_t)G - 1);
+  *lv = Leaves{w->p0.as<uint32_t>(), ps, S2, mc.W, G, mc.wS() * ((int64_t)G - (int64_t)count), nullptr};
   return DDS_OK;
+}
+
+// Reduce n leaves holding prod * 2^Ein to the canonical product (finalize: *value; synchronises the
+// stream) or to a canonical partial (S2 limbs of W bits, consecutive, at *part; exponent *Eout).
+int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const Leaves& lv, bool finalize,
+                  bn::Limbs* value, const uint32_t** part, int64_t* Eout) {
+  const int S2 = mc.S2;
+  if (!use_tree()) {  // round 1: one launch per level in the tail shape, then k_finalize
+    if (lv.Sin != S2 || lv.ids) return fail(DDS_E_ARG, "tail levels need leaves in the tail shape");
+    HIP_TRY(w->p1.ensure((size_t)S2 * round_up((lv.n + 1) / 2, 64) * 4));
+    HIP_TRY(w->x2.ensure((size_t)S2 * round_up((lv.n + 1) / 2, 64) * 4));
+    const uint32_t* cur = lv.X;
+    uint32_t* bufs[2] = {w->p1.as<uint32_t>(), w->x2.as<uint32_t>()};
+    size_t n = lv.n, cs = lv.xs;
+    int flip = 0;
+    while (n > 1) {
+      size_t ng = (n + 1) / 2, ns = round_up(ng, 64);
+      HIP_TRY(launch_fold_tail(S2, cur, cs, n, mc.d2, mc.dq, mc.n0, bufs[flip], ns, ng, st));
+      cur = bufs[flip];
+      flip ^= 1;
+      n = ng;
+      cs = ns;
+    }
+    const int64_t E = lv.E - mc.wS2() * ((int64_t)lv.n - 1);
+    if (!finalize) {  // partial: S2 limbs at stride cs -> consecutive
+      HIP_TRY(w->out.ensure((size_t)S2 * 4));
+      HIP_TRY(launch_strided_copy(cur, 0, cs, w->out.as<uint32_t>(), 0, 1, 1, S2, st));
+      *part = w->out.as<uint32_t>();
+      *Eout = E;
+      return DDS_OK;
+    }
+    const std::vector<uint32_t> y = mc.y_for(E);  // local copy outlives the async H2D (synced below)
+    HIP_TRY(w->y.ensure((size_t)S2 * 4));
+    HIP_TRY(w->out.ensure((size_t)S2 * 4));
+    HIP_TRY(hipMemcpyAsync(w->y.p, y.data(), (size_t)S2 * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_finalize_tail(S2, cur, cs, mc.d2, w->y.as<uint32_t>(), mc.n0, w->out.as<uint32_t>(), st));
+    std::vector<uint32_t> res(S2);
+    HIP_TRY(hipMemcpyAsync(res.data(), w->out.p, (size_t)S2 * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    account_fold(ctx, w);
+    *value = mc.value2(res.data());
+    return DDS_OK;
+  }
+  const int S3 = mc.S3;
+  const int64_t E = lv.E - mc.wS3() * ((int64_t)lv.n - 1);  // n-1 tree products, R3^-1 each
+  // nodes (2n + 2 rows) + two level buffers (n rows each, multi-launch trees) + flags (2n + 2 words)
+  HIP_TRY(w->tree.ensure(((4 * lv.n + 2) * (size_t)S3 + 2 * lv.n + 2) * 4));
+  uint32_t* nodes = w->tree.as<uint32_t>();
+  uint32_t* tflags = nodes + (4 * lv.n + 2) * (size_t)S3;
+  HIP_TRY(w->out.ensure((size_t)std::max(S2, S3) * 4));
+  std::vector<uint32_t> y;
+  if (finalize) {
+    y = mc.y3_for(E);  // local copy outlives the async H2D (synced below)
+    HIP_TRY(w->y.ensure((size_t)S3 * 4));
+    HIP_TRY(hipMemcpyAsync(w->y.p, y.data(), (size_t)S3 * 4, hipMemcpyHostToDevice, st));
+  }
+  HIP_TRY(launch_tree(S3, lv.X, lv.xs, lv.Sin, lv.Win, lv.n, lv.ids, mc.d3, finalize ? w->y.as<uint32_t>() : nullptr,
+                      nodes, tflags, w->out.as<uint32_t>(), S2, mc.W, st));
+  if (!finalize) {
+    *part = w->out.as<uint32_t>();
+    *Eout = E;
+    return DDS_OK;
+  }
+  std::vector<uint32_t> res(S3);
+  HIP_TRY(hipMemcpyAsync(res.data(), w->out.p, (size_t)S3 * 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  account_fold(ctx, w);
+  *value = bn::from_rw(res.data(), S3, mc.W3);
+  return DDS_OK;
+}
+
+int fold_partial_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
+                        size_t count, const uint32_t** part, size_t* part_stride, int64_t* E, const uint32_t* d_ids) {
+  Leaves lv;
+  int rc = fold_level1(ctx, w, st, mc, X, xstride, count, d_ids, &lv);
+  if (rc) return rc;
+  *part_stride = 1;
+  return reduce_leaves(ctx, w, st, mc, lv, false, nullptr, part, E);
+}
+
+int fold_value_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
+                      size_t count, const uint32_t* d_ids, bn::Limbs* value) {
+  Leaves lv;
+  int rc = fold_level1(ctx, w, st, mc, X, xstride, count, d_ids, &lv);
+  if (rc) return rc;
+  return reduce_leaves(ctx, w, st, mc, lv, true, value, nullptr, nullptr);
 }
 
 // after the stream has synchronised: account the timed first-level fold launch, if any
@@ -200,22 +319,6 @@ void account_fold(dds_ctx* ctx, Worker* w) {
     ctx->fold_launches += 1;
     ctx->fold_modmuls += ctx->pending_modmuls;
   }
-}
-
-// canonical prod from a tail-shape partial holding prod * 2^E
-int finalize_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* part, size_t pstride,
-                    int64_t E, std::vector<uint32_t>* result_rw) {
-  const int S2 = mc.S2;
-  const std::vector<uint32_t> y = mc.y_for(E);  // local copy outlives the async H2D (synced below)
-  HIP_TRY(w->y.ensure((size_t)S2 * 4));
-  HIP_TRY(w->out.ensure((size_t)S2 * 4));
-  HIP_TRY(hipMemcpyAsync(w->y.p, y.data(), (size_t)S2 * 4, hipMemcpyHostToDevice, st));
-  HIP_TRY(launch_finalize_tail(S2, part, pstride, mc.d2, w->y.as<uint32_t>(), mc.n0, w->out.as<uint32_t>(), st));
-  result_rw->assign(S2, 0);
-  HIP_TRY(hipMemcpyAsync(result_rw->data(), w->out.p, (size_t)S2 * 4, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  account_fold(ctx, w);
-  return DDS_OK;
 }
 
 int emit_be(const bn::Limbs& v, size_t width, uint8_t* out, size_t out_cap, size_t* out_len) {
@@ -433,13 +536,9 @@ int modmul_fold_be(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, size_t
   const size_t stride = round_up(count, 64);
   HIP_TRY(w->x.ensure((size_t)mc->S * stride * 4));
   if ((rc = ingest(ctx, w, wl.st, *mc, ops, width, count, w->in, w->x.as<uint32_t>(), stride))) return rc;
-  const uint32_t* part;
-  size_t ps;
-  int64_t E;
-  if ((rc = fold_partial_device(ctx, w, wl.st, *mc, w->x.as<uint32_t>(), stride, count, &part, &ps, &E))) return rc;
-  std::vector<uint32_t> res;
-  if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, E, &res))) return rc;
-  return emit_be(mc->value2(res.data()), mod_bytes, out, out_cap, out_len);
+  bn::Limbs v;
+  if ((rc = fold_value_device(ctx, w, wl.st, *mc, w->x.as<uint32_t>(), stride, count, nullptr, &v))) return rc;
+  return emit_be(v, mod_bytes, out, out_cap, out_len);
 }
 
 // Product of `count` rows of radix-2^16 limbs (h: count x len u32 words, row-major) on the GPU product
@@ -593,7 +692,7 @@ int combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, cons
   // the tree kernels' lazy-accumulation bound needs fully normalised limbs and a value below the
   // bound the fold leaves its partials under (2N~ when a QP shape is used, else 2N): reject the rest
   const bn::Limbs bound = bn::add(mc->qbound, mc->qbound);
-  int64_t E = -mc->wS2() * ((int64_t)nparts - 1);  // the tree below multiplies by R2^-(n-1)
+  int64_t E = 0;  // sum of the partials' exponents (reduce_leaves accounts for its own products)
   for (size_t i = 0; i < nparts; ++i) {
     const uint32_t* pl = h_parts + i * pw;
     for (size_t l = 0; l < S2; ++l)
@@ -603,8 +702,6 @@ int combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, cons
   }
   const size_t stride = round_up(nparts, 64);
   HIP_TRY(w->x.ensure(S2 * stride * 4));
-  HIP_TRY(w->p0.ensure(S2 * stride * 4));
-  HIP_TRY(w->p1.ensure(S2 * stride * 4));
   std::vector<uint32_t> h;
   if (d_parts) {
     HIP_TRY(launch_strided_copy(d_parts, pw, 1, w->x.as<uint32_t>(), 1, stride, nparts, S2, wl.st));
@@ -614,21 +711,10 @@ int combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, cons
       for (size_t l = 0; l < S2; ++l) h[l * stride + i] = h_parts[i * pw + l];
     HIP_TRY(hipMemcpyAsync(w->x.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, wl.st));
   }
-  const uint32_t* cur = w->x.as<uint32_t>();
-  size_t n = nparts, cs = stride;
-  uint32_t* bufs[2] = {w->p0.as<uint32_t>(), w->p1.as<uint32_t>()};
-  int flip = 0;
-  while (n > 1) {
-    size_t ng = (n + 1) / 2, ns = round_up(ng, 64);
-    HIP_TRY(launch_fold_tail(mc->S2, cur, cs, n, mc->d2, mc->dq, mc->n0, bufs[flip], ns, ng, wl.st));
-    cur = bufs[flip];
-    flip ^= 1;
-    n = ng;
-    cs = ns;
-  }
-  std::vector<uint32_t> res;
-  if ((rc = finalize_device(ctx, w, wl.st, *mc, cur, cs, E, &res))) return rc;  // syncs: h may go
-  return emit_be(mc->value2(res.data()), mod_bytes, out, out_cap, out_len);
+  bn::Limbs v;
+  const Leaves lv{w->x.as<uint32_t>(), stride, (int)S2, mc->W, nparts, E, nullptr};
+  if ((rc = reduce_leaves(ctx, w, wl.st, *mc, lv, true, &v, nullptr, nullptr))) return rc;  // syncs: h may go
+  return emit_be(v, mod_bytes, out, out_cap, out_len);
 }
 
 // SumAll/MultAll over rows of a resident column (DDSRestServer.scala:412-430, 506-524): rows
@@ -673,16 +759,8 @@ int col_fold_value(dds_col* col, const uint64_t* row_ids, size_t first, size_t n
     HIP_TRY(hipMemcpyAsync(w->ids.p, ids32.data(), n * 4, hipMemcpyHostToDevice, wl.st));
     d_ids = w->ids.as<uint32_t>();
   }
-  const uint32_t* part;
-  size_t ps;
-  int64_t E;
-  if ((rc = fold_partial_device(col->ctx, w, wl.st, mc, col->d + (row_ids ? 0 : first), col->stride, n, &part, &ps,
-                                &E, d_ids)))
-    return rc;
-  std::vector<uint32_t> res;
-  if ((rc = finalize_device(col->ctx, w, wl.st, mc, part, ps, E, &res))) return rc;  // syncs: ids32 may go
-  *v = mc.value2(res.data());
-  return DDS_OK;
+  // synchronises: ids32 may go afterwards
+  return fold_value_device(col->ctx, w, wl.st, mc, col->d + (row_ids ? 0 : first), col->stride, n, d_ids, v);
 }
 
 }  // namespace host
@@ -2035,13 +2113,9 @@ int fold_dec_mod(dds_ctx* ctx, const char* const* values, size_t count, const ch
     HIP_TRY(hipMemcpy2DAsync(X + host_rows[k], stride * 4, fixed.data() + k * mc->S, 4, 4, (size_t)mc->S,
                              hipMemcpyHostToDevice, wl.st));
   if (!host_rows.empty()) HIP_TRY(hipStreamSynchronize(wl.st));
-  const uint32_t* part;
-  size_t ps;
-  int64_t E;
-  if ((rc = fold_partial_device(ctx, w, wl.st, *mc, X, stride, count, &part, &ps, &E))) return rc;
-  std::vector<uint32_t> res;
-  if ((rc = finalize_device(ctx, w, wl.st, *mc, part, ps, E, &res))) return rc;
-  return write_dec(bn::to_dec(mc->value2(res.data())), out, out_cap, out_len);
+  bn::Limbs v;
+  if ((rc = fold_value_device(ctx, w, wl.st, *mc, X, stride, count, nullptr, &v))) return rc;
+  return write_dec(bn::to_dec(v), out, out_cap, out_len);
 }
 
 int fold_dec(dds_ctx* ctx, const char* const* values, size_t count, const char* mod_dec, bool additive, char* out,

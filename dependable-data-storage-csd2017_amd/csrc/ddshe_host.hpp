@@ -84,6 +84,7 @@ struct Worker {
   bool timed_fold = false;  // ev[0]/ev[1] bracket a first-level fold launch not yet accounted
   DevBuf in, in2, x, x2, p0, p1, out, flags, y, misc, misc2, tab, ids;
   DevBuf pk, gather;         // multi-device fold: packed partial (shard side), gathered partials (combiner)
+  DevBuf tree;               // reduction tree: node values + arrival flags
   hipEvent_t ev_peer = {};   // shard partial copied to the combining device
   DevBuf crt[7];  // CRT encryption scratch (see encrypt_crt_device)
   hipEvent_t ev[4] = {};
@@ -118,6 +119,9 @@ struct ModConsts {
   uint32_t* d2 = nullptr;
   uint32_t* dq = nullptr;        // N~ = N·n0 in tail limbs (tail_qp shapes), else null
   uint32_t* dqm = nullptr;       // N~ in main limbs when R > 4N~ holds for the main shape, else null
+  int S3 = 0, W3 = 0;            // reduction-tree shape (ddshe_tree.hip), R3 = 2^(W3*S3)
+  uint32_t* d3 = nullptr;        // tree constants: N | n' = -N^-1 mod R3 | N | 2N | 3N
+  std::map<int64_t, std::vector<uint32_t>> y3cache;  // E -> 2^(W3*S3 - E) mod N, tree limbs
   std::mutex ymu;
   std::map<int64_t, std::vector<uint32_t>> ycache;  // E -> 2^(W*S2 - E) mod N, tail limbs
   // decimal codec table (k_dec_parse), built on first use: Pt[l*jpad + j] = limb l of 10^(8j)
@@ -130,6 +134,7 @@ struct ModConsts {
     if (d2) (void)hipFree(d2);
     if (dq) (void)hipFree(dq);
     if (dqm) (void)hipFree(dqm);
+    if (d3) (void)hipFree(d3);
     if (dtab) (void)hipFree(dtab);
   }
   std::vector<uint32_t> rw(const bn::Limbs& v) const { return bn::to_rw(v, S, W); }
@@ -149,6 +154,16 @@ struct ModConsts {
     bn::Limbs y = pow2((int64_t)W * S2 - E);
     return ycache.emplace(E, bn::to_rw(y, S2, W)).first->second;
   }
+  // finalize multiplier of the reduction tree for a root holding prod * 2^E (by value, as y_for)
+  std::vector<uint32_t> y3_for(int64_t E) {
+    std::lock_guard<std::mutex> lk(ymu);
+    auto it = y3cache.find(E);
+    if (it != y3cache.end()) return it->second;
+    if (y3cache.size() >= 64) y3cache.clear();
+    bn::Limbs y = pow2((int64_t)W3 * S3 - E);
+    return y3cache.emplace(E, bn::to_rw(y, S3, W3)).first->second;
+  }
+  int64_t wS3() const { return (int64_t)W3 * S3; }
   // bits of 2 contributed by one Montgomery product of the main / tail shape
   int64_t wS() const { return (int64_t)W * S; }
   int64_t wS2() const { return (int64_t)W * S2; }
@@ -363,15 +378,29 @@ int fold_even_modulus(dds_ctx* ctx, const bn::Limbs& M, const std::vector<bn::Li
 void record_time(dds_ctx* ctx, Worker* w, hipStream_t st, bool begin, int slot);
 int pick_tpi(int S);
 size_t max_fold_groups(dds_ctx* ctx, int S);
+// Leaves of the reduction tree: X[l * xs + g] (g = ids[k] when ids), l < Sin limbs of Win bits, holding
+// prod * 2^E over n leaves
+struct Leaves {
+  const uint32_t* X;
+  size_t xs;
+  int Sin, Win;
+  size_t n;
+  int64_t E;
+  const uint32_t* ids;
+};
+int fold_level1(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
+                size_t count, const uint32_t* d_ids, Leaves* lv);
+int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const Leaves& lv, bool finalize,
+                  bn::Limbs* value, const uint32_t** part, int64_t* Eout);
+// canonical product of `count` rows (rows d_ids[0..count) when given); synchronises the stream
+int fold_value_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
+                      size_t count, const uint32_t* d_ids, bn::Limbs* value);
 // Fold `count` rows of an rW column (rows ids[0..count) when d_ids != nullptr) into one un-finalised
 // partial: tail-shape limbs (row 0 of `*part`, stride `*part_stride`) holding prod(rows) * 2^(*E).
 int fold_partial_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
                         size_t count, const uint32_t** part, size_t* part_stride, int64_t* E,
                         const uint32_t* d_ids = nullptr);
 void account_fold(dds_ctx* ctx, Worker* w);
-// canonical prod from a tail-shape partial holding prod * 2^E (synchronises the stream)
-int finalize_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* part, size_t pstride,
-                    int64_t E, std::vector<uint32_t>* result_rw);
 int emit_be(const bn::Limbs& v, size_t width, uint8_t* out, size_t out_cap, size_t* out_len);
 // Upload `count` big-endian operands into an rW column (X, stride) validated against mc; rows >= 2N
 // are reduced on the GPU and, when `reduced` is given, listed there (ascending).

@@ -45,6 +45,15 @@ hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t cou
                             const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups,
                             hipStream_t st);
 bool tail_qp(int S);
+// Reduction tree (ddshe_tree.hip): S limbs of W bits (Shape.TPI unused) for a main shape of up to
+// mod_bits bits; one launch reduces nleaves leaves (limb-major X, Sin limbs of Win bits, stride xstride;
+// leaf g is row ids[g] when ids != nullptr) to the canonical result (Y != nullptr: S limbs of W bits,
+// times Y R^-1) or a canonical partial (Sout limbs of Wout bits). consts: N | n' | N | 2N | 3N.
+// nodes: 4 nleaves + 2 rows of S words (nodes + level buffers), flags: 2 nleaves + 2 words (zeroed here).
+Shape tree_shape(size_t mod_bits);
+hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Win, size_t nleaves, const uint32_t* ids,
+                       const uint32_t* consts, const uint32_t* Y, uint32_t* nodes, uint32_t* flags, uint32_t* out,
+                       int Sout, int Wout, hipStream_t st);
 hipError_t launch_finalize_tail(int S, const uint32_t* P, size_t pstride, const uint32_t* consts, const uint32_t* Y,
                                 uint32_t n0, uint32_t* out, hipStream_t st);
 hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stride, size_t count,

@@ -112,7 +112,7 @@ int mcol_fold(dds_mcol* mcol, const uint64_t* ids, size_t n, bn::Limbs* v, bool*
   uint32_t* gather = l0.w->gather.as<uint32_t>();
   std::vector<std::unique_ptr<WorkerLease>> ls;
   std::vector<std::vector<uint32_t>> ids32(G);  // alive until the final synchronisation
-  int64_t E = -mc0.wS2() * ((int64_t)na - 1);
+  int64_t E = 0;  // sum of the shard exponents (reduce_leaves accounts for its own products)
   for (size_t j = 0; j < na; ++j) {
     const size_t s = act[j];
     dds_col* col = mcol->cols[s];
@@ -145,25 +145,10 @@ int mcol_fold(dds_mcol* mcol, const uint64_t* ids, size_t n, bn::Limbs* v, bool*
   const size_t stride = round_up(na, 64);
   Worker* w0 = l0.w;
   HIP_TRY(w0->x.ensure(S2 * stride * 4));
-  HIP_TRY(w0->p0.ensure(S2 * stride * 4));
-  HIP_TRY(w0->p1.ensure(S2 * stride * 4));
   HIP_TRY(launch_strided_copy(gather, S2, 1, w0->x.as<uint32_t>(), 1, stride, na, S2, l0.st));
-  const uint32_t* cur = w0->x.as<uint32_t>();
-  size_t m = na, cstr = stride;
-  uint32_t* bufs[2] = {w0->p0.as<uint32_t>(), w0->p1.as<uint32_t>()};
-  int flip = 0;
-  while (m > 1) {
-    const size_t ng = (m + 1) / 2, ns = round_up(ng, 64);
-    HIP_TRY(launch_fold_tail(mc0.S2, cur, cstr, m, mc0.d2, mc0.dq, mc0.n0, bufs[flip], ns, ng, l0.st));
-    cur = bufs[flip];
-    flip ^= 1;
-    m = ng;
-    cstr = ns;
-  }
-  std::vector<uint32_t> res;
-  if ((rc = finalize_device(c0, w0, l0.st, mc0, cur, cstr, E, &res))) return rc;
+  const Leaves lv{w0->x.as<uint32_t>(), stride, (int)S2, mc0.W, na, E, nullptr};
+  if ((rc = reduce_leaves(c0, w0, l0.st, mc0, lv, true, v, nullptr, nullptr))) return rc;
   for (auto& l : ls) account_fold(l->ctx, l->w);
-  *v = mc0.value2(res.data());
   return DDS_OK;
 }
 

@@ -1,5 +1,6 @@
 """Multi-GPU orchestration of the fold: rows sharded by contiguous key range, one
 partial per rank, partials gathered to rank 0 and combined there.
+(One process driving all GPUs uses the C-ABI's dds_mctx instead: ddshe.MultiEngine.)
 
 Each rank's partial is the un-finalised Montgomery fold of its shard,
 v(S) = prod(S) * R^(1-|S|) mod N (S r27 words), plus its row count. Modular product
@@ -43,3 +44,21 @@ def gather_partials(part: np.ndarray, rows: int, device=None, group=None):
     dist.all_gather(bufs, t, group=group)
     mat = torch.stack(bufs).cpu().numpy()
     return unpack_partials(mat)
+
+
+def gather_partials_device(col, first: int, count: int, coll_dev, group=None):
+    """Device-to-device form: this rank's partial is folded straight into a device tensor
+    (dds_col_fold_partial_device), all-gathered (RCCL over xGMI when coll_dev is a GPU; the gloo
+    rehearsal stages through host memory) and returned as one device tensor of world x partial_words
+    words on this rank's GPU, ready for Engine.combine_partials_device. No host staging of the limbs
+    on the RCCL path."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    pw = col.partial_words
+    part = torch.empty(pw, dtype=torch.int32, device="cuda")
+    col.fold_partial_device(part.data_ptr(), first, count)
+    src = part if coll_dev.type == "cuda" else part.cpu()
+    out = torch.empty(world * pw, dtype=torch.int32, device=src.device)
+    dist.all_gather_into_tensor(out, src, group=group)
+    return out if out.is_cuda else out.to("cuda")

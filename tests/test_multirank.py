@@ -1,9 +1,9 @@
 """World-size-2 gloo test (CPU) of the multi-GPU fold orchestration: row sharding,
 the all-gather of per-rank partials and the partial algebra used by
 dds_combine_partials. Each rank's partial is restated from the engine's definition
-(dds_col_fold_partial): S2 = 160 radix-2^28 limbs holding prod * 2^E plus the signed
-exponent E in two words, where a fold with G first-level groups gives
-E = 28*148*(G - rows) - 28*160*(G - 1)."""
+(dds_col_fold_partial): S2 = 160 radix-2^28 limbs holding the canonical prod * 2^E mod N plus the
+signed exponent E in two words, where a fold with G first-level groups and the reduction tree
+(ddshe_tree.hip: 162 limbs of 26 bits) gives E = 28*148*(G - rows) - 26*162*(G - 1)."""
 import os
 import random
 
@@ -12,8 +12,8 @@ import torch.multiprocessing as mp
 
 from oracle import homo
 
-W, S, S2 = 28, 148, 160  # throughput / tail limb counts for a 4095-bit modulus
-WS, WS2 = W * S, W * S2
+W, S, S2 = 28, 148, 160  # throughput / partial limb counts for a 4095-bit modulus
+WS, WS2 = W * S, 26 * 162  # level-1 and reduction-tree Montgomery exponents
 
 
 def limbs(x):
