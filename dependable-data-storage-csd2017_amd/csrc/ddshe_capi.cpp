@@ -126,6 +126,8 @@ int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_p
     mc->S3 = t3.S;
     mc->W3 = t3.W;
     const size_t k3 = (size_t)mc->W3 * mc->S3;
+    // a tree product of raw rows a, b < 2^(W S) stays < 2N when a b / R3 < N (forced-wide shapes fail this)
+    mc->tree_direct = k3 + bn::bit_length(N) - 1 >= 2 * (size_t)mc->W * S;
     bn::Limbs inv{1};  // N^-1 mod 2^k3 by Newton: inv <- inv (2 - N inv), doubling the correct bits
     const bn::Limbs two{2};
     for (size_t ok = 1; ok < k3; ok *= 2) {
@@ -192,7 +194,17 @@ bool use_tree() {  // off until it measures faster than the per-level launches (
 size_t tree_direct_rows() {
   static const size_t n = [] {
     const char* e = getenv("DDSHE_TREE_DIRECT");
-    return e ? (size_t)atoll(e) : (size_t)8192;
+    return e ? (size_t)atoll(e) : (size_t)512;
+  }();
+  return n;
+}
+// DDSHE_TREE_SWITCH (leaves, default 512): wider levels run as tail-shape lane-group launches (many
+// products per launch: throughput), the last log2(switch) levels as tree launches (one workgroup per
+// product: latency)
+size_t tree_switch_leaves() {
+  static const size_t n = [] {
+    const char* e = getenv("DDSHE_TREE_SWITCH");
+    return e ? (size_t)atoll(e) : (size_t)512;
   }();
   return n;
 }
@@ -202,7 +214,7 @@ size_t tree_direct_rows() {
 int fold_level1(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
                 size_t count, const uint32_t* d_ids, Leaves* lv) {
   const int S = mc.S, S2 = mc.S2;
-  if (use_tree() && count <= tree_direct_rows()) {
+  if (use_tree() && mc.tree_direct && count <= tree_direct_rows()) {
     *lv = Leaves{X, xstride, S, mc.W, count, 0, d_ids};
     return DDS_OK;
   }
@@ -251,43 +263,66 @@ int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const 
       *Eout = E;
       return DDS_OK;
     }
-    const std::vector<uint32_t> y = mc.y_for(E);  // local copy outlives the async H2D (synced below)
+    uint32_t* hy = nullptr;  // pinned: [0, S2) Y, [S2, 2 S2) result
+    HIP_TRY(stage_ptr(w, &hy));
+    hy += kStageWord0;
+    {
+      const std::vector<uint32_t>& y = mc.y_for(E);
+      std::copy(y.begin(), y.end(), hy);
+    }
     HIP_TRY(w->y.ensure((size_t)S2 * 4));
     HIP_TRY(w->out.ensure((size_t)S2 * 4));
-    HIP_TRY(hipMemcpyAsync(w->y.p, y.data(), (size_t)S2 * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(w->y.p, hy, (size_t)S2 * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(launch_finalize_tail(S2, cur, cs, mc.d2, w->y.as<uint32_t>(), mc.n0, w->out.as<uint32_t>(), st));
-    std::vector<uint32_t> res(S2);
-    HIP_TRY(hipMemcpyAsync(res.data(), w->out.p, (size_t)S2 * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(hy + S2, w->out.p, (size_t)S2 * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     account_fold(ctx, w);
-    *value = mc.value2(res.data());
+    *value = mc.value2(hy + S2);
     return DDS_OK;
   }
-  const int S3 = mc.S3;
-  const int64_t E = lv.E - mc.wS3() * ((int64_t)lv.n - 1);  // n-1 tree products, R3^-1 each
-  // nodes (2n + 2 rows) + two level buffers (n rows each, multi-launch trees) + flags (2n + 2 words)
-  HIP_TRY(w->tree.ensure(((4 * lv.n + 2) * (size_t)S3 + 2 * lv.n + 2) * 4));
-  uint32_t* nodes = w->tree.as<uint32_t>();
-  uint32_t* tflags = nodes + (4 * lv.n + 2) * (size_t)S3;
-  HIP_TRY(w->out.ensure((size_t)std::max(S2, S3) * 4));
-  std::vector<uint32_t> y;
-  if (finalize) {
-    y = mc.y3_for(E);  // local copy outlives the async H2D (synced below)
-    HIP_TRY(w->y.ensure((size_t)S3 * 4));
-    HIP_TRY(hipMemcpyAsync(w->y.p, y.data(), (size_t)S3 * 4, hipMemcpyHostToDevice, st));
+  Leaves lt = lv;
+  if (lv.Sin == S2 && !lv.ids && lv.n > tree_switch_leaves()) {  // wide levels: tail-shape launches
+    HIP_TRY(w->p1.ensure((size_t)S2 * round_up((lv.n + 1) / 2, 64) * 4));
+    HIP_TRY(w->x2.ensure((size_t)S2 * round_up((lv.n + 1) / 2, 64) * 4));
+    uint32_t* bufs[2] = {w->p1.as<uint32_t>(), w->x2.as<uint32_t>()};
+    int flip = 0;
+    while (lt.n > tree_switch_leaves()) {
+      const size_t ng = (lt.n + 1) / 2, ns = round_up(ng, 64);
+      HIP_TRY(launch_fold_tail(S2, lt.X, lt.xs, lt.n, mc.d2, mc.dq, mc.n0, bufs[flip], ns, ng, st));
+      lt.E -= mc.wS2() * (int64_t)(lt.n - ng);  // n - ng products, R2^-1 each
+      lt.X = bufs[flip];
+      lt.xs = ns;
+      lt.n = ng;
+      flip ^= 1;
+    }
   }
-  HIP_TRY(launch_tree(S3, lv.X, lv.xs, lv.Sin, lv.Win, lv.n, lv.ids, mc.d3, finalize ? w->y.as<uint32_t>() : nullptr,
+  const int S3 = mc.S3;
+  const int64_t E = lt.E - mc.wS3() * ((int64_t)lt.n - 1);  // n-1 tree products, R3^-1 each
+  // nodes (2n + 2 rows) + two level buffers (n rows each, multi-launch trees) + flags (2n + 2 words)
+  HIP_TRY(w->tree.ensure(((4 * lt.n + 2) * (size_t)S3 + 2 * lt.n + 2) * 4));
+  uint32_t* nodes = w->tree.as<uint32_t>();
+  uint32_t* tflags = nodes + (4 * lt.n + 2) * (size_t)S3;
+  HIP_TRY(w->out.ensure((size_t)std::max(S2, S3) * 4));
+  uint32_t* hy = nullptr;  // pinned: [0, S3) Y, [S3, 2 S3) result
+  if (finalize) {
+    HIP_TRY(stage_ptr(w, &hy));
+    hy += kStageWord0;
+    const std::vector<uint32_t>& y = mc.y3_for(E);
+    std::copy(y.begin(), y.end(), hy);
+    HIP_TRY(w->y.ensure((size_t)S3 * 4));
+    HIP_TRY(hipMemcpyAsync(w->y.p, hy, (size_t)S3 * 4, hipMemcpyHostToDevice, st));
+  }
+  HIP_TRY(launch_tree(S3, lt.X, lt.xs, lt.Sin, lt.Win, lt.n, lt.ids, mc.d3, finalize ? w->y.as<uint32_t>() : nullptr,
                       nodes, tflags, w->out.as<uint32_t>(), S2, mc.W, st));
   if (!finalize) {
     *part = w->out.as<uint32_t>();
     *Eout = E;
     return DDS_OK;
   }
-  std::vector<uint32_t> res(S3);
-  HIP_TRY(hipMemcpyAsync(res.data(), w->out.p, (size_t)S3 * 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(hy + S3, w->out.p, (size_t)S3 * 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   account_fold(ctx, w);
-  *value = bn::from_rw(res.data(), S3, mc.W3);
+  *value = bn::from_rw(hy + S3, S3, mc.W3);
   return DDS_OK;
 }
 
@@ -366,8 +401,7 @@ int ingest(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint8_t
     }
   }
   uint32_t flags = 0;
-  HIP_TRY(hipMemcpyAsync(&flags, w->flags.p, 4, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
+  HIP_TRY(read_sync(w, st, w->flags.p, &flags, 4));
   if (flags & 2u) return fail(DDS_E_RANGE, "operand wider than the modulus limb width");
   if (flags & 1u) {
     HIP_TRY(launch_reduce_rows(mc.S, X, stride, count, mc.d, mc.n0, st));
@@ -506,8 +540,7 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
     b = e;
   }
   uint32_t fl = 0;
-  HIP_TRY(hipMemcpyAsync(&fl, w->flags.p, 4, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
+  HIP_TRY(read_sync(w, st, w->flags.p, &fl, 4));
   if (fl & (kDecNeg | kDecReduce))
     HIP_TRY(launch_dec_fix(mc.S, X, stride, count, w->rflags.as<uint8_t>(), mc.d, mc.n0, st));
   *orflags = fl;
@@ -566,8 +599,7 @@ int product_tree(dds_ctx* ctx, const std::vector<uint32_t>& h, size_t count, siz
       HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, wl.st));
       HIP_TRY(launch_bigmul_carry(v, pairs, outlen, u, w->flags.as<uint32_t>(), wl.st));
       uint32_t flag = 0;
-      HIP_TRY(hipMemcpyAsync(&flag, w->flags.p, 4, hipMemcpyDeviceToHost, wl.st));
-      HIP_TRY(hipStreamSynchronize(wl.st));
+      HIP_TRY(read_sync(w, wl.st, w->flags.p, &flag, 4));
       std::swap(u, v);
       if (!flag) break;
     }
@@ -1447,8 +1479,7 @@ int encrypt_crt_device(Worker* w, hipStream_t st, CrtKey& k, const bn::Limbs& g,
     HIP_TRY(launch_crt_out(mn.S, F, Gq, chunk, cc, mn.d, k.d + 2 * (size_t)mp.S, mn.n0, d_out + c0, ostride, st));
   }
   uint32_t flags = 0;
-  HIP_TRY(hipMemcpyAsync(&flags, fl, 4, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
+  HIP_TRY(read_sync(w, st, fl, &flags, 4));
   if (flags) return fail(DDS_E_RANGE, "r does not fit below 2^bits(n)");
   return DDS_OK;
 }
@@ -1766,9 +1797,8 @@ int dds_ope_filter_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_v
     record_time(ctx, w, wl.st, true, 2);
     HIP_TRY(launch_ope_filter(d_col, d_valid, n, bound, op, w->misc.p, w->flags.as<uint64_t>(), d_out, wl.st));
     record_time(ctx, w, wl.st, false, 2);
-    uint64_t total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, w->flags.p, 8, hipMemcpyDeviceToHost, wl.st));
-    HIP_TRY(hipStreamSynchronize(wl.st));
+    uint64_t total = 0;  // pinned readback: one small DMA, no staging copy
+    HIP_TRY(read_sync(w, wl.st, w->flags.p, &total, 8));
     if (ctx->timing.load()) {
       float ms = 0;
       if (hipEventElapsedTime(&ms, w->ev[2], w->ev[3]) == hipSuccess) {
@@ -1961,8 +1991,7 @@ int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values
   HIP_TRY(launch_flag_compact(flags, nrows, req, w->misc.p, w->flags.as<uint64_t>(), dst, wl.st));
   record_time(ctx, w, wl.st, false, 2);
   uint64_t total = 0;
-  HIP_TRY(hipMemcpyAsync(&total, w->flags.p, 8, hipMemcpyDeviceToHost, wl.st));
-  HIP_TRY(hipStreamSynchronize(wl.st));
+  HIP_TRY(read_sync(w, wl.st, w->flags.p, &total, 8));
   if (!device_out && total) HIP_TRY(hipMemcpy(out_rows, dst, total * 4, hipMemcpyDeviceToHost));
   if (ctx->timing.load()) {
     float ms = 0;

@@ -91,6 +91,7 @@ struct Worker {
   // decimal codec: double-buffered pinned chunks (chars, offsets), their device copies,
   // per-row status bytes, and the event after each slot's last use
   HostBuf hch[2], hoff[2];
+  HostBuf hstage;  // fold finalize: Y in, result out (pinned: no staging copies on the latency path)
   DevBuf dch[2], doff[2], rflags;
   hipEvent_t ev_dec[2] = {};
   ~Worker() {
@@ -120,6 +121,7 @@ struct ModConsts {
   uint32_t* dq = nullptr;        // N~ = N·n0 in tail limbs (tail_qp shapes), else null
   uint32_t* dqm = nullptr;       // N~ in main limbs when R > 4N~ holds for the main shape, else null
   int S3 = 0, W3 = 0;            // reduction-tree shape (ddshe_tree.hip), R3 = 2^(W3*S3)
+  bool tree_direct = false;      // raw rows (< 2^(W*S)) may be tree leaves: 2^(2WS) <= R3 * 2^(bits(N)-1)
   uint32_t* d3 = nullptr;        // tree constants: N | n' = -N^-1 mod R3 | N | 2N | 3N
   std::map<int64_t, std::vector<uint32_t>> y3cache;  // E -> 2^(W3*S3 - E) mod N, tree limbs
   std::mutex ymu;
@@ -217,6 +219,26 @@ struct dds_col {
 
 namespace ddshe {
 namespace host {
+
+// pinned staging of a worker (fixed 16 KiB, allocated once: pointers into it stay valid across a call):
+// bytes [0, 64) small readbacks (read_sync), words [16, 4096) the finalize Y and result
+constexpr size_t kStageBytes = 16384, kStageWord0 = 16;
+inline hipError_t stage_ptr(Worker* w, uint32_t** p) {
+  hipError_t e = w->hstage.ensure(kStageBytes);
+  *p = e == hipSuccess ? (uint32_t*)w->hstage.p : nullptr;
+  return e;
+}
+// copy `bytes` (<= 64) device -> host through the pinned slot and synchronise the stream
+inline hipError_t read_sync(Worker* w, hipStream_t st, const void* dsrc, void* dst, size_t bytes) {
+  uint32_t* h = nullptr;
+  hipError_t e = stage_ptr(w, &h);
+  if (e != hipSuccess) return e;
+  if (bytes > 64) return hipErrorInvalidValue;
+  if ((e = hipMemcpyAsync(h, dsrc, bytes, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+  memcpy(dst, h, bytes);
+  return hipSuccess;
+}
 
 struct WorkerLease {
   dds_ctx* ctx;

@@ -556,20 +556,35 @@ __global__ void __launch_bounds__(kOpeBlock) k_flag_count(const uint32_t* __rest
   }
 }
 
+// The tile's matches are ranked in row order (k*256 + tid), staged in LDS at their tile-local rank,
+// and written out by consecutive threads: full-line, coalesced stores instead of each thread writing
+// its own scattered run.
 __global__ void __launch_bounds__(kOpeBlock) k_ope_scatter(const uint32_t* __restrict__ masks,
                                                            const uint32_t* __restrict__ counts,
                                                            uint32_t* __restrict__ out, uint64_t* __restrict__ total) {
   constexpr int kWaves = kOpeBlock / 64;
   __shared__ uint32_t wtot[kOpeGroups][kWaves];
   __shared__ uint64_t s_part[kWaves];
+  __shared__ uint32_t sids[kOpeTile];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const uint64_t lt = (1ull << lane) - 1ull;
   const size_t tile = blockIdx.x;
   const size_t t0 = tile * kOpeTile + 4 * (size_t)tid;
   const uint32_t mask = masks[tile * kOpeBlock + tid];
   // exclusive prefix of this tile: sum of the counts of tiles [0, tile)
+  // (8 independent loads per thread and pass: one L2/MALL round trip per 2048 preceding tiles instead
+  // of one per 256 — the tiles' counts were written by other XCDs, so every load misses this L2)
   uint64_t pre = 0;
-  for (size_t t = tid; t < tile; t += kOpeBlock) pre += counts[t];
+  for (size_t base = 0; base < tile; base += 8 * kOpeBlock) {
+    uint32_t cv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const size_t t = base + (size_t)q * kOpeBlock + tid;
+      cv[q] = t < tile ? counts[t] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) pre += cv[q];
+  }
   for (int off = 32; off >= 1; off >>= 1) pre += (uint64_t)__shfl_xor((long long)pre, off);
   if (lane == 0) s_part[wid] = pre;
   // per group: matches of the lanes below me in my wave (4 bit-ballots), wave total
@@ -590,6 +605,7 @@ __global__ void __launch_bounds__(kOpeBlock) k_ope_scatter(const uint32_t* __res
   uint64_t off = 0;
 #pragma unroll
   for (int w = 0; w < kWaves; ++w) off += s_part[w];
+  uint32_t loc = 0;  // tile-local rank of the first match of group k
 #pragma unroll
   for (int k = 0; k < kOpeGroups; ++k) {
     uint32_t pw = 0, tot = 0;
@@ -599,13 +615,16 @@ __global__ void __launch_bounds__(kOpeBlock) k_ope_scatter(const uint32_t* __res
       tot += wtot[k][w];
     }
     const uint32_t q = (mask >> (4 * k)) & 0xFu;
-    uint64_t dst = off + pw + below[k];
+    uint32_t dst = loc + pw + below[k];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if ((q >> j) & 1u) out[dst++] = (uint32_t)(t0 + (size_t)k * 4 * kOpeBlock + j);
-    off += tot;
+      if ((q >> j) & 1u) sids[dst++] = (uint32_t)(t0 + (size_t)k * 4 * kOpeBlock + j);
+    loc += tot;
   }
-  if (tid == 0 && tile == gridDim.x - 1) *total = off;
+  __syncthreads();
+  uint32_t* o = out + off;
+  for (uint32_t k = tid; k < loc; k += kOpeBlock) o[k] = sids[k];
+  if (tid == 0 && tile == gridDim.x - 1) *total = off + loc;
 }
 
 // ------------------------------------------------------------------------------

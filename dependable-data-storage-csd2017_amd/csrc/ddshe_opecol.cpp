@@ -255,8 +255,7 @@ int dds_opecol_search(dds_opecol* col, const char* bound_dec, int op, uint32_t* 
                               w->out.as<uint32_t>(), wl.st, kSearch, kWide));
     record_time(ctx, w, wl.st, false, 2);
     uint64_t total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, w->flags.p, 8, hipMemcpyDeviceToHost, wl.st));
-    HIP_TRY(hipStreamSynchronize(wl.st));
+    HIP_TRY(read_sync(w, wl.st, w->flags.p, &total, 8));
     if (total) HIP_TRY(hipMemcpy(out_idx, w->out.p, total * 4, hipMemcpyDeviceToHost));
     if (ctx->timing.load()) {
       float ms = 0;

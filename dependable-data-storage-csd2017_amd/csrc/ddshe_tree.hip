@@ -3,7 +3,7 @@
 // 412-430 / 506-524; the tree replaces the per-level launches of round 1).
 //
 // Product ("SOS", separated operand scanning) on S limbs of W bits, R = 2^(W*S) >= 2^64 * N:
-//   T  = a * b                      column sums, 64-bit lazy (one workgroup, S column pairs)
+//   T  = a * b                      column sums, 64-bit lazy (one 1024-thread workgroup)
 //   d  = T mod R                    as W-bit pieces: d_p = lo(T_p) + mid(T_{p-1}) + hi(T_{p-2}) < 3*2^W
 //   m  = d * n' mod R               n' = -N^-1 mod R (full width), low-half column sums, split again
 //   V  = T + m * N                  column sums; V == 0 mod R
@@ -11,8 +11,8 @@
 //                                   ceil((V_{S-1} 2^2W + V_{S-2} 2^W + V_{S-3}) / 2^3W): the low half
 //                                   is an exact multiple of R and lower columns add < 2^-48
 //   two split passes give limbs < 2^W + 3 ("almost normalised")
-// No step of it is sequential over the limbs: 3 passes of S mads per thread, 9 barriers, instead of
-// S dependent CIOS steps. Bounds (static_assert): column sums < 7 S 2^2W < 2^64; any input below
+// No step of it is sequential over the limbs: three convolutions spread over the workgroup's 16 waves
+// (register-blocked, Sos::conv), 10 barriers, instead of S dependent CIOS steps. Bounds (static_assert): column sums < 7 S 2^2W < 2^64; any input below
 // 2^31 N (leaves from the QP levels are < 2N~ <= 2^29 N) gives U < N/4 + 3.0001 N < 4N.
 //
 // Tree: block b starts with leaves (2b, 2b+1) and walks up. A node's first-arriving child stores
@@ -28,7 +28,7 @@
 
 namespace ddshe {
 
-constexpr int kTreeThreads = 256;
+constexpr int kTreeThreads = 1024;
 
 template <int S, int W>
 struct Sos {
@@ -43,69 +43,86 @@ struct Sos {
     return v;
   }
 
-  // Column sums with wave-uniform loop bounds. y operands are zero-padded in LDS (yz[S + j] = y[j],
-  // yz[0..S) = yz[2S..3S) = 0), so a lane whose column does not contain a term reads a zero instead of
-  // leaving the loop: each wave runs S + 64 mads (regions A | B | C below) with scalar loop control.
-  // Full-product column pair of thread t (wave's first thread t0): c0 = col t, c1 = col S + t:
-  //   A: i < t0        every lane's term is in col t
-  //   B: t0 <= i < t0+64  both (one of the two reads hits a zero)
-  //   C: i >= t0+64    every lane's term is in col S + t
-  __device__ static __forceinline__ void colpair(const uint32_t* __restrict__ x, const uint32_t* __restrict__ yz, int t,
-                                                 int t0, uint64_t& c0, uint64_t& c1) {
-    t0 = __builtin_amdgcn_readfirstlane(t0);  // wave-uniform: scalar loop control
-    const int eA = t0 < S ? t0 : S, eB = t0 + 64 < S ? t0 + 64 : S;
-    const uint32_t* y0 = yz + S + t;      // y0[-i] = y[t - i] (zero when t - i < 0)
-    const uint32_t* y1 = yz + 2 * S + t;  // y1[-i] = y[S + t - i] (zero when S + t - i >= S)
-#pragma unroll 8
-    for (int i = 0; i < eA; ++i) c0 += (uint64_t)x[i] * y0[-i];
-#pragma unroll 8
-    for (int i = eA; i < eB; ++i) {
-      c0 += (uint64_t)x[i] * y0[-i];
-      c1 += (uint64_t)x[i] * y1[-i];
+  // Column sums as a register-blocked convolution. Work unit = (chunk of C consecutive x limbs,
+  // block of 4 consecutive columns): the lane loads the C + 4 y words its 4 columns meet in the chunk
+  // once (aligned 128-bit reads), the chunk's x words as 128-bit broadcasts, and runs 4 C mads on 4
+  // independent accumulators, then adds its 4 sums into the columns (LDS 64-bit atomics: the chunks
+  // of one column land from different waves). A wave holds one chunk and the 64 column blocks from
+  // the chunk's first column on: the band of S + C - 1 columns the chunk reaches (one wave for
+  // S <= 240), so the ~S / C chunks of a pass fit the 16 waves in about one round.
+  static constexpr int C = S <= 64 ? 4 : S <= 128 ? 8 : S <= 192 ? 12 : S <= 256 ? 16 : S <= 384 ? 24 : 48;
+  static constexpr int NCH = (S + C - 1) / C;    // chunks
+  static constexpr int XL = (NCH * C + 3) / 4 * 4;    // x operands: zero words up to XL
+  static constexpr int YL = (C + 8 + 3) / 4 * 4;      // zero words before y[0] (multiple of 4: aligned strips)
+  static constexpr int YTOT = YL + S + S + 8;         // ... and S + 8 after y[S-1]
+  static constexpr int BAND = (S + C + 2) / 4 + 1;    // column blocks a chunk can reach
+  static constexpr int NGR = (BAND + 63) / 64;
+  static_assert(YL % 4 == 0 && C % 4 == 0, "aligned strips");
+
+  // acc[col] += sum_i x[i] * y[col - i] for col < ncols; x: XL words (16-byte aligned, zero past S);
+  // yz: y[0] (16-byte aligned), zero for indices in [-YL, 0) and [S, 2S + 8)
+  template <int NT>
+  __device__ static __forceinline__ void conv(const uint32_t* __restrict__ x, const uint32_t* __restrict__ yz,
+                                              uint64_t* acc, int ncols) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ncb = (ncols + 3) / 4;
+    for (int u = wave; u < NCH * NGR; u += NT / 64) {
+      const int ch = u / NGR, g = u - ch * NGR;
+      const int i0 = ch * C;
+      const int cb = i0 / 4 + g * 64 + lane;
+      // past the columns asked for, or past the band (every term has col - i >= S)
+      if (cb >= ncb || 4 * cb > i0 + C + S - 2) continue;
+      const int base = 4 * cb - i0 - C;  // ys[q] = y[base + q]; term (i0 + r, 4 cb + j) is ys[C + j - r]
+      uint32_t ys[C + 4];
+#pragma unroll
+      for (int q = 0; q < C + 4; q += 4) {
+        const uint4 v = *(const uint4*)(yz + base + q);
+        ys[q] = v.x;
+        ys[q + 1] = v.y;
+        ys[q + 2] = v.z;
+        ys[q + 3] = v.w;
+      }
+      uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#pragma unroll
+      for (int r4 = 0; r4 < C; r4 += 4) {
+        const uint4 xv = *(const uint4*)(x + i0 + r4);
+        const uint32_t xr[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = r4 + q;
+          c0 += (uint64_t)xr[q] * ys[C - r];
+          c1 += (uint64_t)xr[q] * ys[C + 1 - r];
+          c2 += (uint64_t)xr[q] * ys[C + 2 - r];
+          c3 += (uint64_t)xr[q] * ys[C + 3 - r];
+        }
+      }
+      const int col = 4 * cb;
+      if (c0) atomicAdd((unsigned long long*)&acc[col], (unsigned long long)c0);
+      if (c1 && col + 1 < ncols) atomicAdd((unsigned long long*)&acc[col + 1], (unsigned long long)c1);
+      if (c2 && col + 2 < ncols) atomicAdd((unsigned long long*)&acc[col + 2], (unsigned long long)c2);
+      if (c3 && col + 3 < ncols) atomicAdd((unsigned long long*)&acc[col + 3], (unsigned long long)c3);
     }
-#pragma unroll 8
-    for (int i = eB; i < S; ++i) c1 += (uint64_t)x[i] * y1[-i];
   }
 
-  // a <- a * b * R^-1 (mod N), redundant limbs < 2^W + 3, value < 4N. LDS: bz, nz, npz zero-padded
-  // (3S words, see colpair; b lives in bz[S..2S)), T: 2S words, d: S words, M: S words. Ends with a barrier.
-  __device__ static void monpro(uint32_t* a, const uint32_t* bz, const uint32_t* nz, const uint32_t* npz, uint64_t* T,
+  // a <- a * b * R^-1 (mod N), redundant limbs < 2^W + 3, value < 4N. LDS: by, ny, npy = b, N, n' at
+  // their y[0] (zero-padded, see conv); a, d: XL words (zero past S); T: 2S words, M: S words.
+  // Ends with a barrier.
+  template <int NT>
+  __device__ static void monpro(uint32_t* a, const uint32_t* by, const uint32_t* ny, const uint32_t* npy, uint64_t* T,
                                 uint32_t* d, uint64_t* M) {
     const int tid = threadIdx.x;
-    // T = a*b: thread t owns columns t and S+t
-    for (int t = tid; t < S; t += kTreeThreads) {
-      uint64_t c0 = 0, c1 = 0;
-      colpair(a, bz, t, t & ~63, c0, c1);
-      T[t] = c0;
-      T[S + t] = c1;
-    }
+    for (int j = tid; j < 2 * S; j += NT) T[j] = 0;
+    for (int j = tid; j < S; j += NT) M[j] = 0;
     __syncthreads();
-    for (int p = tid; p < S; p += kTreeThreads) d[p] = split3(T, p);
+    conv<NT>(a, by, T, 2 * S);  // T = a*b
     __syncthreads();
-    // m = d * n' mod R: low columns t and u = S-1-t; uniform bounds t0+64 and S-t0 (zeros beyond)
-    for (int t = tid; t < S / 2; t += kTreeThreads) {
-      const int t0 = __builtin_amdgcn_readfirstlane(t & ~63), u = S - 1 - t;
-      const int e0 = t0 + 64 < S ? t0 + 64 : S, e1 = S - t0;
-      const uint32_t* y0 = npz + S + t;
-      const uint32_t* y1 = npz + S + u;
-      uint64_t c0 = 0, c1 = 0;
-#pragma unroll 8
-      for (int i = 0; i < e0; ++i) c0 += (uint64_t)d[i] * y0[-i];
-#pragma unroll 8
-      for (int i = 0; i < e1; ++i) c1 += (uint64_t)d[i] * y1[-i];
-      M[t] = c0;
-      M[u] = c1;
-    }
+    for (int p = tid; p < S; p += NT) d[p] = split3(T, p);
     __syncthreads();
-    for (int p = tid; p < S; p += kTreeThreads) d[p] = split3(M, p);  // d now holds m (< 3*2^W limbs)
+    conv<NT>(d, npy, M, S);  // m = d * n' mod R (low columns)
     __syncthreads();
-    // V = T + m*N
-    for (int t = tid; t < S; t += kTreeThreads) {
-      uint64_t c0 = T[t], c1 = T[S + t];
-      colpair(d, nz, t, t & ~63, c0, c1);
-      T[t] = c0;
-      T[S + t] = c1;
-    }
+    for (int p = tid; p < S; p += NT) d[p] = split3(M, p);  // d now holds m (< 3*2^W limbs)
+    __syncthreads();
+    conv<NT>(d, ny, T, 2 * S);  // V = T + m*N
     __syncthreads();
     if (tid == 0) {  // carry out of the low half (see the header): ceil(X / 2^3W), X < 2^(64+2W+1)
       const uint64_t v2 = T[S - 1], v1 = T[S - 2], v0 = T[S - 3];
@@ -114,9 +131,9 @@ struct Sos {
       T[S] += (uint64_t)(x >> (3 * W));
     }
     __syncthreads();
-    for (int j = tid; j < S; j += kTreeThreads) d[j] = split3(T + S, j);
+    for (int j = tid; j < S; j += NT) d[j] = split3(T + S, j);
     __syncthreads();
-    for (int j = tid; j < S; j += kTreeThreads) a[j] = (d[j] & kMask) + (j >= 1 ? d[j - 1] >> W : 0u);
+    for (int j = tid; j < S; j += NT) a[j] = (d[j] & kMask) + (j >= 1 ? d[j - 1] >> W : 0u);
     __syncthreads();
   }
 
@@ -216,31 +233,51 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
                                                        int Wout, int max_levels, uint32_t* __restrict__ lvl_out,
                                                        int fence_mode) {
   using O = Sos<S, W>;
-  // bz, nz, npz: zero-padded operands (Sos::colpair); b itself is sb = bz + S
-  __shared__ uint32_t sa[S], bz[3 * S], nz[3 * S], npz[3 * S], sd[S], stmp[S + 64];
+  constexpr int NT = kTreeThreads;
+  // y operands (b, N, n') zero-padded around y[0] (Sos::conv); x operands (a, d) zero past S
+  __shared__ __attribute__((aligned(16))) uint32_t sa[O::XL], sd[O::XL], byp[O::YTOT], nyp[O::YTOT], npyp[O::YTOT];
+  __shared__ uint32_t stmp[S + 64], stmp2[S + 64];
   __shared__ uint64_t sT[2 * S], sM[S];
   __shared__ int s_go;
-  uint32_t* const sb = bz + S;
+  uint32_t* const sb = byp + O::YL;
+  const uint32_t* const ny = nyp + O::YL;
+  const uint32_t* const npy = npyp + O::YL;
   const int tid = threadIdx.x;
-  for (int j = tid; j < 3 * S; j += kTreeThreads) {
-    const bool mid = j >= S && j < 2 * S;
-    bz[j] = 0u;
-    nz[j] = mid ? consts[j - S] : 0u;
-    npz[j] = mid ? consts[j] : 0u;  // n' = consts[S + (j - S)]
+  for (int j = tid; j < O::YTOT; j += NT) {
+    const int k = j - O::YL;  // logical index
+    const bool in = k >= 0 && k < S;
+    byp[j] = 0u;
+    nyp[j] = in ? consts[k] : 0u;
+    npyp[j] = in ? consts[S + k] : 0u;
   }
-  auto load_leaf = [&](uint32_t* dst, size_t g) {
-    const size_t row = ids ? (size_t)ids[g] : g;
-    for (int l = tid; l < Sin; l += kTreeThreads) stmp[l] = X[(size_t)l * xstride + row * gstride];
-    __syncthreads();
-    for (int j = tid; j < S; j += kTreeThreads) dst[j] = repack_limb(stmp, Sin, Win, W, j);
-    __syncthreads();
-  };
+  for (int j = tid; j < O::XL; j += NT) {
+    sa[j] = 0u;
+    sd[j] = 0u;
+  }
   const size_t b = blockIdx.x;
-  load_leaf(sa, 2 * b);
-  if (2 * b + 1 < nleaves) {
-    load_leaf(sb, 2 * b + 1);
-    O::monpro(sa, bz, nz, npz, sT, sd, sM);
+  const bool pair = 2 * b + 1 < nleaves;
+  {  // both leaves at once
+    const size_t r0 = ids ? (size_t)ids[2 * b] : 2 * b;
+    const size_t r1 = pair ? (ids ? (size_t)ids[2 * b + 1] : 2 * b + 1) : r0;
+    for (int l = tid; l < Sin; l += kTreeThreads) {
+      stmp[l] = X[(size_t)l * xstride + r0 * gstride];
+      if (pair) stmp2[l] = X[(size_t)l * xstride + r1 * gstride];
+    }
+    __syncthreads();
+    if (Sin == S && Win == W) {  // a previous launch's nodes: redundant limbs (< 2^W + 3), kept as they are
+      for (int j = tid; j < S; j += kTreeThreads) {
+        sa[j] = stmp[j];
+        if (pair) sb[j] = stmp2[j];
+      }
+    } else {  // rows / first-level partials: normalised limbs of another radix
+      for (int j = tid; j < S; j += kTreeThreads) {
+        sa[j] = repack_limb(stmp, Sin, Win, W, j);
+        if (pair) sb[j] = repack_limb(stmp2, Sin, Win, W, j);
+      }
+    }
+    __syncthreads();
   }
+  if (pair) O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM);
   // walk up: node (h, i) holds this block's value
   int h = 1;
   size_t i = b;
@@ -268,7 +305,7 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
       const uint32_t* other = nodes + node_row(h, sib) * S;
       for (int j = tid; j < S; j += kTreeThreads) sb[j] = __builtin_nontemporal_load(other + j);
       __syncthreads();
-      O::monpro(sa, bz, nz, npz, sT, sd, sM);
+      O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM);
     }
     i >>= 1;
     ++h;
@@ -277,7 +314,7 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
   if (Y) {
     for (int j = tid; j < S; j += kTreeThreads) sb[j] = Y[j];
     __syncthreads();
-    O::monpro(sa, bz, nz, npz, sT, sd, sM);
+    O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM);
   }
   if (tid < 64) O::canon(sa, consts + 2 * S);
   __syncthreads();
@@ -336,7 +373,7 @@ hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Wi
   for (;;) {
     const bool last = levels <= 0 || nleaves <= ((size_t)1 << levels);
     const size_t blocks = (nleaves + 1) / 2;
-    if (nleaves > 2) {
+    if (nleaves > 2 && (last ? levels != 1 : levels > 1)) {  // hand-offs happen in this launch
       hipError_t e = hipMemsetAsync(flags, 0, (2 * nleaves + 2) * 4, st);
       if (e != hipSuccess) return e;
     }
