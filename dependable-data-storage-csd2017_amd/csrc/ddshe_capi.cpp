@@ -180,14 +180,16 @@ size_t max_fold_groups(dds_ctx* ctx, int S) {
   return (size_t)ctx->cus * bpc * (256 / pick_tpi(S));
 }
 
-// The reduction tree after the first fold level (ddshe_tree.hip: one launch, workgroup-cooperative
-// Montgomery products). DDSHE_TREE=0 selects round 1's per-level launches (k_fold in the tail shape +
-// k_finalize), DDSHE_TREE=1 the tree, for A/B timing. DDSHE_TREE_DIRECT (rows, default 8192): folds up to that many rows skip
-// the first level and run the tree over the rows themselves.
-bool use_tree() {  // off until it measures faster than the per-level launches (tools/tree_ab.py)
+// The reduction tree after the first fold level (ddshe_tree.hip: workgroup-cooperative Montgomery
+// products, one launch per level). Default on: faster than round 1's per-level lane-group launches at
+// every fold size measured (tools/tree_ab.py); DDSHE_TREE=0 selects those (k_fold in the
+// tail shape + k_finalize) for A/B runs. DDSHE_TREE_DIRECT (rows, default 512): folds up to that many
+// rows skip the first level and run the tree over the rows themselves (when the tree's R3 covers raw
+// rows, ModConsts::tree_direct).
+bool use_tree() {
   static const bool on = [] {
     const char* e = getenv("DDSHE_TREE");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return on;
 }

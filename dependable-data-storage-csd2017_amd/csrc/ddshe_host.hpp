@@ -174,6 +174,8 @@ struct ModConsts {
 // partial exchanged between GPUs: S2 tail limbs + signed exponent E (two words)
 inline size_t partial_words_for(const ModConsts& mc) { return (size_t)mc.S2 + 2; }
 
+struct PairQueue;  // ddshe_pairs.cpp
+
 }  // namespace host
 }  // namespace ddshe
 
@@ -195,6 +197,10 @@ struct dds_ctx {
   std::mutex tmu;
   double fold_ms = 0, total_ms = 0;
   uint64_t fold_launches = 0, fold_modmuls = 0, pending_modmuls = 0;
+  // pairwise routes (ddshe_pairs.cpp): one coalescing queue per modulus, and its counters
+  std::mutex pmu;
+  std::map<ddshe::bn::Limbs, std::shared_ptr<ddshe::host::PairQueue>> pair_queues;
+  std::atomic<uint64_t> pair_calls{0}, pair_launches{0};
 };
 
 struct dds_col {
@@ -219,6 +225,22 @@ struct dds_col {
 
 namespace ddshe {
 namespace host {
+
+// Coalescing queue of the pairwise routes for one modulus: a caller queues its pair; whoever finds
+// the queue idle becomes the leader and runs one k_pairs launch over everything queued so far (group
+// commit: no added wait when calls arrive one at a time, one launch per burst under load).
+struct PairReq {
+  bn::Limbs a, b;  // magnitudes, already < N
+  bn::Limbs r;     // a*b mod N
+  int rc = 0;
+  bool done = false;
+};
+struct PairQueue {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<PairReq*> pending;
+  bool busy = false;
+};
 
 // pinned staging of a worker (fixed 16 KiB, allocated once: pointers into it stay valid across a call):
 // bytes [0, 64) small readbacks (read_sync), words [16, 4096) the finalize Y and result

@@ -1,0 +1,122 @@
+// Pairwise routes with a modulus, coalesced across concurrent callers.
+//   GET /Sum  (DDSRestServer.scala:355-395): HomoAdd.sum(op1, op2, nsquare)        (:385)
+//   GET /Mult (DDSRestServer.scala:447-490): HomoMult.multiply(op1, op2, pubkey)   (:479)
+// Each request is one modular product. Served one by one, a request costs a full GPU round trip for
+// one Montgomery product; the proxy runs routes concurrently on its pool (DDSRestServer.scala:21), so
+// concurrent requests under one modulus share a queue and the first caller to find it idle runs ONE
+// k_pairs launch over every pair queued so far (the others sleep on the queue's condition variable
+// and wake with their result). A lone request pays no batching wait.
+#include <string.h>
+
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "ddshe_host.hpp"
+
+using namespace ddshe;
+using namespace ddshe::host;
+
+namespace {
+
+// one k_pairs launch for the batch: results into each request (rc on failure)
+void run_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& batch) {
+  const size_t mb = bn::byte_length(M), n = batch.size();
+  std::vector<uint8_t> mbe(mb), A(n * mb), B(n * mb), O(n * mb);
+  bn::to_be(M, mbe.data(), mb);
+  for (size_t i = 0; i < n; ++i) {
+    bn::to_be(batch[i]->a, A.data() + i * mb, mb);
+    bn::to_be(batch[i]->b, B.data() + i * mb, mb);
+  }
+  int rc = dds_modmul_pairs(ctx, mbe.data(), mb, A.data(), B.data(), mb, n, O.data());
+  ctx->pair_launches.fetch_add(1);
+  for (size_t i = 0; i < n; ++i) {
+    batch[i]->rc = rc;
+    if (!rc) batch[i]->r = bn::from_be(O.data() + i * mb, mb);
+  }
+}
+
+int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req) {
+  std::shared_ptr<PairQueue> q;
+  {
+    std::lock_guard<std::mutex> lk(ctx->pmu);
+    auto& slot = ctx->pair_queues[M];
+    if (!slot) slot = std::make_shared<PairQueue>();
+    q = slot;
+  }
+  std::unique_lock<std::mutex> lk(q->mu);
+  q->pending.push_back(req);
+  while (!req->done) {
+    if (q->busy) {
+      q->cv.wait(lk);
+      continue;
+    }
+    // leader: take everything queued (this request included) and launch once
+    q->busy = true;
+    std::vector<PairReq*> batch;
+    batch.swap(q->pending);
+    lk.unlock();
+    try {
+      run_batch(ctx, M, batch);
+    } catch (...) {
+      for (PairReq* r : batch) r->rc = DDS_E_NOMEM;
+    }
+    lk.lock();
+    for (PairReq* r : batch) r->done = true;
+    q->busy = false;
+    q->cv.notify_all();  // finished requests return; a queued one becomes the next leader
+  }
+  return req->rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dds_pair_modmul_dec(dds_ctx* ctx, const char* a_dec, const char* b_dec, const char* mod_dec, char* out,
+                        size_t out_cap, size_t* out_len) {
+  try {
+    if (!ctx || !a_dec || !b_dec || !mod_dec) return fail(DDS_E_ARG, "bad arguments");
+    ctx->pair_calls.fetch_add(1);
+    // operands first, then the modulus (:380-383): any of them malformed -> NumberFormatException -> 500
+    bn::Limbs a, b, M;
+    bool an = false, bneg = false, mneg = false;
+    if (!bn::from_dec(a_dec, strlen(a_dec), a, &an)) return fail(DDS_E_FORMAT, "NumberFormatException: operand1");
+    if (!bn::from_dec(b_dec, strlen(b_dec), b, &bneg)) return fail(DDS_E_FORMAT, "NumberFormatException: operand2");
+    if (!bn::from_dec(mod_dec, strlen(mod_dec), M, &mneg)) return fail(DDS_E_FORMAT, "NumberFormatException: modulus");
+    if (mneg || M.empty()) return fail(DDS_E_FORMAT, "ArithmeticException: BigInteger: modulus not positive");
+    if (!(M[0] & 1u) || bn::bit_length(M) < 2) {  // even modulus or 1: the fold's CRT path, uncoalesced
+      const char* vals[2] = {a_dec, b_dec};
+      return dds_sum_all_dec(ctx, vals, 2, mod_dec, out, out_cap, out_len);
+    }
+    // BigInteger.mod semantics: |a| |b| mod M on the GPU, the sign applied after
+    if (bn::cmp(a, M) >= 0) a = bn::mod(a, M);
+    if (bn::cmp(b, M) >= 0) b = bn::mod(b, M);
+    PairReq req;
+    req.a = a;
+    req.b = b;
+    int rc = modmul_coalesced(ctx, M, &req);
+    if (rc) return rc;
+    bn::Limbs r = req.r;
+    bn::trim(r);
+    if ((an != bneg) && !r.empty()) r = bn::sub(M, r);
+    const std::string s = bn::to_dec(r);
+    if (out_len) *out_len = s.size();
+    if (!out || out_cap < s.size() + 1) return fail(DDS_E_BUFSIZE, "output buffer too small");
+    memcpy(out, s.c_str(), s.size() + 1);
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_pair_stats(dds_ctx* ctx, uint64_t* calls, uint64_t* launches) {
+  if (!ctx) return fail(DDS_E_ARG, "bad arguments");
+  if (calls) *calls = ctx->pair_calls.load();
+  if (launches) *launches = ctx->pair_launches.load();
+  return DDS_OK;
+}
+
+}  // extern "C"

@@ -54,6 +54,7 @@ EXPORTS = [
     "dds_mctx_create", "dds_mctx_create_devices", "dds_mctx_destroy", "dds_mctx_shards", "dds_mcol_create",
     "dds_mcol_destroy", "dds_mcol_count", "dds_mcol_append", "dds_mcol_append_dec", "dds_mcol_fill_paillier_synth",
     "dds_mcol_fold", "dds_mcol_fold_rows", "dds_mcol_fold_dec",
+    "dds_pair_modmul_dec", "dds_pair_stats",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -119,6 +120,8 @@ _sig("dds_modexp_batch", C.c_int, C.c_void_p, C.c_char_p, _sz, C.c_char_p, _sz, 
 for _n in ("dds_sum_all_dec", "dds_mult_all_dec"):
     _sig(_n, C.c_int, C.c_void_p, C.POINTER(C.c_char_p), _sz, C.c_char_p, C.c_char_p, _sz, _szp)
 _u64p = C.POINTER(C.c_uint64)
+_sig("dds_pair_modmul_dec", C.c_int, C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, _sz, _szp)
+_sig("dds_pair_stats", C.c_int, C.c_void_p, _u64p, _u64p)
 _sig("dds_col_fold_rows", C.c_int, C.c_void_p, _u64p, _sz, _u8p, _sz, _szp)
 _sig("dds_col_fold_dec", C.c_int, C.c_void_p, _u64p, _sz, C.c_char_p, _sz, _szp)
 _sig("dds_col_fold_partial_device", C.c_int, C.c_void_p, _sz, _sz, C.c_void_p)
@@ -292,6 +295,22 @@ class Engine:
 
     def mult_all_dec(self, values, n: str | None) -> str:
         return self._dec(_lib.dds_mult_all_dec, values, n)
+
+    def pair_modmul_dec(self, op1: str, op2: str, modulus: str) -> str:
+        """op1*op2 mod modulus (BigInteger semantics): GET /Sum with nsqr, GET /Mult with a pubkey.
+        Concurrent calls under one modulus share one k_pairs launch (dds_pair_modmul_dec)."""
+        a, b, m = str(op1).encode(), str(op2).encode(), str(modulus).encode()
+        cap = 2 * len(m) + 64
+        out = C.create_string_buffer(cap)
+        olen = C.c_size_t()
+        _check(_lib.dds_pair_modmul_dec(self._h, a, b, m, out, cap, C.byref(olen)), "dds_pair_modmul_dec")
+        return out.value.decode()
+
+    def pair_stats(self):
+        """(calls, k_pairs launches) of pair_modmul_dec on this engine."""
+        calls, launches = C.c_uint64(), C.c_uint64()
+        _check(_lib.dds_pair_stats(self._h, C.byref(calls), C.byref(launches)), "dds_pair_stats")
+        return calls.value, launches.value
 
     # ---- OPE filter ----
     def ope_filter(self, col, valid, bound: int, op: str) -> np.ndarray:

@@ -134,7 +134,10 @@ def _pair(set1, set2, position):
 def pair_sum(eng: Engine, set1, set2, position: int, nsqr: str | None = None) -> str:
     """GET /Sum?key1&key2&position&nsqr — DDSRestServer.scala:355-395 (HomoAdd.sum, :385).
     Two keys, two operands: no dedup (the same set twice is folded twice)."""
-    return _call(eng.sum_all_dec, _pair(set1, set2, position), None if nsqr is None else _dec_text(nsqr))
+    vals = _pair(set1, set2, position)
+    if nsqr is None:
+        return _call(eng.sum_all_dec, vals, None)  # operand1.add(operand2) (:387)
+    return _call(eng.pair_modmul_dec, vals[0], vals[1], _dec_text(nsqr))
 
 
 def pair_mult(eng: Engine, set1, set2, position: int, n: str | None = None, pubkey: str | None = None) -> str:
@@ -142,7 +145,9 @@ def pair_mult(eng: Engine, set1, set2, position: int, n: str | None = None, pubk
     vals = _pair(set1, set2, position)
     if pubkey is not None:
         n = _pubkey_modulus(pubkey)
-    return _call(eng.mult_all_dec, vals, None if n is None else _dec_text(n))
+    if n is None:
+        return _call(eng.mult_all_dec, vals, None)  # operand1.multiply(operand2)
+    return _call(eng.pair_modmul_dec, vals[0], vals[1], _dec_text(n))
 
 
 _ROUTE_OP = {"SearchGt": "gt", "SearchGtEq": "ge", "SearchLt": "lt", "SearchLtEq": "le"}

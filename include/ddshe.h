@@ -94,6 +94,17 @@ int dds_rsa_product(dds_ctx* ctx, const uint8_t* n_be, size_t n_bytes, const uin
  * out[i] = a[i]*b[i] mod modulus, each mod_bytes wide. */
 int dds_modmul_pairs(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint8_t* a_be, const uint8_t* b_be,
                      size_t width, size_t n, uint8_t* out);
+/* Pairwise routes with a modulus, one request per call, decimal in and out:
+ *   GET /Sum  op1*op2 mod nsquare (HomoAdd.sum, DDSRestServer.scala:385)
+ *   GET /Mult op1*op2 mod n of the pubkey (HomoMult.multiply, DDSRestServer.scala:479)
+ * BigInteger semantics (signed operands, any modulus > 0; operands parsed before the modulus,
+ * malformed -> DDS_E_FORMAT). Concurrent calls on one context under the same modulus are coalesced:
+ * the first caller to find the modulus' queue idle runs ONE k_pairs launch over every pair queued
+ * until then, the others block until their result is ready. A lone call adds no wait. */
+int dds_pair_modmul_dec(dds_ctx* ctx, const char* op1_dec, const char* op2_dec, const char* mod_dec, char* out,
+                        size_t out_cap, size_t* out_len);
+/* Counters of dds_pair_modmul_dec on this context: calls, and k_pairs launches that served them. */
+int dds_pair_stats(dds_ctx* ctx, uint64_t* calls, uint64_t* launches);
 /* SumAll without nsqr (plain BigInteger add, DDSRestServer.scala:425): sum of count
  * operands; result big-endian in out (min(out_cap) = width + 8 is always enough). */
 int dds_bigint_sum(dds_ctx* ctx, const uint8_t* operands_be, size_t width, size_t count, uint8_t* out,

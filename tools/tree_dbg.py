@@ -13,7 +13,8 @@ import ddshe  # noqa: E402
 def main():
     eng = ddshe.Engine(0)
     rng = random.Random(5)
-    mods = {"q4094": (1 << 4094) - 1, "rand4094": rng.getrandbits(4094) | (1 << 4093) | 1,
+    mods = {"rand1024": rng.getrandbits(1024) | (1 << 1023) | 1, "rand1100": rng.getrandbits(1100) | (1 << 1099) | 1,
+            "rand600": rng.getrandbits(600) | (1 << 599) | 1, "q4094": (1 << 4094) - 1, "rand4094": rng.getrandbits(4094) | (1 << 4093) | 1,
             "rand4095": rng.getrandbits(4095) | (1 << 4094) | 1, "rand2048": rng.getrandbits(2048) | (1 << 2047) | 1}
     for name, Q in mods.items():
         for desc, xs in (("small2", [rng.randrange(Q) for _ in range(2)]),
