@@ -405,7 +405,8 @@ class SumWorkload(_Workload):
         col.close()
         k2 = self.key
         a, b = (str(x) for x in (self.col_sample[0], self.col_sample[1]))
-        pair, pair_ms, pair_p99 = med(lambda: eng.sum_all_dec([a, b], str(k2["nsquare"])), 200)
+        pair, pair_ms, pair_p99 = med(lambda: eng.pair_modmul_dec(a, b, str(k2["nsquare"])), 200)
+        conc = self.concurrent_pairs(k2["nsquare"], threads=64, per_thread=32)
         rng = np.random.default_rng(5)
         n_pairs = 65536
         xa = [self.col_sample[i % len(self.col_sample)] for i in range(n_pairs)]
@@ -422,11 +423,52 @@ class SumWorkload(_Workload):
                     "speedup_resident_vs_cpu": cpu_ms / fold_ms,
                     "matches": gpu == ref and dec == str(ref)},
                 "pair_sum_route_2048bit": {"median_ms": pair_ms, "p99_ms": pair_p99,
-                                           "path": "dds_sum_all_dec with two operands (the /Sum route body)",
+                                           "path": "dds_pair_modmul_dec, one caller (the /Sum route body)",
                                            "matches": pair == str(int(a) * int(b) % k2["nsquare"])},
+                "pair_sum_route_concurrent_2048bit": conc,
                 "pairs_batched_2048bit": {"pairs": n_pairs, "pairs_per_s": pairs_s,
                                           "path": "dds_modmul_pairs (k_pairs), host buffers in and out",
                                           "matches": pr[:4] == [x * y % k2["nsquare"] for x, y in zip(xa[:4], xb[:4])]}}
+
+    def concurrent_pairs(self, m, threads, per_thread):
+        """/Sum requests from `threads` concurrent callers (the proxy's route pool), each a blocking
+        dds_pair_modmul_dec call: throughput, per-call latency and calls per k_pairs launch."""
+        import threading
+        eng = self.eng
+        samp = [str(x) for x in self.col_sample]
+        want = {}
+        lat, bad = [], []
+        c0, l0 = eng.pair_stats()
+        start = threading.Barrier(threads + 1)
+
+        def worker(t):
+            mine = []
+            start.wait()
+            for i in range(per_thread):
+                a, b = samp[(t * 131 + i) % len(samp)], samp[(t * 17 + 7 * i + 1) % len(samp)]
+                t0 = time.perf_counter()
+                r = eng.pair_modmul_dec(a, b, str(m))
+                mine.append(time.perf_counter() - t0)
+                if (t + i) % 16 == 0 and r != str(int(a) * int(b) % m):
+                    bad.append((t, i))
+            lat.extend(mine)
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+        for x in th:
+            x.start()
+        start.wait()
+        t0 = time.perf_counter()
+        for x in th:
+            x.join()
+        wall = time.perf_counter() - t0
+        c1, l1 = eng.pair_stats()
+        lat.sort()
+        del want
+        return {"threads": threads, "calls": threads * per_thread, "pairs_per_s": threads * per_thread / wall,
+                "median_ms": lat[len(lat) // 2] * 1e3, "p99_ms": lat[int(len(lat) * 0.99)] * 1e3,
+                "calls_per_launch": (c1 - c0) / max(1, l1 - l0),
+                "path": "dds_pair_modmul_dec from concurrent threads: one k_pairs launch per burst",
+                "matches": not bad}
 
     def end_to_end(self, res):
         """Host-boundary rates, outside the timed region (never `value`): (1) the binary boundary

@@ -183,7 +183,7 @@ size_t max_fold_groups(dds_ctx* ctx, int S) {
 // The reduction tree after the first fold level (ddshe_tree.hip: workgroup-cooperative Montgomery
 // products, one launch per level). Default on: faster than round 1's per-level lane-group launches at
 // every fold size measured (tools/tree_ab.py); DDSHE_TREE=0 selects those (k_fold in the
-// tail shape + k_finalize) for A/B runs. DDSHE_TREE_DIRECT (rows, default 512): folds up to that many
+// tail shape + k_finalize) for A/B runs. DDSHE_TREE_DIRECT (rows, default 2048): folds up to that many
 // rows skip the first level and run the tree over the rows themselves (when the tree's R3 covers raw
 // rows, ModConsts::tree_direct).
 bool use_tree() {
@@ -196,7 +196,7 @@ bool use_tree() {
 size_t tree_direct_rows() {
   static const size_t n = [] {
     const char* e = getenv("DDSHE_TREE_DIRECT");
-    return e ? (size_t)atoll(e) : (size_t)512;
+    return e ? (size_t)atoll(e) : (size_t)2048;
   }();
   return n;
 }
@@ -306,15 +306,20 @@ int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const 
   uint32_t* tflags = nodes + (4 * lt.n + 2) * (size_t)S3;
   HIP_TRY(w->out.ensure((size_t)std::max(S2, S3) * 4));
   uint32_t* hy = nullptr;  // pinned: [0, S3) Y, [S3, 2 S3) result
+  const uint32_t* dY = nullptr;
   if (finalize) {
     HIP_TRY(stage_ptr(w, &hy));
     hy += kStageWord0;
-    const std::vector<uint32_t>& y = mc.y3_for(E);
-    std::copy(y.begin(), y.end(), hy);
-    HIP_TRY(w->y.ensure((size_t)S3 * 4));
-    HIP_TRY(hipMemcpyAsync(w->y.p, hy, (size_t)S3 * 4, hipMemcpyHostToDevice, st));
+    dY = mc.y3_device(E);  // cached on the device: no copy in the stream
+    if (!dY) {
+      const std::vector<uint32_t>& y = mc.y3_for(E);
+      std::copy(y.begin(), y.end(), hy);
+      HIP_TRY(w->y.ensure((size_t)S3 * 4));
+      HIP_TRY(hipMemcpyAsync(w->y.p, hy, (size_t)S3 * 4, hipMemcpyHostToDevice, st));
+      dY = w->y.as<uint32_t>();
+    }
   }
-  HIP_TRY(launch_tree(S3, lt.X, lt.xs, lt.Sin, lt.Win, lt.n, lt.ids, mc.d3, finalize ? w->y.as<uint32_t>() : nullptr,
+  HIP_TRY(launch_tree(S3, lt.X, lt.xs, lt.Sin, lt.Win, lt.n, lt.ids, mc.d3, finalize ? dY : nullptr,
                       nodes, tflags, w->out.as<uint32_t>(), S2, mc.W, st));
   if (!finalize) {
     *part = w->out.as<uint32_t>();

@@ -137,6 +137,7 @@ struct ModConsts {
     if (dq) (void)hipFree(dq);
     if (dqm) (void)hipFree(dqm);
     if (d3) (void)hipFree(d3);
+    for (auto& kv : y3dev) (void)hipFree(kv.second);
     if (dtab) (void)hipFree(dtab);
   }
   std::vector<uint32_t> rw(const bn::Limbs& v) const { return bn::to_rw(v, S, W); }
@@ -164,6 +165,29 @@ struct ModConsts {
     if (y3cache.size() >= 64) y3cache.clear();
     bn::Limbs y = pow2((int64_t)W3 * S3 - E);
     return y3cache.emplace(E, bn::to_rw(y, S3, W3)).first->second;
+  }
+  // device copy of y3_for(E), made on first use and kept until the constants go (a fold's finalize
+  // then needs no H2D copy on its critical path); nullptr once kYDev exponents are cached
+  static constexpr size_t kYDev = 256;
+  std::map<int64_t, uint32_t*> y3dev;
+  const uint32_t* y3_device(int64_t E) {
+    {
+      std::lock_guard<std::mutex> lk(ymu);
+      auto it = y3dev.find(E);
+      if (it != y3dev.end()) return it->second;
+      if (y3dev.size() >= kYDev) return nullptr;
+    }
+    const std::vector<uint32_t> y = y3_for(E);
+    uint32_t* d = nullptr;
+    if (hipMalloc(&d, y.size() * 4) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, y.data(), y.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(d);
+      return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(ymu);
+    auto ins = y3dev.emplace(E, d);
+    if (!ins.second) (void)hipFree(d);  // a concurrent caller made it first
+    return ins.first->second;
   }
   int64_t wS3() const { return (int64_t)W3 * S3; }
   // bits of 2 contributed by one Montgomery product of the main / tail shape
