@@ -622,8 +622,10 @@ __global__ void __launch_bounds__(kOpeBlock) k_ope_scatter(const uint32_t* __res
     loc += tot;
   }
   __syncthreads();
+  // nontemporal stores: the ids stream to memory instead of leaving ~20 MB of dirty L2 lines for the
+  // kernel boundary to write back (scatter pass 11.7 -> 9.9 us at 10M rows, tools/microbench/ope_ubench.hip)
   uint32_t* o = out + off;
-  for (uint32_t k = tid; k < loc; k += kOpeBlock) o[k] = sids[k];
+  for (uint32_t k = tid; k < loc; k += kOpeBlock) __builtin_nontemporal_store(sids[k], o + k);
   if (tid == 0 && tile == gridDim.x - 1) *total = off + loc;
 }
 
@@ -814,10 +816,31 @@ static bool use_tail32(int S, size_t ngroups) {
   return on && S == 160 && ngroups <= kTail32MaxGroups;
 }
 
+// The widest tail levels of the 4096-bit shape (>= 8192 products: throughput-bound, 2+ waves per SIMD at
+// 8 lanes per bignum) run at TPI = 8: 40 mads per step against the same ~18 exchange/quotient
+// instructions as at TPI = 16 (20 mads). DDSHE_TAIL8=0 disables (A/B timing).
+constexpr size_t kTail8MinGroups = 8192;
+static bool use_tail8(int S, size_t ngroups) {
+  static const bool on = [] {
+    const char* e = getenv("DDSHE_TAIL8");
+    return !(e && e[0] == '0');
+  }();
+  return on && S == 160 && ngroups >= kTail8MinGroups;
+}
+
 hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
                             const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups,
                             hipStream_t st) {
   if (ngroups == 0 || ngroups > count) return hipErrorInvalidValue;
+  if (use_tail8(S, ngroups)) {
+    if (qp_mod)
+      hipLaunchKernelGGL((k_fold<160, 8, 28, true>), dim3(grid_for(ngroups * 8)), dim3(256), 0, st, X, xstride, count,
+                         qp_mod, n0, P, pstride, ngroups);
+    else
+      hipLaunchKernelGGL((k_fold<160, 8, 28>), dim3(grid_for(ngroups * 8)), dim3(256), 0, st, X, xstride, count,
+                         consts, n0, P, pstride, ngroups);
+    return hipGetLastError();
+  }
   if (use_tail32(S, ngroups)) {
     if (qp_mod)  // N~ = N·n0 in place of N (Mont QP): the quotient needs no multiply
       hipLaunchKernelGGL((k_fold<160, 32, 28, true>), dim3(grid_for(ngroups * 32)), dim3(256), 0, st, X, xstride,
