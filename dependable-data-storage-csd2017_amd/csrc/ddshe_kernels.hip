@@ -418,13 +418,12 @@ __global__ void k_gather_rows(const uint32_t* __restrict__ T, size_t tstride, ui
 // OPE range filter: keep row i iff valid[i] && col[i] <op> bound (signed int64)
 // DDSRestServer.scala:704 (Gt), :742 (GtEq), :779 (Lt), :816 (LtEq)
 // ------------------------------------------------------------------------------
-__device__ __forceinline__ bool ope_pred(int64_t c, int64_t b, int op) {
-  switch (op) {
-    case 0: return c > b;
-    case 1: return c >= b;
-    case 2: return c < b;
-    default: return c <= b;
-  }
+// One compare for all four operators: the host turns (op, bound) into (t, code) with
+// c <op> bound == ((c > t) != (code & 1)), or a constant (code 2: every row, 4: none)
+// (launch_ope_filter) — no per-row branch on the operator.
+__device__ __forceinline__ bool ope_pred(int64_t c, int64_t t, int code) {
+  const bool r = (c > t) != (bool)(code & 1);
+  return (code & 2) ? true : (code & 4) ? false : r;
 }
 
 constexpr int kOpeBlock = 256;
@@ -486,6 +485,34 @@ __device__ __forceinline__ uint32_t ope_thread_mask(const int64_t* __restrict__ 
   return mask;
 }
 
+// Loads give thread tid the rows k*1024 + 4*tid + j (bit 4k + j of its mask: coalesced 16-byte loads).
+// Stored mask words are transposed through LDS to row order: word w of a tile covers rows
+// [32w, 32w + 32) (group k = w / 32, the nibbles of threads 8(w % 32) .. +7), so the scatter ranks a
+// tile with one block-wide scan of 256 popcounts instead of 32 ballots per thread. Also writes the
+// tile's match count.
+__device__ __forceinline__ void ope_store_mask(uint32_t m, uint32_t* __restrict__ masks, uint32_t* __restrict__ counts,
+                                               size_t tile) {
+  __shared__ uint8_t nib[kOpeGroups * kOpeBlock];
+  __shared__ uint32_t wsum[kOpeBlock / 64];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kOpeGroups; ++k) nib[k * kOpeBlock + tid] = (uint8_t)((m >> (4 * k)) & 0xFu);
+  uint32_t s = __builtin_popcount(m);
+  for (int off = 32; off >= 1; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off);
+  if ((tid & 63) == 0) wsum[tid >> 6] = s;
+  __syncthreads();
+  const uint64_t eight = *reinterpret_cast<const uint64_t*>(&nib[(tid >> 5) * kOpeBlock + (tid & 31) * 8]);
+  uint32_t word = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) word |= (uint32_t)((eight >> (8 * i)) & 0xFu) << (4 * i);
+  masks[tile * kOpeBlock + tid] = word;
+  if (tid == 0) {
+    uint32_t c = 0;
+    for (int w = 0; w < kOpeBlock / 64; ++w) c += wsum[w];
+    counts[tile] = c;
+  }
+}
+
 // Stable compaction in two launches (no inter-block waiting: a decoupled look-back's tile-state
 // probes are agent-scope atomics that cross the 8 XCDs' L2s, and measured slower here):
 //   k_ope_count:   reads the column once; per-thread match mask (32 rows -> 1 u32, 1/72 of the
@@ -498,20 +525,9 @@ __global__ void __launch_bounds__(kOpeBlock) k_ope_count(const int64_t* __restri
                                                          const uint8_t* __restrict__ valid, size_t n, int64_t bound,
                                                          int op, uint32_t vmask, uint32_t vbad,
                                                          uint32_t* __restrict__ masks, uint32_t* __restrict__ counts) {
-  __shared__ uint32_t wsum[kOpeBlock / 64];
-  const size_t t = (size_t)blockIdx.x * kOpeBlock + threadIdx.x;
   const bool vec = ((uintptr_t)col % 16 == 0) && (!HasValid || (uintptr_t)valid % 4 == 0);
   const uint32_t m = ope_thread_mask<HasValid>(col, valid, n, bound, op, blockIdx.x, vec, vmask, vbad);
-  masks[t] = m;
-  uint32_t s = __builtin_popcount(m);
-  for (int off = 32; off >= 1; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t c = 0;
-    for (int w = 0; w < kOpeBlock / 64; ++w) c += wsum[w];
-    counts[blockIdx.x] = c;
-  }
+  ope_store_mask(m, masks, counts, blockIdx.x);
 }
 
 // Row-flag compaction front end (deterministic-equality scans): same tile layout and masks as
@@ -519,7 +535,6 @@ __global__ void __launch_bounds__(kOpeBlock) k_ope_count(const int64_t* __restri
 __global__ void __launch_bounds__(kOpeBlock) k_flag_count(const uint32_t* __restrict__ flags, size_t n, uint32_t req,
                                                           uint32_t* __restrict__ masks,
                                                           uint32_t* __restrict__ counts) {
-  __shared__ uint32_t wsum[kOpeBlock / 64];
   const size_t t0 = (size_t)blockIdx.x * kOpeTile + 4 * (size_t)threadIdx.x;
   uint32_t f[kOpeItems];
   if (t0 + (kOpeGroups - 1) * 4 * kOpeBlock + 3 < n) {
@@ -544,86 +559,69 @@ __global__ void __launch_bounds__(kOpeBlock) k_flag_count(const uint32_t* __rest
 #pragma unroll
   for (int i = 0; i < kOpeItems; ++i)
     if (req ? (f[i] & req) == req : f[i] != 0) m |= 1u << i;
-  masks[(size_t)blockIdx.x * kOpeBlock + threadIdx.x] = m;
-  uint32_t s = __builtin_popcount(m);
-  for (int off = 32; off >= 1; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t c = 0;
-    for (int w = 0; w < kOpeBlock / 64; ++w) c += wsum[w];
-    counts[blockIdx.x] = c;
-  }
+  ope_store_mask(m, masks, counts, blockIdx.x);
 }
 
-// The tile's matches are ranked in row order (k*256 + tid), staged in LDS at their tile-local rank,
-// and written out by consecutive threads: full-line, coalesced stores instead of each thread writing
-// its own scattered run.
+// inclusive prefix sum over the 64 lanes of a wave (DPP row shifts + row broadcasts: no LDS round trips)
+__device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// Thread tid owns mask word tid of its tile, i.e. rows [32 tid, 32 tid + 32) of the tile (ope_store_mask).
+// Its matches' tile-local rank is an exclusive block-wide scan of the words' popcounts; the ids are
+// staged in LDS at their rank and written out by consecutive threads as full-line nontemporal stores
+// (the ids stream to memory instead of leaving ~20 MB of dirty L2 lines for the kernel boundary).
+// The tile's global offset is the sum of the counts of the tiles before it (<= a few thousand u32,
+// 8 independent loads per thread per pass).
 __global__ void __launch_bounds__(kOpeBlock) k_ope_scatter(const uint32_t* __restrict__ masks,
                                                            const uint32_t* __restrict__ counts,
                                                            uint32_t* __restrict__ out, uint64_t* __restrict__ total) {
   constexpr int kWaves = kOpeBlock / 64;
-  __shared__ uint32_t wtot[kOpeGroups][kWaves];
-  __shared__ uint64_t s_part[kWaves];
+  __shared__ uint32_t wtot[kWaves];
+  __shared__ uint32_t s_part[kWaves];
   __shared__ uint32_t sids[kOpeTile];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const uint64_t lt = (1ull << lane) - 1ull;
   const size_t tile = blockIdx.x;
-  const size_t t0 = tile * kOpeTile + 4 * (size_t)tid;
-  const uint32_t mask = masks[tile * kOpeBlock + tid];
-  // exclusive prefix of this tile: sum of the counts of tiles [0, tile)
-  // (8 independent loads per thread and pass: one L2/MALL round trip per 2048 preceding tiles instead
-  // of one per 256 — the tiles' counts were written by other XCDs, so every load misses this L2)
-  uint64_t pre = 0;
+  const uint32_t word = masks[tile * kOpeBlock + tid];
+  // exclusive prefix of this tile: sum of the counts of tiles [0, tile) (< 2^32: n is)
+  uint32_t pre = 0;
   for (size_t base = 0; base < tile; base += 8 * kOpeBlock) {
     uint32_t cv[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const size_t t = base + (size_t)q * kOpeBlock + tid;
-      cv[q] = t < tile ? counts[t] : 0u;
+      cv[q] = counts[t < tile ? t : 0];  // unconditional loads (issued together), masked below
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) pre += cv[q];
+    for (int q = 0; q < 8; ++q) pre += (base + (size_t)q * kOpeBlock + tid < tile) ? cv[q] : 0u;
   }
-  for (int off = 32; off >= 1; off >>= 1) pre += (uint64_t)__shfl_xor((long long)pre, off);
+  pre = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum(pre), 63);  // wave total
+  const uint32_t c = __builtin_popcount(word);
+  const uint32_t inc = wave_inclusive_sum(c);
+  if (lane == 63) wtot[wid] = inc;
   if (lane == 0) s_part[wid] = pre;
-  // per group: matches of the lanes below me in my wave (4 bit-ballots), wave total
-  uint32_t below[kOpeGroups];
-#pragma unroll
-  for (int k = 0; k < kOpeGroups; ++k) {
-    uint32_t b = 0, tot = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint64_t bal = __ballot((mask >> (4 * k + j)) & 1u);
-      b += (uint32_t)__popcll(bal & lt);
-      tot += (uint32_t)__popcll(bal);
-    }
-    below[k] = b;
-    if (lane == 0) wtot[k][wid] = tot;
-  }
   __syncthreads();
+  uint32_t rank = inc - c, loc = 0;
   uint64_t off = 0;
 #pragma unroll
-  for (int w = 0; w < kWaves; ++w) off += s_part[w];
-  uint32_t loc = 0;  // tile-local rank of the first match of group k
-#pragma unroll
-  for (int k = 0; k < kOpeGroups; ++k) {
-    uint32_t pw = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-      pw += (w < wid) ? wtot[k][w] : 0u;
-      tot += wtot[k][w];
-    }
-    const uint32_t q = (mask >> (4 * k)) & 0xFu;
-    uint32_t dst = loc + pw + below[k];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if ((q >> j) & 1u) sids[dst++] = (uint32_t)(t0 + (size_t)k * 4 * kOpeBlock + j);
-    loc += tot;
+  for (int w = 0; w < kWaves; ++w) {
+    rank += (w < wid) ? wtot[w] : 0u;
+    loc += wtot[w];
+    off += s_part[w];
+  }
+  const uint32_t row0 = (uint32_t)(tile * kOpeTile) + 32u * (uint32_t)tid;
+  uint32_t m = word;
+  while (m) {
+    sids[rank++] = row0 + (uint32_t)__builtin_ctz(m);
+    m &= m - 1u;
   }
   __syncthreads();
-  // nontemporal stores: the ids stream to memory instead of leaving ~20 MB of dirty L2 lines for the
-  // kernel boundary to write back (scatter pass 11.7 -> 9.9 us at 10M rows, tools/microbench/ope_ubench.hip)
   uint32_t* o = out + off;
   for (uint32_t k = tid; k < loc; k += kOpeBlock) __builtin_nontemporal_store(sids[k], o + k);
   if (tid == 0 && tile == gridDim.x - 1) *total = off + loc;
@@ -986,11 +984,21 @@ hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n,
   if (nb == 0) return hipSuccess;
   uint32_t* counts = (uint32_t*)scratch;
   uint32_t* masks = counts + nb;
+  // gt: c > b; le: !(c > b); ge: c > b-1; lt: !(c > b-1); b-1 underflows only for b = INT64_MIN, where
+  // ge keeps every row and lt none
+  int64_t t = bound;
+  int code = 0;
+  switch (op) {
+    case 0: break;
+    case 3: code = 1; break;
+    case 1: if (bound == INT64_MIN) code = 2; else t = bound - 1; break;
+    default: if (bound == INT64_MIN) code = 4; else { t = bound - 1; code = 1; } break;
+  }
   if (valid)
-    hipLaunchKernelGGL(k_ope_count<true>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, bound, op, vmask,
+    hipLaunchKernelGGL(k_ope_count<true>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, t, code, vmask,
                        vbad, masks, counts);
   else
-    hipLaunchKernelGGL(k_ope_count<false>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, bound, op, vmask,
+    hipLaunchKernelGGL(k_ope_count<false>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, t, code, vmask,
                        vbad, masks, counts);
   hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, masks, counts, out, total);
   return hipGetLastError();

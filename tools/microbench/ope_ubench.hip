@@ -123,6 +123,28 @@ __global__ void __launch_bounds__(B) k_scatter(const uint32_t* __restrict__ mask
   const size_t t0 = tile * TILE + 4 * (size_t)tid;
   const uint32_t mask = masks[tile * B + tid];
   uint64_t off = 0;
+  if (STORE == 3) {  // floor: load the mask, store one word
+    if (mask == 0xFFFFFFFFu && tid == 0) out[tile] = mask;
+    if (tid == 0 && tile == (ntiles ? ntiles : gridDim.x) - 1) *total = 0;
+    return;
+  }
+  if (STORE == 4) {  // floor + prefix of the earlier tiles' counts
+    uint64_t pre = 0;
+    for (size_t base = 0; base < tile; base += 8 * B) {
+      uint32_t cv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const size_t t = base + (size_t)q * B + tid;
+        cv[q] = t < tile ? counts[t] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) pre += cv[q];
+    }
+    for (int o = 32; o >= 1; o >>= 1) pre += (uint64_t)__shfl_xor((long long)pre, o);
+    if (pre == 0x12345 || mask == 0xFFFFFFFFu) out[tile] = (uint32_t)pre;
+    if (tid == 0 && tile == (ntiles ? ntiles : gridDim.x) - 1) *total = 0;
+    return;
+  }
   if (PREFIX == 0) {
     uint64_t pre = 0;
     for (size_t base = 0; base < tile; base += 8 * B) {
@@ -359,9 +381,9 @@ int main() {
     printf("{\"variant\": \"read_only\", \"ms\": %.5f, \"GBps\": %.1f}\n", ms / 50, 9.0 * n / (ms / 50) / 1e6);
   }
   run<256, 32, 0>("prefix", b, want, st);
-  run<256, 16, 0>("prefix", b, want, st);
   run<256, 32, 0, 1>("prefix_ntstore", b, want, st);
-  run<256, 16, 0, 1>("prefix_ntstore", b, want, st);
   run<256, 32, 0, 2>("prefix_nostore", b, want, st);
+  run<256, 32, 0, 3>("floor_maskload", b, want, st);
+  run<256, 32, 0, 4>("floor_plus_prefix", b, want, st);
   return 0;
 }
