@@ -566,10 +566,13 @@ def run_extra_configs(main_wl):
     return out
 
 
+PMC_FILE = "r02_pmc_filter_order.json"  # tools/profile_all.sh passes, summarised by tools/rocpd_stats.py
+
+
 def pmc_traffic(workload, kernels, per_step=False):
     """HBM bytes per call from the committed rocprofv3 PMC passes (10M rows): the sum over `kernels`
     of bytes per dispatch (times dispatches per call when per_step: the PMC run did one call)."""
-    tf = os.path.join(ROOT, "profiles", "r01_pmc_filter_order.json")
+    tf = os.path.join(ROOT, "profiles", PMC_FILE)
     if not os.path.exists(tf):
         return None
     ks = json.load(open(tf))["kernels"]
@@ -652,9 +655,15 @@ class ProductFilterWorkload(_Workload):
             if not ok:
                 print("VERIFY FAILED", file=sys.stderr)
         roof = self.fold_roofline(64)
-        roof["kernel"] = "k_fold<76,2,28,QP> (first MultAll fold level, 2048-bit n)"
-        roof["traffic"] = pmc_traffic("product_filter", ("k_fold<76, 2, 28, true>",))
-        roof["traffic_unit"] = "HBM bytes per launch (PMC, profiles/r01_pmc_filter_order.json)"
+        if os.environ.get("DDSHE_FOLD1", "1") != "0":  # >= 1M rows: one bignum per lane (ddshe_fold.hpp)
+            s1 = 76 if os.environ.get("DDSHE_FOLD1_74", "1") == "0" else 74
+            roof["kernel"] = f"k_fold1<{s1},28> (first MultAll fold level, 2048-bit n, one bignum per lane)"
+            kname = f"k_fold1<{s1}, 28, {'true' if s1 == 76 else 'false'}, false>"
+        else:
+            roof["kernel"] = "k_fold<76,2,28,QP> (first MultAll fold level, 2048-bit n)"
+            kname = "k_fold<76, 2, 28, true>"
+        roof["traffic"] = pmc_traffic("product_filter", (kname,))
+        roof["traffic_unit"] = f"HBM bytes per launch (PMC, profiles/{PMC_FILE})"
         _, _, filt_dev_ms, _ = self.eng.timing()  # HIP events around the filter launches (device time)
         filt_s = filt_dev_ms / 1e3 / (4 * a.steps)
         matches = sum(counts.values()) / 4
@@ -664,7 +673,7 @@ class ProductFilterWorkload(_Workload):
                 "kernel": "k_ope_count + k_ope_scatter (device time, HIP events on the launch stream)",
                 "avg_filter_call_ms": self.filter_ms / (4 * a.steps),
                 "algorithmic_bytes": filt_bytes, "traffic": pmc_traffic("product_filter", ("k_ope_count<true>", "k_ope_scatter")),
-                "traffic_unit": "HBM bytes per filter call (PMC, profiles/r01_pmc_filter_order.json)"}
+                "traffic_unit": "HBM bytes per filter call (PMC, profiles/" + PMC_FILE + ")"}
         cpu = None
         if self.world == 1 and not a.no_cpu_baseline:
             n = key["n"]
@@ -825,7 +834,7 @@ class OrderWorkload(_Workload):
                 "algorithmic_bytes": alg, "issued_bytes_est": self.mine * (8 * 32 + 9),  # 8 passes x (hist 8 + scatter 24) + prep
                 "traffic": pmc_traffic("order", ("k_rs_prep", "k_rs_red", "k_rs_hist", "k_rs_scan_digits", "k_rs_scatter"),
                                        per_step=True),
-                "traffic_unit": "HBM bytes per OrderLS call (PMC, profiles/r01_pmc_filter_order.json)"}
+                "traffic_unit": "HBM bytes per OrderLS call (PMC, profiles/" + PMC_FILE + ")"}
         roof["issued_GBps"] = roof["issued_bytes_est"] / step_s / 1e9  # what the 8-pass LSD design moves
         roof["issued_frac"] = roof["issued_GBps"] / 8000.0
         cpu = None

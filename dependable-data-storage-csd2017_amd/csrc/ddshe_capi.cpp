@@ -220,11 +220,20 @@ int fold_level1(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const ui
     *lv = Leaves{X, xstride, S, mc.W, count, 0, d_ids};
     return DDS_OK;
   }
-  size_t G = std::min(max_fold_groups(ctx, S), std::max<size_t>(1, count / 2));
+  // one bignum per lane for long folds of the narrow shapes (k_fold1), lane groups otherwise
+  // (k_fold1 may run with fewer limbs than the column's shape: its partials then carry R1 = 2^(W*S1))
+  const int S1 = (fold1_shape(S) && count >= fold1_min_rows(S, ctx->cus)) ? fold1_limbs(S, mc.bits) : 0;
+  size_t gmax = max_fold_groups(ctx, S);
+  if (S1) {
+    int bpc = 0;
+    if (fold1_occupancy(S1, &bpc) != hipSuccess || bpc < 1) bpc = 1;
+    gmax = (size_t)ctx->cus * bpc * 256;
+  }
+  size_t G = std::min(gmax, std::max<size_t>(1, count / 2));
   size_t ps = round_up(G, 64);
   HIP_TRY(w->p0.ensure((size_t)S2 * ps * 4));
   record_time(ctx, w, st, true, 0);
-  HIP_TRY(launch_fold(S, X, xstride, count, mc.d, mc.dqm, mc.n0, w->p0.as<uint32_t>(), ps, G, S2, st, d_ids));
+  HIP_TRY(launch_fold(S, X, xstride, count, mc.d, mc.dqm, mc.n0, w->p0.as<uint32_t>(), ps, G, S2, st, d_ids, S1));
   record_time(ctx, w, st, false, 0);
   if (ctx->timing.load()) {
     w->timed_fold = true;
@@ -232,7 +241,8 @@ int fold_level1(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const ui
     std::lock_guard<std::mutex> lk(ctx->tmu);
     ctx->pending_modmuls = count > G ? count - G : 0;
   }
-  *lv = Leaves{w->p0.as<uint32_t>(), ps, S2, mc.W, G, mc.wS() * ((int64_t)G - (int64_t)count), nullptr};
+  *lv = Leaves{w->p0.as<uint32_t>(), ps, S2, mc.W, G, (int64_t)mc.W * (S1 ? S1 : S) * ((int64_t)G - (int64_t)count),
+               nullptr};
   return DDS_OK;
 }
 

@@ -116,6 +116,157 @@ __global__ void __launch_bounds__(256, 2) k_fold(const uint32_t* __restrict__ X,
   g.store_col(a, P, pstride, grp);
 }
 
+// ------------------------------------------------------------------------------
+// One bignum per lane (TPI = 1) for the narrow shapes (S <= 76: the 2048-bit RSA n of MultAll,
+// DDSRestServer.scala:518, and the 2048-bit n² of a 1024-bit Paillier key, :423). A lane holds the
+// whole accumulator (S 64-bit lazy sums + S limbs of a); N is wave-uniform and lives in SGPRs, so the
+// m·N half of every CIOS step reads its multiplicand from the scalar file, and a step needs no lane
+// exchange at all: 2S mads + 4 instructions, against 2S/TPI mads + ~20 exchange/quotient
+// instructions per lane at TPI = 2. Rows of a wave are 64 consecutive rows (one 256-byte load per
+// limb). Latency per product is TPI times longer, so the launcher uses it only for folds with many
+// rows per lane (fold1_min_rows).
+// ------------------------------------------------------------------------------
+template <int S, int W, bool QP>
+struct Mont1 {
+  static constexpr uint32_t kMask = (1u << W) - 1u;
+  static constexpr int PF = (S % 4 == 0) ? 4 : 2;  // limbs per block; two blocks in flight
+  static_assert(S % PF == 0 && S >= 2 * PF, "S % PF");
+  static_assert(3ull * S < (1ull << (65 - 2 * W)), "lazy 64-bit accumulation bound");
+
+  // t = (t + a·b + m·N) / 2^W; QP: N ≡ -1 mod 2^W, so m = t0 mod 2^W
+  __device__ __forceinline__ static void step(uint64_t (&t)[S], const uint32_t (&a)[S], const uint32_t (&n)[S],
+                                              uint32_t b, uint32_t n0) {
+    t[0] = (uint64_t)a[0] * b + t[0];
+    const uint32_t m = (QP ? (uint32_t)t[0] : (uint32_t)t[0] * n0) & kMask;
+#pragma unroll
+    for (int l = 1; l < S; ++l) t[l] = (uint64_t)a[l] * b + t[l];
+    const uint64_t u0 = (uint64_t)m * n[0] + t[0];
+    t[0] = (uint64_t)m * n[1] + (t[1] + (u0 >> W));
+#pragma unroll
+    for (int l = 2; l < S; ++l) t[l - 1] = (uint64_t)m * n[l] + t[l];
+    t[S - 1] = 0;
+  }
+  __device__ __forceinline__ static void fence_t(uint64_t (&t)[S]) {
+#pragma unroll
+    for (int l = 0; l < S; ++l) asm volatile("" : "+v"(t[l]));
+  }
+  // lazy sums -> fully normalised limbs (the whole carry chain is in this lane; value < R: no carry out)
+  __device__ __forceinline__ static void settle(const uint64_t (&t)[S], uint32_t (&a)[S]) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int l = 0; l < S; ++l) {
+      const uint64_t v = t[l] + c;
+      asm volatile("v_and_b32 %0, %1, %2" : "=&v"(a[l]) : "v"((uint32_t)v), "v"(kMask));
+      c = v >> W;
+    }
+  }
+  __device__ __forceinline__ static auto rsrc(const uint32_t* X, size_t stride, int i) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(X + (size_t)i * stride), (short)0,
+                                             (int)(PF * (uint32_t)stride * 4u), 0x00020000);
+  }
+  __device__ __forceinline__ static void load_blocks2(uint32_t (&pre)[2][PF], const uint32_t* __restrict__ X,
+                                                      size_t stride, uint32_t row) {
+    const uint32_t voff = row * 4u, sstride = (uint32_t)stride * 4u;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const auto rs = rsrc(X, stride, d * PF);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) pre[d][q] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, q * sstride, 0);
+    }
+  }
+  // a <- MonPro(a, X[., row]); the first two blocks of `row` arrive in pre, those of `next` leave in it
+  __device__ __forceinline__ static void mul_row_chain(uint32_t (&a)[S], const uint32_t (&n)[S],
+                                                       const uint32_t* __restrict__ X, size_t stride, uint32_t row,
+                                                       uint32_t next, uint32_t (&pre)[2][PF], uint32_t n0) {
+    uint64_t t[S];
+#pragma unroll
+    for (int l = 0; l < S; ++l) t[l] = 0;
+    const uint32_t voff = row * 4u, sstride = (uint32_t)stride * 4u;
+    uint32_t bq[PF], bm[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      bq[q] = pre[0][q];
+      bm[q] = pre[1][q];
+    }
+#pragma unroll 1
+    for (int i = 0; i < S - 2 * PF; i += PF) {
+      // opaque redefinition of a[]: stops LICM hoisting zext(a[l]) out of the block loop as 64-bit
+      // values (every limb pinned to an even register pair: +S VGPRs, which S = 76 cannot afford)
+#pragma unroll
+      for (int l = 0; l < S; ++l) asm volatile("" : "+v"(a[l]));
+      const auto rs = rsrc(X, stride, i + 2 * PF);
+      uint32_t bn[PF];
+#pragma unroll
+      for (int q = 0; q < PF; ++q) bn[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, q * sstride, 0);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        step(t, a, n, bq[q], n0);
+        fence_t(t);
+      }
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        bq[q] = bm[q];
+        bm[q] = bn[q];
+      }
+    }
+    const uint32_t nvoff = next * 4u;
+    {
+      const auto rs = rsrc(X, stride, 0);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) pre[0][q] = __builtin_amdgcn_raw_buffer_load_b32(rs, nvoff, q * sstride, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      step(t, a, n, bq[q], n0);
+      fence_t(t);
+    }
+    {
+      const auto rs = rsrc(X, stride, PF);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) pre[1][q] = __builtin_amdgcn_raw_buffer_load_b32(rs, nvoff, q * sstride, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      step(t, a, n, bm[q], n0);
+      fence_t(t);
+    }
+    settle(t, a);
+  }
+};
+
+// Level-1 fold at one bignum per lane: lane g folds rows g, g+G, ... (same contract and partial layout
+// as k_fold: limb-major, fully normalised, prod * R^(1-c)).
+template <int S, int W, bool QP = true, bool Idx = false>
+__global__ void __launch_bounds__(256, 2) k_fold1(const uint32_t* __restrict__ X, size_t xstride, size_t count,
+                                               const uint32_t* __restrict__ consts, uint32_t n0,
+                                               uint32_t* __restrict__ P, size_t pstride, size_t ngroups,
+                                               const uint32_t* __restrict__ ids = nullptr) {
+  using M = Mont1<S, W, QP>;
+  const size_t grp = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (grp >= ngroups) return;
+  auto rowat = [&](size_t pos) -> uint32_t { return Idx ? ids[pos] : (uint32_t)pos; };
+  uint32_t n[S], a[S];
+#pragma unroll
+  for (int l = 0; l < S; ++l) n[l] = __builtin_amdgcn_readfirstlane(consts[kConstN * S + l]);
+#pragma unroll
+  for (int l = 0; l < S; ++l) asm volatile("" : "+s"(n[l]));
+  const uint32_t r0 = rowat(grp);
+#pragma unroll
+  for (int l = 0; l < S; ++l) a[l] = X[(size_t)l * xstride + r0];
+  if (grp + ngroups < count) {
+    uint32_t pre[2][M::PF];
+    uint32_t row = rowat(grp + ngroups);
+    M::load_blocks2(pre, X, xstride, row);
+    for (size_t pos = grp + ngroups; pos < count; pos += ngroups) {
+      const uint32_t nxt = pos + ngroups < count ? rowat(pos + ngroups) : row;
+      M::mul_row_chain(a, n, X, xstride, row, nxt, pre, n0);
+      row = nxt;
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < S; ++l) P[(size_t)l * pstride + grp] = a[l];
+}
+
 // result = canon(MonPro(P[0], Y)), Y = R^k mod N; writes S rW limbs to out
 template <int S, int TPI, int W>
 __global__ void __launch_bounds__(64) k_finalize(const uint32_t* __restrict__ P, size_t pstride,

@@ -761,12 +761,43 @@ hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, c
 
 hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
                        const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups, int s_out,
-                       hipStream_t st, const uint32_t* ids) {
+                       hipStream_t st, const uint32_t* ids, int lane1) {
   if (ngroups == 0 || ngroups > count) return hipErrorInvalidValue;
-  // limbs S..s_out of the partials (tail shape is wider): zero, contiguous in the limb-major layout
-  if (s_out > S) {
-    hipError_t e = hipMemsetAsync(P + (size_t)S * pstride, 0, (size_t)(s_out - S) * pstride * 4, st);
+  if (lane1 && !(fold1_shape(S) && (lane1 == S || (S == 76 && lane1 == 74)))) return hipErrorInvalidValue;
+  const int sw = lane1 ? lane1 : S;  // limbs the kernel writes
+  // limbs sw..s_out of the partials (tail shape is wider): zero, contiguous in the limb-major layout
+  if (s_out > sw) {
+    hipError_t e = hipMemsetAsync(P + (size_t)sw * pstride, 0, (size_t)(s_out - sw) * pstride * 4, st);
     if (e != hipSuccess) return e;
+  }
+  if (lane1) {
+    // k_fold1 at the column's own S may reduce against N~ (QP); at S = 74 over a 76-limb column
+    // (moduli of <= 2070 bits: the top two limbs of every row are zero) it uses N and the CIOS quotient
+    const bool qp = qp_mod && lane1 == S;
+    const uint32_t* c = qp ? qp_mod : consts;
+#define DDSHE_FOLD1(S_)                                                                                            \
+  case S_:                                                                                                         \
+    if (qp && ids)                                                                                                 \
+      hipLaunchKernelGGL((k_fold1<S_, 28, true, true>), dim3(grid_for(ngroups)), dim3(256), 0, st, X, xstride,     \
+                         count, c, n0, P, pstride, ngroups, ids);                                                  \
+    else if (qp)                                                                                                   \
+      hipLaunchKernelGGL((k_fold1<S_, 28, true>), dim3(grid_for(ngroups)), dim3(256), 0, st, X, xstride, count, c, \
+                         n0, P, pstride, ngroups, nullptr);                                                        \
+    else if (ids)                                                                                                  \
+      hipLaunchKernelGGL((k_fold1<S_, 28, false, true>), dim3(grid_for(ngroups)), dim3(256), 0, st, X, xstride,    \
+                         count, c, n0, P, pstride, ngroups, ids);                                                  \
+    else                                                                                                           \
+      hipLaunchKernelGGL((k_fold1<S_, 28, false>), dim3(grid_for(ngroups)), dim3(256), 0, st, X, xstride, count,   \
+                         c, n0, P, pstride, ngroups, nullptr);                                                     \
+    break;
+    switch (lane1) {
+      DDSHE_FOLD1(40)
+      DDSHE_FOLD1(74)
+      DDSHE_FOLD1(76)
+      default: return hipErrorInvalidValue;
+    }
+#undef DDSHE_FOLD1
+    return hipGetLastError();
   }
   const uint32_t* c = qp_mod ? qp_mod : consts;  // N~ = N·n0 in place of N (Mont QP): no v_mul_lo per CIOS step
   if (qp_mod && ids) {
@@ -783,6 +814,46 @@ hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, c
                                        pstride, ngroups, nullptr));
   }
   return hipGetLastError();
+}
+
+bool fold1_shape(int S) {
+  static const bool on = [] {
+    const char* e = getenv("DDSHE_FOLD1");
+    return !(e && e[0] == '0');
+  }();
+  return on && (S == 40 || S == 76);
+}
+// limbs k_fold1 runs with for a modulus of `bits` in shape S: 2048-bit moduli (RSA n, a 1024-bit
+// Paillier key's n^2) fit 74 limbs (74 * 28 >= bits + 2): 5 % fewer mads than 76 for one v_mul_lo per
+// CIOS step (the QP modulus N~ needs 76). DDSHE_FOLD1_74=0 keeps 76 (A/B timing).
+int fold1_limbs(int S, size_t bits) {
+  static const bool s74 = [] {
+    const char* e = getenv("DDSHE_FOLD1_74");
+    return !(e && e[0] == '0');
+  }();
+  if (S == 76 && s74 && bits + 2 <= 74 * 28) return 74;
+  return S;
+}
+// A product at one lane per bignum takes ~TPI times longer than at TPI lanes, so small folds (a few rows
+// per lane) keep the lane-group kernel; from ~8 rows per lane of a full k_fold1 grid on, the fold is
+// throughput-bound and k_fold1 issues fewer instructions per product.
+size_t fold1_min_rows(int S, int cus) {
+  static const long long env = [] {
+    const char* e = getenv("DDSHE_FOLD1_MIN");
+    return e ? atoll(e) : -1ll;
+  }();
+  if (env >= 0) return (size_t)env;
+  int bpc = 0;
+  if (fold1_occupancy(S, &bpc) != hipSuccess || bpc < 1) bpc = 1;
+  return (size_t)8 * cus * bpc * 256;
+}
+hipError_t fold1_occupancy(int S, int* blocks_per_cu) {
+  switch (S) {
+    case 40: return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (const void*)k_fold1<40, 28, true>, 256, 0);
+    case 76: return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (const void*)k_fold1<76, 28, true>, 256, 0);
+    case 74: return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (const void*)k_fold1<74, 28, false>, 256, 0);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 bool fold_qp_enabled() {  // DDSHE_FOLD_QP=0 disables (A/B timing)

@@ -37,8 +37,15 @@ hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, c
 hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
                        const uint32_t* qp_mod, uint32_t n0,
                        uint32_t* P, size_t pstride, size_t ngroups, int s_out, hipStream_t st,
-                       const uint32_t* ids = nullptr);  // ids: fold rows ids[0..count) (device, u32)
+                       const uint32_t* ids = nullptr,  // ids: fold rows ids[0..count) (device, u32)
+                       int lane1 = 0);  // != 0: one bignum per lane (k_fold1) at lane1 = fold1_limbs(S, bits) limbs
 bool fold_qp_enabled();
+// k_fold1 (one bignum per lane) exists for S (40, 76) and is worth its longer per-product latency for
+// folds of at least fold1_min_rows(S) rows (DDSHE_FOLD1=0 disables it, DDSHE_FOLD1_MIN=<rows> overrides)
+bool fold1_shape(int S);
+int fold1_limbs(int S, size_t bits);
+size_t fold1_min_rows(int S, int cus);
+hipError_t fold1_occupancy(int S, int* blocks_per_cu);
 // tree levels / finalize in the tail shape (S = tail limb count, consts of the tail shape)
 // qp_mod (nullable): N~ = N·n0 in tail limbs, used by the latency-bound levels when tail_qp(S)
 hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
