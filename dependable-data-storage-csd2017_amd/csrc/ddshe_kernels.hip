@@ -90,6 +90,72 @@ __global__ void k_ingest_be(const uint8_t* __restrict__ in, size_t width, size_t
   if (rowflags) rowflags[row] = (!overflow && cmpv >= 0) ? 1 : 0;
 }
 
+// Same conversion with the rows staged through LDS: the 64 rows of a block are loaded by all its lanes
+// as consecutive 16-byte pieces (coalesced: a wave reads 1 KiB of contiguous row bytes per load,
+// instead of 64 lanes each walking its own row 512 bytes from its neighbours'), then each lane
+// converts its row from LDS. Row pitch width + 4 bytes: lanes reading word k of consecutive rows hit
+// consecutive banks. Used when width % 16 == 0, the input is 16-byte aligned and width <= kIngestMaxW.
+constexpr int kIngestRows = 64;
+constexpr size_t kIngestMaxW = 1024;
+__global__ void __launch_bounds__(kIngestRows) k_ingest_be_lds(const uint8_t* __restrict__ in, size_t width,
+                                                               size_t count, int S, int W,
+                                                               const uint32_t* __restrict__ n2x,
+                                                               uint32_t* __restrict__ X, size_t stride,
+                                                               uint32_t* __restrict__ flags,
+                                                               uint8_t* __restrict__ rowflags) {
+  extern __shared__ uint32_t srow[];  // kIngestRows rows of width/4 + 1 words
+  const int tid = threadIdx.x;
+  const size_t r0 = (size_t)blockIdx.x * kIngestRows;
+  const size_t nrows = min((size_t)kIngestRows, count - r0);
+  const uint32_t wq = (uint32_t)(width / 16), pitch = (uint32_t)(width / 4 + 1);
+  const u32x4* src = reinterpret_cast<const u32x4*>(in + r0 * width);
+  const uint32_t npieces = (uint32_t)nrows * wq;
+  for (uint32_t i = tid; i < npieces; i += kIngestRows) {
+    const u32x4 v = __builtin_nontemporal_load(src + i);
+    const uint32_t rr = i / wq, k = (i % wq) * 4;
+    uint32_t* d = srow + rr * pitch + k;
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+  }
+  __syncthreads();
+  if ((size_t)tid >= nrows) return;
+  const size_t row = r0 + tid;
+  const uint32_t* pw = srow + tid * pitch;
+  const uint32_t kMask = (1u << W) - 1u;
+  uint64_t bitbuf = 0;
+  int nbits = 0, l = 0, cmpv = 0;
+  bool overflow = false;
+  auto put = [&](uint32_t limb) {
+    if (l < S) {
+      X[(size_t)l * stride + row] = limb;
+      const uint32_t nl = n2x[l];
+      cmpv = limb > nl ? 1 : (limb < nl ? -1 : cmpv);
+    } else if (limb) {
+      overflow = true;
+    }
+    ++l;
+  };
+  for (size_t i = width / 4; i-- > 0;) {
+    bitbuf |= (uint64_t)__builtin_bswap32(pw[i]) << nbits;
+    nbits += 32;
+    while (nbits >= W) {
+      put((uint32_t)bitbuf & kMask);
+      bitbuf >>= W;
+      nbits -= W;
+    }
+  }
+  while (l < S || bitbuf != 0) {
+    put((uint32_t)bitbuf & kMask);
+    bitbuf >>= W;
+  }
+  if (n2x[S] != 0) cmpv = -1;
+  if (overflow) atomicOr(flags, 2u);
+  else if (cmpv >= 0) atomicOr(flags, 1u);
+  if (rowflags) rowflags[row] = (!overflow && cmpv >= 0) ? 1 : 0;
+}
+
 // rows >= 2N: x <- MonPro(MonPro(x, R^2 mod N), 1) = x mod N
 template <int S, int TPI, int W>
 __global__ void __launch_bounds__(256, 2) k_reduce_rows(uint32_t* __restrict__ X, size_t stride, size_t count,
@@ -746,6 +812,16 @@ size_t max_modulus_bits() {
 hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, int W, const uint32_t* n2x,
                             uint32_t* X, size_t stride, uint32_t* flags, hipStream_t st, uint8_t* rowflags) {
   if (count == 0) return hipSuccess;
+  static const bool lds = [] {  // DDSHE_INGEST_LDS=0: per-thread row walk (A/B timing)
+    const char* e = getenv("DDSHE_INGEST_LDS");
+    return !(e && e[0] == '0');
+  }();
+  if (lds && width % 16 == 0 && width <= kIngestMaxW && (uintptr_t)in % 16 == 0) {
+    const size_t smem = (size_t)kIngestRows * (width / 4 + 1) * 4;
+    hipLaunchKernelGGL(k_ingest_be_lds, dim3((unsigned)((count + kIngestRows - 1) / kIngestRows)), dim3(kIngestRows),
+                       smem, st, in, width, count, S, W, n2x, X, stride, flags, rowflags);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_ingest_be, dim3(grid_for(count)), dim3(256), 0, st, in, width, count, S, W, n2x, X, stride,
                      flags, rowflags);
   return hipGetLastError();
