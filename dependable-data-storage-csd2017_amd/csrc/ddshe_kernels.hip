@@ -90,27 +90,34 @@ __global__ void k_ingest_be(const uint8_t* __restrict__ in, size_t width, size_t
   if (rowflags) rowflags[row] = (!overflow && cmpv >= 0) ? 1 : 0;
 }
 
-// Same conversion with the rows staged through LDS: the 64 rows of a block are loaded by all its lanes
-// as consecutive 16-byte pieces (coalesced: a wave reads 1 KiB of contiguous row bytes per load,
-// instead of 64 lanes each walking its own row 512 bytes from its neighbours'), then each lane
-// converts its row from LDS. Row pitch width + 4 bytes: lanes reading word k of consecutive rows hit
-// consecutive banks. Used when width % 16 == 0, the input is 16-byte aligned and width <= kIngestMaxW.
-constexpr int kIngestRows = 64;
+// Same conversion with the rows staged through LDS: the 64 rows of a block are loaded by its 256
+// lanes as consecutive 16-byte pieces (a wave reads 1 KiB of contiguous row bytes per load, instead of
+// 64 lanes each walking its own row 512 bytes from its neighbours'). Limb l of a row is bits
+// [W·l, W·l + W) of the value, i.e. a funnel shift of two words of the big-endian row, so every limb is
+// extracted independently: lane (q, j) of the block (j = lane % 64 = row) extracts limbs q, q+4, ... of
+// row j, and the 64 lanes of a wave store one limb of 64 consecutive rows (coalesced). The compare with
+// 2N (highest differing limb) and the overflow test (bits at or above W·S) are combined per row in LDS.
+// Row pitch width + 4 bytes: lanes reading word k of consecutive rows hit consecutive banks. Used when
+// width % 16 == 0, the input is 16-byte aligned and width <= kIngestMaxW.
+constexpr int kIngestRows = 64, kIngestThreads = 256;
 constexpr size_t kIngestMaxW = 1024;
-__global__ void __launch_bounds__(kIngestRows) k_ingest_be_lds(const uint8_t* __restrict__ in, size_t width,
-                                                               size_t count, int S, int W,
-                                                               const uint32_t* __restrict__ n2x,
-                                                               uint32_t* __restrict__ X, size_t stride,
-                                                               uint32_t* __restrict__ flags,
-                                                               uint8_t* __restrict__ rowflags) {
+__global__ void __launch_bounds__(kIngestThreads) k_ingest_be_lds(const uint8_t* __restrict__ in, size_t width,
+                                                                  size_t count, int S, int W,
+                                                                  const uint32_t* __restrict__ n2x,
+                                                                  uint32_t* __restrict__ X, size_t stride,
+                                                                  uint32_t* __restrict__ flags,
+                                                                  uint8_t* __restrict__ rowflags) {
   extern __shared__ uint32_t srow[];  // kIngestRows rows of width/4 + 1 words
-  const int tid = threadIdx.x;
+  __shared__ int sdiff[kIngestThreads / kIngestRows][kIngestRows];  // per lane: (highest differing limb + 1) * sign
+  __shared__ uint32_t sover[kIngestRows];
+  const int tid = threadIdx.x, j = tid % kIngestRows, q = tid / kIngestRows;
+  constexpr int Q = kIngestThreads / kIngestRows;
   const size_t r0 = (size_t)blockIdx.x * kIngestRows;
   const size_t nrows = min((size_t)kIngestRows, count - r0);
-  const uint32_t wq = (uint32_t)(width / 16), pitch = (uint32_t)(width / 4 + 1);
+  const uint32_t wq = (uint32_t)(width / 16), nw = (uint32_t)(width / 4), pitch = nw + 1;
   const u32x4* src = reinterpret_cast<const u32x4*>(in + r0 * width);
   const uint32_t npieces = (uint32_t)nrows * wq;
-  for (uint32_t i = tid; i < npieces; i += kIngestRows) {
+  for (uint32_t i = tid; i < npieces; i += kIngestThreads) {
     const u32x4 v = __builtin_nontemporal_load(src + i);
     const uint32_t rr = i / wq, k = (i % wq) * 4;
     uint32_t* d = srow + rr * pitch + k;
@@ -119,38 +126,43 @@ __global__ void __launch_bounds__(kIngestRows) k_ingest_be_lds(const uint8_t* __
     d[2] = v.z;
     d[3] = v.w;
   }
+  if (tid < kIngestRows) sover[tid] = 0;
   __syncthreads();
-  if ((size_t)tid >= nrows) return;
-  const size_t row = r0 + tid;
-  const uint32_t* pw = srow + tid * pitch;
+  const bool live = (size_t)j < nrows;
+  const size_t row = r0 + j;
+  const uint32_t* pw = srow + j * pitch;  // pw[nw - 1 - k]: word k counted from the least significant end
+  auto word = [&](uint32_t k) -> uint32_t { return k < nw ? __builtin_bswap32(pw[nw - 1 - k]) : 0u; };
   const uint32_t kMask = (1u << W) - 1u;
-  uint64_t bitbuf = 0;
-  int nbits = 0, l = 0, cmpv = 0;
-  bool overflow = false;
-  auto put = [&](uint32_t limb) {
-    if (l < S) {
+  int diff = 0;  // (l + 1) * sign(limb - 2N limb) at the highest l of this lane that differs
+  if (live) {
+    for (int l = q; l < S; l += Q) {
+      const uint32_t bit = (uint32_t)l * (uint32_t)W, k = bit >> 5, sh = bit & 31u;
+      const uint64_t two = ((uint64_t)word(k + 1) << 32) | word(k);
+      const uint32_t limb = (uint32_t)(two >> sh) & kMask;
       X[(size_t)l * stride + row] = limb;
       const uint32_t nl = n2x[l];
-      cmpv = limb > nl ? 1 : (limb < nl ? -1 : cmpv);
-    } else if (limb) {
-      overflow = true;
+      if (limb != nl) diff = (l + 1) * (limb > nl ? 1 : -1);
     }
-    ++l;
-  };
-  for (size_t i = width / 4; i-- > 0;) {
-    bitbuf |= (uint64_t)__builtin_bswap32(pw[i]) << nbits;
-    nbits += 32;
-    while (nbits >= W) {
-      put((uint32_t)bitbuf & kMask);
-      bitbuf >>= W;
-      nbits -= W;
+    // bits at or above W·S must be zero (lane q = 0 checks them)
+    if (q == 0) {
+      const uint32_t top = (uint32_t)S * (uint32_t)W, k0 = top >> 5;
+      uint32_t over = k0 < nw ? (word(k0) >> (top & 31u)) : 0u;
+      for (uint32_t k = k0 + 1; k < nw; ++k) over |= word(k);
+      sover[j] = over;
     }
   }
-  while (l < S || bitbuf != 0) {
-    put((uint32_t)bitbuf & kMask);
-    bitbuf >>= W;
+  sdiff[q][j] = diff;
+  __syncthreads();
+  if (q != 0 || !live) return;
+  int best = 0;
+#pragma unroll
+  for (int t = 0; t < Q; ++t) {
+    const int d = sdiff[t][j];
+    if ((d < 0 ? -d : d) > (best < 0 ? -best : best)) best = d;
   }
-  if (n2x[S] != 0) cmpv = -1;
+  int cmpv = best > 0 ? 1 : (best < 0 ? -1 : 0);
+  const bool overflow = sover[j] != 0;
+  if (n2x[S] != 0) cmpv = -1;  // 2N may need limb S (if 2N >= 2^(W*S)); row limbs beyond S are zero here
   if (overflow) atomicOr(flags, 2u);
   else if (cmpv >= 0) atomicOr(flags, 1u);
   if (rowflags) rowflags[row] = (!overflow && cmpv >= 0) ? 1 : 0;
@@ -818,8 +830,8 @@ hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S
   }();
   if (lds && width % 16 == 0 && width <= kIngestMaxW && (uintptr_t)in % 16 == 0) {
     const size_t smem = (size_t)kIngestRows * (width / 4 + 1) * 4;
-    hipLaunchKernelGGL(k_ingest_be_lds, dim3((unsigned)((count + kIngestRows - 1) / kIngestRows)), dim3(kIngestRows),
-                       smem, st, in, width, count, S, W, n2x, X, stride, flags, rowflags);
+    hipLaunchKernelGGL(k_ingest_be_lds, dim3((unsigned)((count + kIngestRows - 1) / kIngestRows)),
+                       dim3(kIngestThreads), smem, st, in, width, count, S, W, n2x, X, stride, flags, rowflags);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_ingest_be, dim3(grid_for(count)), dim3(256), 0, st, in, width, count, S, W, n2x, X, stride,

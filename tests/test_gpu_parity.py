@@ -141,6 +141,22 @@ def test_fold_operand_too_wide_is_range_error(eng):
     assert ei.value.status == ddshe.DDS_E_RANGE
 
 
+def test_ingest_lds_path_wide_rows(eng, keys):
+    """Rows of a 16-byte multiple width take the LDS-staged ingest (k_ingest_be_lds): rows >= 2N are
+    classified and reduced, rows wider than the shape's limbs are a range error, rows just below 2^(W*S)
+    pass."""
+    import ddshe
+    N = keys["rsa2048_seed3"]["n"]
+    rng = random.Random(17)
+    xs = [rng.randrange(N) for _ in range(200)] + [2 * N, 2 * N - 1, 3 * N + 7, 5 * N + 1, (1 << 2127) + 9]
+    rng.shuffle(xs)
+    for w in (272, 288):
+        assert eng.modmul_fold(N, xs, width=w) == homo.modmul_fold(xs, N)
+    with pytest.raises(ddshe.DDSError) as ei:
+        eng.modmul_fold(N, xs + [1 << 2200], width=288)
+    assert ei.value.status == ddshe.DDS_E_RANGE
+
+
 def test_even_modulus_folds_like_biginteger(eng):
     """Round 1 refused even moduli; BigInteger.mod takes any positive modulus (see test_gpu_moduli.py)."""
     assert eng.modmul_fold(1 << 100, [3, 5]) == 15
