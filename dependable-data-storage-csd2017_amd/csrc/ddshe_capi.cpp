@@ -200,13 +200,13 @@ size_t tree_direct_rows() {
   }();
   return n;
 }
-// DDSHE_TREE_SWITCH (leaves, default 512): wider levels run as tail-shape lane-group launches (many
+// DDSHE_TREE_SWITCH (leaves, default 1024; A/B at 10M rows: tail 0.232 -> 0.226 ms against 512): wider levels run as tail-shape lane-group launches (many
 // products per launch: throughput), the last log2(switch) levels as tree launches (one workgroup per
 // product: latency)
 size_t tree_switch_leaves() {
   static const size_t n = [] {
     const char* e = getenv("DDSHE_TREE_SWITCH");
-    return e ? (size_t)atoll(e) : (size_t)512;
+    return e ? (size_t)atoll(e) : (size_t)1024;
   }();
   return n;
 }
