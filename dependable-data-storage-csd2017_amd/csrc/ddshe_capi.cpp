@@ -946,6 +946,45 @@ int dds_rsa_product(dds_ctx* ctx, const uint8_t* n, size_t n_bytes, const uint8_
   return dds_modmul_fold(ctx, n, n_bytes, c, width, count, out, out_cap, out_len);
 }
 
+// A few pairs (one /Sum or /Mult request, or a small burst of them, DDSRestServer.scala:385,479) are
+// latency-bound: operands go to the tail (latency) shape on the host (limb split; an operand >= 2N is
+// reduced first, as BigInteger.multiply(..).mod would), one pinned H2D copy, one k_pairs launch at 16-32
+// lanes per bignum, one D2H copy: one stream synchronisation instead of three (two ingest range checks
+// and the readback), and two Montgomery products of ~14 us instead of ~30 us at the throughput shape.
+constexpr size_t kSmallPairs = 8;
+int small_pairs(Worker* w, hipStream_t st, ModConsts& mc, const uint8_t* a, const uint8_t* b, size_t width, size_t n,
+                size_t mod_bytes, uint8_t* out) {
+  const int S2 = mc.S2;
+  const size_t words = (size_t)S2 * n;
+  HIP_TRY(w->hch[0].ensure(3 * words * 4));
+  HIP_TRY(w->x.ensure(3 * words * 4));
+  uint32_t* h = (uint32_t*)w->hch[0].p;
+  const bn::Limbs twoN = bn::add(mc.N, mc.N);
+  for (int k = 0; k < 2; ++k) {
+    const uint8_t* src = k ? b : a;
+    for (size_t i = 0; i < n; ++i) {
+      bn::Limbs v = bn::from_be(src + i * width, width);
+      if (bn::bit_length(v) > (size_t)mc.W * mc.S)  // as the lane-group path's ingest (k_ingest_be flag 2)
+        return fail(DDS_E_RANGE, "operand wider than the modulus limb width");
+      if (bn::cmp(v, twoN) >= 0) v = bn::mod(v, mc.N);
+      const std::vector<uint32_t> rw = bn::to_rw(v, S2, mc.W);
+      for (int l = 0; l < S2; ++l) h[k * words + (size_t)l * n + i] = rw[l];
+    }
+  }
+  uint32_t* d = w->x.as<uint32_t>();
+  HIP_TRY(hipMemcpyAsync(d, h, 2 * words * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(launch_pairs_tail(S2, d, d + words, n, n, mc.d2, mc.n0, d + 2 * words, st));
+  HIP_TRY(hipMemcpyAsync(h + 2 * words, d + 2 * words, words * 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  std::vector<uint32_t> limbs(S2);
+  for (size_t i = 0; i < n; ++i) {
+    for (int l = 0; l < S2; ++l) limbs[l] = h[2 * words + (size_t)l * n + i];
+    if (!bn::to_be(mc.value2(limbs.data()), out + i * mod_bytes, mod_bytes))
+      return fail(DDS_E_RANGE, "result does not fit");
+  }
+  return DDS_OK;
+}
+
 int dds_modmul_pairs(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint8_t* a, const uint8_t* b,
                      size_t width, size_t n, uint8_t* out) {
   try {
@@ -958,6 +997,7 @@ int dds_modmul_pairs(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, cons
     WorkerLease wl(ctx);
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
+    if (n <= kSmallPairs) return small_pairs(w, wl.st, *mc, a, b, width, n, mod_bytes, out);
     const int S = mc->S;
     const size_t stride = round_up(n, 64);
     HIP_TRY(w->x.ensure((size_t)S * stride * 4));

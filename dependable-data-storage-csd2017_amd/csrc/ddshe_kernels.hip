@@ -1038,6 +1038,14 @@ hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stri
   return hipGetLastError();
 }
 
+hipError_t launch_pairs_tail(int S, const uint32_t* A, const uint32_t* B, size_t stride, size_t count,
+                             const uint32_t* consts, uint32_t n0, uint32_t* O, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  DDSHE_TAIL_SWITCH(S, hipLaunchKernelGGL((k_pairs<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), 0, st, A, B,
+                                          stride, count, consts, n0, O));
+  return hipGetLastError();
+}
+
 hipError_t launch_modexp_pre(int S, const uint32_t* Xcol, size_t xstride, size_t count, const uint32_t* consts,
                              const uint32_t* qp_mod, uint32_t n0, int nodd, uint32_t* Tab, size_t tstride,
                              hipStream_t st) {

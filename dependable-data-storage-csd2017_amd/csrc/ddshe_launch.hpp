@@ -65,6 +65,9 @@ hipError_t launch_finalize_tail(int S, const uint32_t* P, size_t pstride, const 
                                 uint32_t n0, uint32_t* out, hipStream_t st);
 hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stride, size_t count,
                         const uint32_t* consts, uint32_t n0, uint32_t* O, hipStream_t st);
+// the same in a tail (latency) shape: S = tail limbs, consts of the tail shape (a few pairs per launch)
+hipError_t launch_pairs_tail(int S, const uint32_t* A, const uint32_t* B, size_t stride, size_t count,
+                             const uint32_t* consts, uint32_t n0, uint32_t* O, hipStream_t st);
 // modexp table: Tab[j] = x^(2j+1)*R mod N (j < nodd), entry j at Tab + j*S*tstride
 hipError_t launch_modexp_pre(int S, const uint32_t* Xcol, size_t xstride, size_t count, const uint32_t* consts,
                              const uint32_t* qp_mod, uint32_t n0, int nodd, uint32_t* Tab, size_t tstride,

@@ -171,6 +171,27 @@ def test_pairs_random(eng, keys):
     assert eng.modmul_pairs(N, a, b) == [x * y % N for x, y in zip(a, b)]
 
 
+@pytest.mark.parametrize("bits", [61, 512, 1024, 2047, 2048, 3072, 4095, 6144, 8192, 16000])
+def test_small_pair_batches_tail_shape(eng, bits):
+    """n <= 8 pairs take the latency path (host limb split, k_pairs in the tail shape, one sync):
+    every shape, operands >= 2N reduced like BigInteger, wider ones a range error as on the batch path."""
+    import ddshe
+    rng = random.Random(bits)
+    N = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+    for n in (1, 2, 3, 8):
+        a = [rng.randrange(N) for _ in range(n)]
+        b = [rng.randrange(N) for _ in range(n)]
+        if n == 8:
+            a[0], b[1], a[2], b[2] = N - 1, N - 1, 2 * N + 3, 3 * N
+        assert eng.modmul_pairs(N, a, b) == [x * y % N for x, y in zip(a, b)], n
+    with pytest.raises(ddshe.DDSError) as ei:
+        eng.modmul_pairs(N, [1 << (2 * bits + 2000)], [3])
+    assert ei.value.status == ddshe.DDS_E_RANGE
+    m = (1 << bits) - 1
+    x = [m - 1, m - 2]
+    assert eng.modmul_pairs(m, x, x[::-1]) == [(m - 1) * (m - 2) % m] * 2
+
+
 def test_bigint_sum(eng):
     rng = random.Random(12)
     xs = [rng.getrandbits(4096) for _ in range(5000)]
