@@ -129,8 +129,10 @@ __global__ void __launch_bounds__(256, 2) k_fold(const uint32_t* __restrict__ X,
 template <int S, int W, bool QP>
 struct Mont1 {
   static constexpr uint32_t kMask = (1u << W) - 1u;
-  static constexpr int PF = (S % 4 == 0) ? 4 : 2;  // limbs per block; two blocks in flight
-  static_assert(S % PF == 0 && S >= 2 * PF, "S % PF");
+  static constexpr int PF = 4;      // limbs per block; two blocks in flight
+  static constexpr int RM = S % PF;  // remainder limbs (S = 74: 2), one short block after the last full one
+  static constexpr int SB = S - RM;  // limbs in full blocks
+  static_assert(RM % 2 == 0 && SB >= 2 * PF, "S % PF");
   static_assert(3ull * S < (1ull << (65 - 2 * W)), "lazy 64-bit accumulation bound");
 
   // t = (t + a·b + m·N) / 2^W; QP: N ≡ -1 mod 2^W, so m = t0 mod 2^W
@@ -146,9 +148,10 @@ struct Mont1 {
     for (int l = 2; l < S; ++l) t[l - 1] = (uint64_t)m * n[l] + t[l];
     t[S - 1] = 0;
   }
+  // t[S - 1] stays visibly zero between steps: the next step's first mad into it takes a 0 addend
   __device__ __forceinline__ static void fence_t(uint64_t (&t)[S]) {
 #pragma unroll
-    for (int l = 0; l < S; ++l) asm volatile("" : "+v"(t[l]));
+    for (int l = 0; l < S - 1; ++l) asm volatile("" : "+v"(t[l]));
   }
   // lazy sums -> fully normalised limbs (the whole carry chain is in this lane; value < R: no carry out)
   __device__ __forceinline__ static void settle(const uint64_t (&t)[S], uint32_t (&a)[S]) {
@@ -189,7 +192,7 @@ struct Mont1 {
       bm[q] = pre[1][q];
     }
 #pragma unroll 1
-    for (int i = 0; i < S - 2 * PF; i += PF) {
+    for (int i = 0; i < SB - 2 * PF; i += PF) {
       // opaque redefinition of a[]: stops LICM hoisting zext(a[l]) out of the block loop as 64-bit
       // values (every limb pinned to an even register pair: +S VGPRs, which S = 76 cannot afford)
 #pragma unroll
@@ -208,6 +211,12 @@ struct Mont1 {
         bq[q] = bm[q];
         bm[q] = bn[q];
       }
+    }
+    uint32_t br[RM > 0 ? RM : 1];  // the short block (limbs SB..S-1), requested with the last full ones
+    if constexpr (RM > 0) {
+      const auto rs = rsrc(X, stride, SB);
+#pragma unroll
+      for (int q = 0; q < RM; ++q) br[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, q * sstride, 0);
     }
     const uint32_t nvoff = next * 4u;
     {
@@ -229,6 +238,13 @@ struct Mont1 {
     for (int q = 0; q < PF; ++q) {
       step(t, a, n, bm[q], n0);
       fence_t(t);
+    }
+    if constexpr (RM > 0) {
+#pragma unroll
+      for (int q = 0; q < RM; ++q) {
+        step(t, a, n, br[q], n0);
+        fence_t(t);
+      }
     }
     settle(t, a);
   }
