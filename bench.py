@@ -169,7 +169,10 @@ def main():
     wl.close()
     if not args.no_extras:
         if rank == 0:
-            out.update(wl.extra_rank0())
+            try:  # extra lines never cost the headline line (nor leave the other ranks in the barrier)
+                out.update(wl.extra_rank0())
+            except Exception as e:  # noqa: BLE001
+                out["extras_error"] = f"{type(e).__name__}: {e}"
         if world > 1:
             dist.barrier()
     if rank == 0:
