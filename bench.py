@@ -682,6 +682,12 @@ class ProductFilterWorkload(_Workload):
             kname = "k_fold<76, 2, 28, true>"
         roof["traffic"] = pmc_traffic("product_filter", (kname,))
         roof["traffic_unit"] = f"HBM bytes per launch (PMC, profiles/{PMC_FILE})"
+        vf = os.path.join(ROOT, "profiles", "r02_pmc_valu_fold1.json")
+        if kname.startswith("k_fold1<74") and os.path.exists(vf):  # VALU counters of the same kernel
+            dv = json.load(open(vf))["derived"]
+            roof["valu_pmc"] = {"mad_issue_frac_at_measured_clock": dv["mad_issue_frac_of_half_rate_peak_at_measured_clock"],
+                                "mad_share_of_valu": dv["mad_share_of_valu"], "clock_GHz": dv["clock_GHz_est"],
+                                "source": "profiles/r02_pmc_valu_fold1.json"}
         _, _, filt_dev_ms, _ = self.eng.timing()  # HIP events around the filter launches (device time)
         filt_s = filt_dev_ms / 1e3 / (4 * a.steps)
         matches = sum(counts.values()) / 4
