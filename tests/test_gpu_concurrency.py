@@ -57,3 +57,44 @@ def test_concurrent_mixed_calls(eng, keys):
     big.close()
     assert not any(th.is_alive() for th in threads)
     assert not errors, errors
+
+
+def test_concurrent_lane_fold_and_small_pairs(eng, keys):
+    """Round-2 paths under concurrency: a MultAll fold large enough for the one-bignum-per-lane kernel
+    (k_fold1, >= ~1M rows), small pair batches (the latency path) and their batched form, from
+    several threads on one context; every result equals the one computed alone."""
+    rsa = keys["rsa2048_seed3"]
+    n = rsa["n"]
+    rows = 1_200_000
+    col = eng.column(n, rows)
+    col.fill_random(2040, 21, 0, rows)
+    want_fold = col.fold()
+    sub = list(range(0, rows, 3))
+    want_sub = col.fold_rows(sub)
+    rng = random.Random(5)
+    pa = [[rng.randrange(n) for _ in range(k)] for k in (1, 2, 8, 40)]
+    pb = [[rng.randrange(n) for _ in range(k)] for k in (1, 2, 8, 40)]
+    want_p = [[x * y % n for x, y in zip(a, b)] for a, b in zip(pa, pb)]
+    errors = []
+
+    def worker(t):
+        try:
+            for it in range(3):
+                k = (t + it) % 3
+                if k == 0:
+                    assert col.fold() == want_fold
+                elif k == 1:
+                    assert col.fold_rows(sub) == want_sub
+                else:
+                    for a, b, w in zip(pa, pb, want_p):
+                        assert eng.modmul_pairs(n, a, b) == w
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    col.close()
+    assert not errors, errors[:3]
