@@ -289,21 +289,39 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
     const size_t sib = i ^ 1u;
     if ((sib << h) < nleaves) {  // the sibling subtree has leaves: meet it at the parent
       uint32_t* mine = nodes + node_row(h, i) * S;
-      for (int j = tid; j < S; j += kTreeThreads) mine[j] = sa[j];
+      if (fence_mode == 2) {
+        // no cache maintenance: the node words go through to memory as relaxed agent-scope atomic
+        // stores (sc1, write-through), each wave waits for its stores to complete (workgroup-scope
+        // release = s_waitcnt), and the sibling reads them with agent-scope atomic loads (sc1: not
+        // served from a stale line of its own XCD's L2). tools/microbench/xcd_flag.hip: ~0.6 us per
+        // hop this way against ~20 us with agent-scope release/acquire (L2 writeback + invalidate).
+        for (int j = tid; j < S; j += kTreeThreads)
+          __hip_atomic_store(mine + j, sa[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      } else {
+        for (int j = tid; j < S; j += kTreeThreads) mine[j] = sa[j];
+      }
       if (fence_mode == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // every wave: its stores
       __syncthreads();
       if (tid == 0) {
-        if (fence_mode != 0) __threadfence();
-        const uint32_t old = __hip_atomic_fetch_add(flags + node_row(h + 1, i >> 1), 1u, __ATOMIC_ACQ_REL,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        if (fence_mode != 0) __threadfence();
+        if (fence_mode == 1) __threadfence();
+        const uint32_t old = fence_mode == 2 ? __hip_atomic_fetch_add(flags + node_row(h + 1, i >> 1), 1u,
+                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                             : __hip_atomic_fetch_add(flags + node_row(h + 1, i >> 1), 1u,
+                                                                      __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (fence_mode == 1) __threadfence();
         s_go = old != 0u;
       }
       __syncthreads();
       if (!s_go) return;  // first to arrive: the sibling's block continues
       if (fence_mode == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every wave: the sibling's stores
       const uint32_t* other = nodes + node_row(h, sib) * S;
-      for (int j = tid; j < S; j += kTreeThreads) sb[j] = __builtin_nontemporal_load(other + j);
+      if (fence_mode == 2) {
+        for (int j = tid; j < S; j += kTreeThreads)
+          sb[j] = __hip_atomic_load(const_cast<uint32_t*>(other) + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        for (int j = tid; j < S; j += kTreeThreads) sb[j] = __builtin_nontemporal_load(other + j);
+      }
       __syncthreads();
       O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM);
     }
@@ -355,7 +373,9 @@ Shape tree_shape(size_t mod_bits) {
 
 // DDSHE_TREE_LEVELS (default 1; 0 = one launch walks to the root through in-kernel hand-offs, whose
 // agent-scope L2 writeback/invalidate fences measured far slower than a launch per level): levels per launch;
-// DDSHE_TREE_FENCE (default 1): hand-off fence style (k_tree)
+// DDSHE_TREE_FENCE (default 1): hand-off fence style (k_tree); 2 = no cache maintenance (sc1 write-through
+// node stores and loads, relaxed flag): bit-exact on the GPU suite, and with it 2-5 levels per launch are
+// within run-to-run noise of one level per launch (10M-row tail 0.24-0.25 ms, 10k-row fold 0.12-0.13 ms)
 static int tree_env(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
