@@ -985,10 +985,32 @@ static bool use_tail8(int S, size_t ngroups) {
   return on && S == 160 && ngroups >= kTail8MinGroups;
 }
 
+// The 2048-bit tail shape (S = 80, 16 lanes per bignum) gets many more leaves since MultAll folds at one
+// bignum per lane (131,072 level-1 partials at 10M rows): its widest levels are throughput-bound and run
+// at 4 lanes per bignum (>= 32768 products: 40 mads per step against ~14 exchange/quotient instructions)
+// or 8 (>= 16384). DDSHE_TAIL80=0 disables (A/B timing).
+static int tail80_tpi(int S, size_t ngroups) {
+  static const bool on = [] {
+    const char* e = getenv("DDSHE_TAIL80");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || S != 80) return 0;
+  return ngroups >= 32768 ? 4 : ngroups >= 16384 ? 8 : 0;
+}
+
 hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
                             const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups,
                             hipStream_t st) {
   if (ngroups == 0 || ngroups > count) return hipErrorInvalidValue;
+  if (const int t80 = tail80_tpi(S, ngroups)) {  // S = 80 has no QP modulus (tail_qp)
+    if (t80 == 4)
+      hipLaunchKernelGGL((k_fold<80, 4, 28>), dim3(grid_for(ngroups * 4)), dim3(256), 0, st, X, xstride, count, consts,
+                         n0, P, pstride, ngroups);
+    else
+      hipLaunchKernelGGL((k_fold<80, 8, 28>), dim3(grid_for(ngroups * 8)), dim3(256), 0, st, X, xstride, count, consts,
+                         n0, P, pstride, ngroups);
+    return hipGetLastError();
+  }
   if (use_tail8(S, ngroups)) {
     if (qp_mod)
       hipLaunchKernelGGL((k_fold<160, 8, 28, true>), dim3(grid_for(ngroups * 8)), dim3(256), 0, st, X, xstride, count,
