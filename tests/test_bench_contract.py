@@ -1,5 +1,5 @@
-"""The committed bench lines (profiles/r01_bench_*.json, written by `python bench.py [--workload …]`
-on an MI355X) carry every field of the driver's JSON contract, with the roofline and CPU-baseline
+"""The committed bench lines (profiles/r01_bench_*.json and the round-2 default line, written
+by `python bench.py [--workload …]` on an MI355X) carry every field of the driver's JSON contract, with the roofline and CPU-baseline
 objects, and a verified result. CPU-only: reads the committed files."""
 import glob
 import json
@@ -8,7 +8,8 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FILES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r01_bench_*.json")))
+FILES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r01_bench_*.json"))) + [
+    os.path.join(ROOT, "profiles", "r02_bench_default_final.json")]
 
 TOP = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
        "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
@@ -46,3 +47,19 @@ def test_headline_metric_matches_baseline():
     assert base["metric"].startswith("Paillier homomorphic adds/sec (2048-bit key, mod n")
     assert d["config"]["rows"] == 10_000_000 and d["config"]["key_bits"] == 2048
     assert d["roofline"]["traffic"] is not None
+
+
+def test_round2_default_line_carries_configs_3_and_4():
+    """The driver-visible default line also carries BASELINE.json configs 3 and 4,
+    each with its own roofline and CPU baseline, and the latency lines."""
+    d = json.loads(open(os.path.join(ROOT, "profiles", "r02_bench_default_final.json")).read())
+    for name in ("config3_product_filter", "config4_encrypt_sum"):
+        c = d["configs"][name]
+        assert c["value"] > 0 and c.get("verified") is True, name
+        r = c["roofline"]
+        assert 0 < r["frac"] <= 1 and abs(r["achieved"] / r["peak"] - r["frac"]) < 1e-6, name
+        assert CPU <= set(c["cpu_baseline"]), name
+    f = d["configs"]["config3_product_filter"]["filter_roofline"]
+    assert 0 < f["frac"] <= 1 and f["traffic"] is not None
+    assert d["latency"]["pair_sum_route_2048bit"]["matches"] is True
+    assert d["latency"]["config1_sumall_10k_1024bit"]["matches"] is True
