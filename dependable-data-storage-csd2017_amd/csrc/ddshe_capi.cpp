@@ -1007,6 +1007,14 @@ int dds_modmul_pairs(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, cons
     if ((rc = ingest(ctx, w, wl.st, *mc, b, width, n, w->in2, w->x2.as<uint32_t>(), stride))) return rc;
     HIP_TRY(launch_pairs(S, w->x.as<uint32_t>(), w->x2.as<uint32_t>(), stride, n, mc->d, mc->n0,
                          w->p0.as<uint32_t>(), wl.st));
+    if (S <= kEgressMaxLimbs) {  // canonical products -> big-endian bytes on the GPU, one copy out
+      HIP_TRY(w->misc.ensure(n * mod_bytes));
+      HIP_TRY(launch_egress_be(w->p0.as<uint32_t>(), stride, n, S, mc->W, nullptr, mod_bytes, w->misc.as<uint8_t>(),
+                               wl.st));
+      HIP_TRY(hipMemcpyAsync(out, w->misc.p, n * mod_bytes, hipMemcpyDeviceToHost, wl.st));
+      HIP_TRY(hipStreamSynchronize(wl.st));
+      return DDS_OK;
+    }
     std::vector<uint32_t> h((size_t)S * stride);
     HIP_TRY(hipMemcpyAsync(h.data(), w->p0.p, h.size() * 4, hipMemcpyDeviceToHost, wl.st));
     HIP_TRY(hipStreamSynchronize(wl.st));
@@ -1207,6 +1215,23 @@ int dds_col_read(dds_col* col, size_t first, size_t count, uint8_t* out) {
   try {
     if (!col || (count && !out) || first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
     const int S = col->mc->S;
+    if (count && S <= kEgressMaxLimbs) {  // rows (< 2N) -> canonical big-endian bytes on the GPU
+      WorkerLease wl(col->ctx);
+      int rc;
+      if ((rc = wl.acquire())) return rc;
+      Worker* w = wl.w;
+      const size_t bytes = col->mc->bytes;
+      for (size_t b = 0; b < count;) {  // bounded device staging: chunks of <= 256 MiB of bytes
+        const size_t n = std::min(count - b, std::max<size_t>(1, ((size_t)256 << 20) / bytes));
+        HIP_TRY(w->misc.ensure(n * bytes));
+        HIP_TRY(launch_egress_be(col->d + first + b, col->stride, n, S, col->mc->W, col->mc->d + (size_t)kConstN * S,
+                                 bytes, w->misc.as<uint8_t>(), wl.st));
+        HIP_TRY(hipMemcpyAsync(out + b * bytes, w->misc.p, n * bytes, hipMemcpyDeviceToHost, wl.st));
+        HIP_TRY(hipStreamSynchronize(wl.st));
+        b += n;
+      }
+      return DDS_OK;
+    }
     std::vector<uint32_t> h((size_t)S * count);
     if (count)
       HIP_TRY(hipMemcpy2D(h.data(), count * 4, col->d + first, col->stride * 4, count * 4, (size_t)S,

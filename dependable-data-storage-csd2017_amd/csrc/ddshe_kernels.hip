@@ -168,6 +168,51 @@ __global__ void __launch_bounds__(kIngestThreads) k_ingest_be_lds(const uint8_t*
   if (rowflags) rowflags[row] = (!overflow && cmpv >= 0) ? 1 : 0;
 }
 
+// egress: rW column rows -> fixed-width big-endian bytes (the binary boundary's output: what a JNA shim
+// turns into BigIntegers). kEgressRows rows per block: their limbs are read limb-major (coalesced over
+// rows) into LDS, rows >= N (columns keep rows < 2N) get N subtracted by one lane per row, and every
+// output byte is a funnel shift of at most two limbs, written row-major by consecutive lanes.
+constexpr int kEgressRows = 32, kEgressMaxS = kEgressMaxLimbs;
+__global__ void __launch_bounds__(256) k_egress_be(const uint32_t* __restrict__ X, size_t stride, size_t count, int S,
+                                                   int W, const uint32_t* __restrict__ nmod, size_t width,
+                                                   uint8_t* __restrict__ out) {
+  __shared__ uint32_t sl[kEgressRows * (kEgressMaxS + 1)];
+  const int tid = threadIdx.x, P = S + 1;
+  const size_t r0 = (size_t)blockIdx.x * kEgressRows;
+  const int nrows = (int)min((size_t)kEgressRows, count - r0);
+  for (int idx = tid; idx < nrows * S; idx += 256) {
+    const int l = idx / nrows, r = idx - l * nrows;
+    sl[r * P + l] = X[(size_t)l * stride + r0 + r];
+  }
+  __syncthreads();
+  if (nmod && tid < nrows) {  // value < 2N: subtract N once if value >= N
+    uint32_t* a = sl + tid * P;
+    int c = 0;
+    for (int l = S - 1; l >= 0 && c == 0; --l) c = a[l] > nmod[l] ? 1 : (a[l] < nmod[l] ? -1 : 0);
+    if (c >= 0) {
+      const uint32_t mask = (1u << W) - 1u;
+      uint32_t br = 0;
+      for (int l = 0; l < S; ++l) {
+        const uint32_t d = a[l] - nmod[l] - br;
+        br = d >> 31;
+        a[l] = d & mask;
+      }
+    }
+  }
+  __syncthreads();
+  const size_t nb = (size_t)nrows * width;
+  uint8_t* o = out + r0 * width;
+  for (size_t idx = tid; idx < nb; idx += 256) {
+    const size_t r = idx / width, b = idx - r * width;
+    const uint32_t bit = (uint32_t)(8 * (width - 1 - b));
+    const uint32_t l = bit / (uint32_t)W, sh = bit - l * (uint32_t)W;
+    const uint32_t* a = sl + r * P;
+    uint32_t v = l < (uint32_t)S ? a[l] >> sh : 0u;
+    if (sh + 8 > (uint32_t)W && l + 1 < (uint32_t)S) v |= a[l + 1] << (W - sh);
+    o[idx] = (uint8_t)v;
+  }
+}
+
 // rows >= 2N: x <- MonPro(MonPro(x, R^2 mod N), 1) = x mod N
 template <int S, int TPI, int W>
 __global__ void __launch_bounds__(256, 2) k_reduce_rows(uint32_t* __restrict__ X, size_t stride, size_t count,
@@ -819,6 +864,15 @@ Shape tail_shape(const Shape& main) {
 size_t max_modulus_bits() {
   const Shape& s = kShapes[sizeof(kShapes) / sizeof(kShapes[0]) - 1];
   return (size_t)s.W * s.S - 2;
+}
+
+hipError_t launch_egress_be(const uint32_t* X, size_t stride, size_t count, int S, int W, const uint32_t* nmod,
+                            size_t width, uint8_t* out, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  if (S > kEgressMaxS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_egress_be, dim3((unsigned)((count + kEgressRows - 1) / kEgressRows)), dim3(256), 0, st, X, stride,
+                     count, S, W, nmod, width, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, int W, const uint32_t* n2x,

@@ -30,6 +30,11 @@ size_t max_modulus_bits();
 hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S, int W, const uint32_t* n2x,
                             uint32_t* X, size_t stride, uint32_t* flags, hipStream_t st,
                             uint8_t* rowflags = nullptr);  // rowflags[i] = 1: row i >= 2N (stored reduced)
+// rows [0, count) of an rW matrix (S <= 160 limbs of W bits, value < 2·nmod when nmod != nullptr, else
+// canonical) -> width big-endian bytes each (canonical residue when nmod is given), row-major in out
+hipError_t launch_egress_be(const uint32_t* X, size_t stride, size_t count, int S, int W, const uint32_t* nmod,
+                            size_t width, uint8_t* out, hipStream_t st);
+constexpr int kEgressMaxLimbs = 160;
 hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, const uint32_t* consts, uint32_t n0,
                               hipStream_t st);
 // main fold level (throughput shape); partial rows are zero-extended to s_out limbs
