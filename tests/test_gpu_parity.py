@@ -349,3 +349,21 @@ def test_fold_host_buffer_chunked(eng, keys):
     ms = ddshe.synth_plaintexts(7, 0, k)
     assert homo.paillier_decrypt(want, key) == int(ms.astype("int64").sum()) % key["n"]
     col.close()
+
+
+@pytest.mark.parametrize("bits", [61, 1100, 2047, 2048, 4095, 4136])
+def test_gpu_egress_pairs_and_column_read(eng, bits):
+    """k_egress_be (rW rows -> big-endian bytes on the GPU): batched pairs and column reads at byte widths
+    that are not multiples of 4, rows in [N, 2N) read back as their residue (the column keeps rows
+    below 2N), rows >= 2N reduced at ingest, the largest shape it serves (S = 160 limbs)."""
+    rng = random.Random(bits * 7)
+    N = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+    a = [rng.randrange(N) for _ in range(300)] + [N - 1, 0, 1]
+    b = [rng.randrange(N) for _ in range(300)] + [N - 1, 5, N - 1]
+    assert eng.modmul_pairs(N, a, b) == [x * y % N for x, y in zip(a, b)]
+    rows = a[:50] + [N + 3, 2 * N - 1, N, 3 * N + 11]
+    col = eng.column(N, len(rows))
+    col.append(rows)
+    assert col.read(0, len(rows)) == [x % N for x in rows]
+    assert col.read(7, 5) == [x % N for x in rows[7:12]]
+    col.close()
