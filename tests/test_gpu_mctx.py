@@ -75,3 +75,28 @@ def test_mcol_append_failure_leaves_column_unchanged(keys):
     assert col.fold() == homo.modmul_fold(list(range(2, 202)), N)
     col.close()
     m.close()
+
+
+def test_mcol_rsa_shards_on_the_lane_fold(keys):
+    """Shards big enough for the one-bignum-per-lane MultAll fold (k_fold1, >= ~1M rows per shard):
+    the same product as one column, and as the oracle on a sampled subset."""
+    import ddshe
+    n = keys["rsa2048_seed3"]["n"]
+    rows = 2_400_000
+    one = ddshe.Engine(0)
+    col1 = one.column(n, rows)
+    col1.fill_random(2040, 33, 0, rows)
+    buf = col1.read_buffer(0, rows)
+    want = col1.fold()
+    m = ddshe.MultiEngine([0, 0])
+    mc = m.column(n, rows)
+    mc.append_buffer(buf)
+    assert len(mc) == rows
+    assert mc.fold() == want
+    ids = list(range(5, rows, 4099))
+    xs = [int.from_bytes(bytes(buf[i]), "big") for i in ids]
+    assert mc.fold_rows(ids) == homo.modmul_fold(xs, n)
+    mc.close()
+    m.close()
+    col1.close()
+    one.close()
