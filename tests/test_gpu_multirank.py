@@ -64,3 +64,53 @@ def test_multirank_fold_matches_single(keys, name, k, world):
     assert all(p.exitcode == 0 for p in procs)
     assert rows == k
     assert res == homo.modmul_fold(xs, N)
+
+
+def _worker_fill(rank, world, port, N, total, seed, out_q):
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ddshe
+    import ddshe.dist as dd
+    eng = ddshe.Engine(0)
+    row0, cnt = dd.shard_range(total, world, rank)
+    col = eng.column(N, max(1, cnt))
+    col.fill_random(2040, seed, row0, cnt)  # rows depend on their global index: shards = slices of one column
+    part, rows = col.fold_partial(0, cnt)
+    parts, rows_all = dd.gather_partials(part, rows)
+    if rank == 0:
+        out_q.put((eng.combine_partials(N, parts, rows_all), int(rows_all.sum())))
+    col.close()
+    eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_multirank_partials_from_lane_folds(eng, keys):
+    """Ranks whose shards take the one-bignum-per-lane MultAll fold (k_fold1: >= ~1M rows each, 74-limb
+    partial exponent): the combined result equals the single-process fold of the whole column."""
+    N = keys["rsa2048_seed3"]["n"]
+    total, seed = 2_400_000, 44
+    col = eng.column(N, total)
+    col.fill_random(2040, seed, 0, total)
+    want = col.fold()
+    col.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31600 + random.Random(seed).randrange(1000)
+    procs = [ctx.Process(target=_worker_fill, args=(r, 2, port, N, total, seed, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res, rows = q.get(timeout=100)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert rows == total
+    assert res == want
