@@ -736,7 +736,26 @@ class ProductFilterWorkload(_Workload):
                 res_ok = res_ok and len(ids) == counts[op] and (len(ids) == 0 or bool(f(self.ope_host[ids], self.bound).all()))
         res_ms.sort()
         filt["resident_opecol_search"] = {"median_ms": res_ms[len(res_ms) // 2], "matches": res_ok,
-                                          "path": "dds_opecol_search (device filter + D2H of the matching row ids)"}
+                                          "path": "dds_opecol_search (device filter + pinned D2H of the matching row ids)"}
+        # the route-shaped answer as a row bitmask (dds_opecol_search_mask): 1 bit per row crosses PCIe
+        mk_ms, mk_ok = [], True
+        for op, f in (("gt", np.greater), ("ge", np.greater_equal), ("lt", np.less), ("le", np.less_equal)):
+            for _ in range(5):
+                t = time.perf_counter()
+                words, cnt = self.opecol.search_mask(str(self.bound), op)
+                mk_ms.append((time.perf_counter() - t) * 1e3)
+            if self.world == 1:
+                bits = np.unpackbits(words.view(np.uint8), bitorder="little")[: self.mine].astype(bool)
+                mk_ok = mk_ok and cnt == counts[op] and bool(np.array_equal(bits, f(self.ope_host, self.bound)))
+        mk_ms.sort()
+        med = mk_ms[len(mk_ms) // 2]
+        route_bytes = 9 * self.mine  # what the route reads per call (int64 + class byte per row)
+        filt["resident_opecol_search_mask"] = {
+            "median_ms": med, "matches": mk_ok, "rows": self.mine,
+            "route_roofline": {"bound": "hbm", "achieved": route_bytes / (med / 1e3) / 1e9, "peak": 8000.0,
+                               "unit": "GB/s", "frac": route_bytes / (med / 1e3) / 1e9 / 8000.0,
+                               "note": "column bytes / whole call time (host clock), mask read-back included"},
+            "path": "dds_opecol_search_mask (k_ope_count + k_count_total, one pinned D2H of n/8 bytes + count)"}
         out.update(data="synthetic (seeded RSA ciphertexts of U[1,10^4) plaintexts, seeded OPE map)",
                    roofline=roof, filter_roofline=filt, cpu_baseline=cpu, verified=ok,
                    fold_ms_per_step=self.fold_ms / a.steps, filter_ms_per_step=self.filter_ms / a.steps,

@@ -766,12 +766,11 @@ int combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, cons
   return emit_be(v, mod_bytes, out, out_cap, out_len);
 }
 
-// SumAll/MultAll over rows of a resident column (DDSRestServer.scala:412-430, 506-524): rows
-// row_ids[0..n) (nullptr: rows [first, first+n)). n == 0 -> DDS_E_EMPTY (404); n == 1 -> the operand
-// as appended, unreduced (:416-417); else the canonical product mod N.
+// SumAll/MultAll over rows of a resident column (DDSRestServer.scala:412-430, 506-524): the live rows
+// among row_ids[0..n) (nullptr: rows [first, first+n)). No live row -> DDS_E_EMPTY (404); one -> the
+// operand as appended, unreduced (:416-417); else the canonical product mod N. Caller holds col->mu.
 int col_fold_value(dds_col* col, const uint64_t* row_ids, size_t first, size_t n, bn::Limbs* v, bool* neg) {
   *neg = false;
-  if (n == 0) return fail(DDS_E_EMPTY, "no operand");
   ModConsts& mc = *col->mc;
   const size_t rows = col->count;
   if (row_ids) {
@@ -780,28 +779,47 @@ int col_fold_value(dds_col* col, const uint64_t* row_ids, size_t first, size_t n
   } else if (first + n > rows) {
     return fail(DDS_E_ARG, "rows out of range");
   }
-  if (n == 1) {
-    const size_t r = row_ids ? (size_t)row_ids[0] : first;
-    {
-      std::lock_guard<std::mutex> lk(col->mu);
-      auto it = col->orig.find(r);
-      if (it != col->orig.end()) {
-        *v = it->second.mag;
-        *neg = it->second.neg;
-        return DDS_OK;
-      }
-    }
-    std::vector<uint32_t> h((size_t)mc.S);  // stored verbatim (< 2N): the raw limbs
-    HIP_TRY(hipMemcpy2D(h.data(), 4, col->d + r, col->stride * 4, 4, (size_t)mc.S, hipMemcpyDeviceToHost));
-    *v = mc.value(h.data());
-    return DDS_OK;
+  std::vector<uint64_t> kept;  // removed sets never fold (RemoveSet, DDSRestServer.scala:207-218)
+  if (row_ids && col->ndead) {
+    kept = col_live_ids(col, row_ids, n);
+    row_ids = kept.data();
+    n = kept.size();
   }
   WorkerLease wl(col->ctx);
   int rc;
   if ((rc = wl.acquire())) return rc;
   Worker* w = wl.w;
-  std::vector<uint32_t> ids32;
   const uint32_t* d_ids = nullptr;
+  const uint32_t* X = col->d;
+  size_t r1 = first;  // the row of a one-operand fold
+  if (!row_ids) {
+    size_t nl = n;
+    if ((rc = col_live_range(col, w, wl.st, first, n, &d_ids, &nl))) return rc;
+    if (d_ids && nl == 1) {
+      uint32_t off = 0;
+      HIP_TRY(read_sync(w, wl.st, d_ids, &off, 4));
+      r1 = first + off;
+    }
+    n = nl;
+    X = col->d + first;
+  } else if (n) {
+    r1 = (size_t)row_ids[0];
+  }
+  if (n == 0) return fail(DDS_E_EMPTY, "no operand");
+  if (n == 1) {
+    auto it = col->orig.find(r1);
+    if (it != col->orig.end()) {
+      *v = it->second.mag;
+      *neg = it->second.neg;
+      return DDS_OK;
+    }
+    std::vector<uint32_t> h((size_t)mc.S);  // stored verbatim (< 2N): the raw limbs
+    HIP_TRY(hipMemcpy2DAsync(h.data(), 4, col->d + r1, col->stride * 4, 4, (size_t)mc.S, hipMemcpyDeviceToHost, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    *v = mc.value(h.data());
+    return DDS_OK;
+  }
+  std::vector<uint32_t> ids32;
   if (row_ids) {
     ids32.assign(row_ids, row_ids + n);  // < count <= max_stride < 2^32
     HIP_TRY(w->ids.ensure(n * 4));
@@ -809,7 +827,159 @@ int col_fold_value(dds_col* col, const uint64_t* row_ids, size_t first, size_t n
     d_ids = w->ids.as<uint32_t>();
   }
   // synchronises: ids32 may go afterwards
-  return fold_value_device(col->ctx, w, wl.st, mc, col->d + (row_ids ? 0 : first), col->stride, n, d_ids, v);
+  return fold_value_device(col->ctx, w, wl.st, mc, X, col->stride, n, d_ids, v);
+}
+
+int col_live_range(dds_col* col, Worker* w, hipStream_t st, size_t first, size_t count, const uint32_t** d_ids,
+                   size_t* n) {
+  *d_ids = nullptr;
+  *n = count;
+  if (col->ndead == 0 || count == 0) return DDS_OK;
+  HIP_TRY(w->misc.ensure(ope_scratch_bytes(count)));
+  HIP_TRY(w->ids.ensure(count * 4));
+  HIP_TRY(w->flags.ensure(16));
+  HIP_TRY(launch_byte_compact(col->dlive + first, count, 1u, w->misc.p, w->flags.as<uint64_t>(), w->ids.as<uint32_t>(),
+                              st));
+  uint64_t total = 0;
+  HIP_TRY(read_sync(w, st, w->flags.p, &total, 8));
+  *n = (size_t)total;
+  *d_ids = w->ids.as<uint32_t>();
+  return DDS_OK;
+}
+
+std::vector<uint64_t> col_live_ids(const dds_col* col, const uint64_t* ids, size_t n) {
+  std::vector<uint64_t> out;
+  out.reserve(n);
+  for (size_t i = 0; i < n; ++i)
+    if (col->live((size_t)ids[i])) out.push_back(ids[i]);
+  return out;
+}
+
+// Overwrite rows ids[0..n) with new operands: big-endian (ops, width) or decimal (chars, offsets). The
+// new values are ingested into scratch exactly as an append would (validation, >= 2N rows reduced and
+// their originals kept for a one-operand fold), then scattered into the column. A repeated id takes
+// its last value.
+int col_write_prepare(dds_col* col, const uint64_t* ids, size_t n, const uint8_t* ops, size_t width,
+                      const char* chars, const uint64_t* offsets, RowWrite* plan) {
+  for (size_t i = 0; i < n; ++i)
+    if (ids[i] >= col->count) return fail(DDS_E_ARG, "row id " + std::to_string(ids[i]) + " out of range");
+  if (n == 0) return DDS_OK;
+  // last occurrence of each id wins (a scatter of duplicates would race)
+  std::vector<size_t> pick;
+  {
+    std::map<uint64_t, size_t> last;
+    for (size_t i = 0; i < n; ++i) last[ids[i]] = i;
+    if (last.size() == n) {
+      pick.resize(n);
+      for (size_t i = 0; i < n; ++i) pick[i] = i;
+    } else {
+      for (auto& kv : last) pick.push_back(kv.second);
+    }
+  }
+  const size_t m = pick.size();
+  ModConsts& mc = *col->mc;
+  plan->wl.reset(new WorkerLease(col->ctx));
+  int rc;
+  if ((rc = plan->wl->acquire())) return rc;
+  Worker* w = plan->wl->w;
+  hipStream_t st = plan->wl->st;
+  const size_t ss = round_up(m, 64);
+  plan->ss = ss;
+  HIP_TRY(w->x2.ensure((size_t)mc.S * ss * 4));
+  std::vector<size_t> changed;
+  if (ops) {
+    std::vector<uint8_t> packed;
+    const uint8_t* src = ops;
+    if (m != n) {
+      packed.resize(m * width);
+      for (size_t j = 0; j < m; ++j) memcpy(packed.data() + j * width, ops + pick[j] * width, width);
+      src = packed.data();
+    }
+    if ((rc = ingest(col->ctx, w, st, mc, src, width, m, w->in, w->x2.as<uint32_t>(), ss, &changed))) return rc;
+    for (size_t j : changed) plan->origs.emplace_back(j, dds_col::Orig{bn::from_be(src + j * width, width), false});
+  } else {
+    std::vector<char> ch;
+    std::vector<uint64_t> of(1, 0);
+    for (size_t j = 0; j < m; ++j) {
+      const size_t i = pick[j];
+      if (offsets[i + 1] < offsets[i]) return fail(DDS_E_ARG, "offsets must be non-decreasing");
+      ch.insert(ch.end(), chars + offsets[i], chars + offsets[i + 1]);
+      of.push_back(ch.size());
+    }
+    ch.push_back('\0');
+    DecRows rows;
+    rows.chars = ch.data();
+    rows.offs = of.data();
+    uint32_t fl = 0;
+    std::vector<size_t> longr;
+    if ((rc = ingest_dec(w, st, mc, rows, m, w->x2.as<uint32_t>(), ss, &fl, &longr))) return rc;
+    if (fl & (kDecFormat | kDecWide)) {
+      std::vector<size_t> bad;
+      if ((rc = dec_rows_with(w, st, m, kDecFormat, &bad))) return rc;
+      if (!bad.empty()) return fail(DDS_E_FORMAT, "row " + std::to_string(ids[pick[bad[0]]]) + ": NumberFormatException");
+      return fail(DDS_E_RANGE, "decimal row wider than the column limb capacity");
+    }
+    if (!longr.empty()) return fail(DDS_E_RANGE, "decimal row wider than the column limb capacity");
+    if (fl & (kDecNeg | kDecReduce))
+      if ((rc = dec_rows_with(w, st, m, kDecNeg | kDecReduce, &changed))) return rc;
+    for (size_t j : changed) {
+      dds_col::Orig o;
+      if (!bn::from_dec(ch.data() + of[j], (size_t)(of[j + 1] - of[j]), o.mag, &o.neg))
+        return fail(DDS_E_FORMAT, "row " + std::to_string(ids[pick[j]]) + ": NumberFormatException");
+      plan->origs.emplace_back(j, std::move(o));
+    }
+  }
+  plan->ids32.resize(m);
+  for (size_t j = 0; j < m; ++j) plan->ids32[j] = (uint32_t)ids[pick[j]];
+  return DDS_OK;
+}
+
+int col_write_commit(dds_col* col, RowWrite& plan) {
+  const size_t m = plan.ids32.size();
+  if (m == 0) return DDS_OK;
+  Worker* w = plan.wl->w;
+  hipStream_t st = plan.wl->st;
+  HIP_TRY(w->ids.ensure(m * 4));
+  HIP_TRY(hipMemcpyAsync(w->ids.p, plan.ids32.data(), m * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(launch_scatter_rows(w->x2.as<uint32_t>(), plan.ss, w->ids.as<uint32_t>(), m, col->mc->S, col->d, col->stride,
+                              st));
+  HIP_TRY(hipStreamSynchronize(st));
+  for (size_t j = 0; j < m; ++j) col->orig.erase((size_t)plan.ids32[j]);
+  for (auto& o : plan.origs) col->orig[(size_t)plan.ids32[o.first]] = std::move(o.second);
+  return DDS_OK;
+}
+
+int col_set_live(dds_col* col, const uint64_t* ids, size_t n, const uint8_t* live) {
+  for (size_t i = 0; i < n; ++i)
+    if (ids[i] >= col->count) return fail(DDS_E_ARG, "row id " + std::to_string(ids[i]) + " out of range");
+  if (n == 0) return DDS_OK;
+  std::map<uint64_t, uint8_t> last;  // last flag of each id wins
+  for (size_t i = 0; i < n; ++i) last[ids[i]] = live[i] ? 1 : 0;
+  std::vector<uint32_t> ids32;
+  std::vector<uint8_t> vals;
+  for (auto& kv : last)
+    if (col->live((size_t)kv.first) != (kv.second != 0)) {
+      ids32.push_back((uint32_t)kv.first);
+      vals.push_back(kv.second);
+    }
+  if (ids32.empty()) return DDS_OK;
+  WorkerLease wl(col->ctx);
+  int rc;
+  if ((rc = wl.acquire())) return rc;
+  Worker* w = wl.w;
+  const size_t m = ids32.size();
+  HIP_TRY(w->ids.ensure(m * 4));
+  HIP_TRY(w->in2.ensure(m));
+  HIP_TRY(hipMemcpyAsync(w->ids.p, ids32.data(), m * 4, hipMemcpyHostToDevice, wl.st));
+  HIP_TRY(hipMemcpyAsync(w->in2.p, vals.data(), m, hipMemcpyHostToDevice, wl.st));
+  HIP_TRY(launch_scatter_bytes(w->ids.as<uint32_t>(), w->in2.as<uint8_t>(), m, col->dlive, wl.st));
+  HIP_TRY(hipStreamSynchronize(wl.st));
+  if (col->hlive.empty()) col->hlive.assign(col->capacity, 1);
+  for (size_t j = 0; j < m; ++j) {
+    col->hlive[ids32[j]] = vals[j];
+    col->ndead = vals[j] ? col->ndead - 1 : col->ndead + 1;
+  }
+  return DDS_OK;
 }
 
 }  // namespace host
@@ -1117,9 +1287,14 @@ int dds_col_create(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, size_t
     c->mc = mc;
     c->capacity = capacity;
     c->stride = round_up(capacity, 64);
-    if (hipSetDevice(ctx->device) != hipSuccess || hipMalloc(&c->d, (size_t)mc->S * c->stride * 4) != hipSuccess) {
+    if (hipSetDevice(ctx->device) != hipSuccess || hipMalloc(&c->d, (size_t)mc->S * c->stride * 4) != hipSuccess ||
+        hipMalloc(&c->dlive, c->stride + 16) != hipSuccess) {
       delete c;
       return fail(DDS_E_NOMEM, "column allocation");
+    }
+    if (hipMemset(c->dlive, 1, c->stride + 16) != hipSuccess) {
+      delete c;
+      return fail(DDS_E_HIP, "live mask initialisation");
     }
     *out = c;
     return DDS_OK;
@@ -1137,11 +1312,64 @@ size_t dds_col_count(const dds_col* col) { return col ? col->count : 0; }
 
 int dds_col_truncate(dds_col* col, size_t count) {
   if (!col) return fail(DDS_E_ARG, "bad arguments");
-  std::lock_guard<std::mutex> lk(col->mu);
+  std::unique_lock<std::shared_mutex> lk(col->mu);
   if (count > col->count) return fail(DDS_E_ARG, "truncate beyond the row count");
+  if (col->ndead) {  // dropped rows come back live (rows past `count` always are)
+    size_t dropped = 0;
+    for (size_t r = count; r < col->count; ++r) {
+      dropped += !col->hlive[r];
+      col->hlive[r] = 1;
+    }
+    if (dropped) {
+      HIP_TRY(hipSetDevice(col->ctx->device));
+      HIP_TRY(hipMemset(col->dlive + count, 1, col->count - count));
+      col->ndead -= dropped;
+    }
+  }
   col->count = count;
   col->orig.erase(col->orig.lower_bound(count), col->orig.end());
   return DDS_OK;
+}
+
+int dds_col_write_rows(dds_col* col, const uint64_t* row_ids, size_t n, const uint8_t* operands_be, size_t width) {
+  try {
+    if (!col || (n && (!row_ids || !operands_be || width == 0))) return fail(DDS_E_ARG, "bad arguments");
+    std::unique_lock<std::shared_mutex> lk(col->mu);
+    RowWrite plan;
+    int rc = col_write_prepare(col, row_ids, n, operands_be, width, nullptr, nullptr, &plan);
+    return rc ? rc : col_write_commit(col, plan);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_col_write_rows_dec(dds_col* col, const uint64_t* row_ids, size_t n, const char* chars,
+                           const uint64_t* offsets) {
+  try {
+    if (!col || (n && (!row_ids || !chars || !offsets))) return fail(DDS_E_ARG, "bad arguments");
+    std::unique_lock<std::shared_mutex> lk(col->mu);
+    RowWrite plan;
+    int rc = col_write_prepare(col, row_ids, n, nullptr, 0, chars, offsets, &plan);
+    return rc ? rc : col_write_commit(col, plan);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_col_set_live(dds_col* col, const uint64_t* row_ids, size_t n, const uint8_t* live) {
+  try {
+    if (!col || (n && (!row_ids || !live))) return fail(DDS_E_ARG, "bad arguments");
+    std::unique_lock<std::shared_mutex> lk(col->mu);
+    return col_set_live(col, row_ids, n, live);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+size_t dds_col_live_count(dds_col* col) {
+  if (!col) return 0;
+  std::shared_lock<std::shared_mutex> lk(col->mu);
+  return col->count - col->ndead;
 }
 
 size_t dds_col_partial_words(const dds_col* col) { return col ? partial_words_for(*col->mc) : 0; }
@@ -1149,7 +1377,7 @@ size_t dds_col_partial_words(const dds_col* col) { return col ? partial_words_fo
 int dds_col_append(dds_col* col, const uint8_t* ops, size_t width, size_t count) {
   try {
     if (!col || width == 0 || (count && !ops)) return fail(DDS_E_ARG, "bad arguments");
-    std::lock_guard<std::mutex> lk(col->mu);
+    std::unique_lock<std::shared_mutex> lk(col->mu);
     if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
     if (count == 0) return DDS_OK;
     WorkerLease wl(col->ctx);
@@ -1172,7 +1400,7 @@ int dds_col_append(dds_col* col, const uint8_t* ops, size_t width, size_t count)
 int dds_col_append_dec(dds_col* col, const char* chars, const uint64_t* offsets, size_t count) {
   try {
     if (!col || (count && (!chars || !offsets))) return fail(DDS_E_ARG, "bad arguments");
-    std::lock_guard<std::mutex> lk(col->mu);
+    std::unique_lock<std::shared_mutex> lk(col->mu);
     if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
     if (count == 0) return DDS_OK;
     for (size_t i = 0; i < count; ++i)
@@ -1213,7 +1441,9 @@ int dds_col_append_dec(dds_col* col, const char* chars, const uint64_t* offsets,
 
 int dds_col_read(dds_col* col, size_t first, size_t count, uint8_t* out) {
   try {
-    if (!col || (count && !out) || first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
+    if (!col) return fail(DDS_E_ARG, "bad arguments");
+    std::shared_lock<std::shared_mutex> lk(col->mu);
+    if ((count && !out) || first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
     const int S = col->mc->S;
     if (count && S <= kEgressMaxLimbs) {  // rows (< 2N) -> canonical big-endian bytes on the GPU
       WorkerLease wl(col->ctx);
@@ -1252,20 +1482,25 @@ int dds_col_read(dds_col* col, size_t first, size_t count, uint8_t* out) {
 
 int dds_col_fold_partial(dds_col* col, size_t first, size_t count, uint32_t* partial, uint64_t* rows) {
   try {
-    if (!col || !partial || first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
+    if (!col || !partial) return fail(DDS_E_ARG, "bad arguments");
+    std::shared_lock<std::shared_mutex> lk(col->mu);
+    if (first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
     ModConsts& mc = *col->mc;
     const size_t S2 = (size_t)mc.S2;
     int64_t E = 0;
+    WorkerLease wl(col->ctx);
+    int rc;
+    if ((rc = wl.acquire())) return rc;
+    const uint32_t* d_ids = nullptr;
+    if ((rc = col_live_range(col, wl.w, wl.st, first, count, &d_ids, &count))) return rc;  // live rows only
     if (count == 0) {  // empty partial: prod = 1, E = 0
       std::fill(partial, partial + S2, 0u);
       partial[0] = 1;
     } else {
-      WorkerLease wl(col->ctx);
-      int rc;
-      if ((rc = wl.acquire())) return rc;
       const uint32_t* part;
       size_t ps;
-      if ((rc = fold_partial_device(col->ctx, wl.w, wl.st, mc, col->d + first, col->stride, count, &part, &ps, &E)))
+      if ((rc = fold_partial_device(col->ctx, wl.w, wl.st, mc, col->d + first, col->stride, count, &part, &ps, &E,
+                                    d_ids)))
         return rc;
       HIP_TRY(hipMemcpy2DAsync(partial, 4, part, ps * 4, 4, S2, hipMemcpyDeviceToHost, wl.st));
       HIP_TRY(hipStreamSynchronize(wl.st));
@@ -1282,7 +1517,9 @@ int dds_col_fold_partial(dds_col* col, size_t first, size_t count, uint32_t* par
 
 int dds_col_fold(dds_col* col, size_t first, size_t count, uint8_t* out, size_t out_cap, size_t* out_len) {
   try {
-    if (!col || first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
+    if (!col) return fail(DDS_E_ARG, "bad arguments");
+    std::shared_lock<std::shared_mutex> lk(col->mu);
+    if (first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
     bn::Limbs v;
     bool neg = false;
     int rc = col_fold_value(col, nullptr, first, count, &v, &neg);
@@ -1298,6 +1535,7 @@ int dds_col_fold_rows(dds_col* col, const uint64_t* row_ids, size_t n, uint8_t* 
                       size_t* out_len) {
   try {
     if (!col || (n && !row_ids)) return fail(DDS_E_ARG, "bad arguments");
+    std::shared_lock<std::shared_mutex> lk(col->mu);
     bn::Limbs v;
     bool neg = false;
     int rc = col_fold_value(col, row_ids, 0, n, &v, &neg);
@@ -1311,7 +1549,9 @@ int dds_col_fold_rows(dds_col* col, const uint64_t* row_ids, size_t n, uint8_t* 
 
 int dds_col_fold_dec(dds_col* col, const uint64_t* row_ids, size_t n, char* out, size_t out_cap, size_t* out_len) {
   try {
-    if (!col || (!row_ids && n > col->count)) return fail(DDS_E_ARG, "bad arguments");
+    if (!col) return fail(DDS_E_ARG, "bad arguments");
+    std::shared_lock<std::shared_mutex> lk(col->mu);
+    if (!row_ids && n > col->count) return fail(DDS_E_ARG, "bad arguments");
     bn::Limbs v;
     bool neg = false;
     int rc = col_fold_value(col, row_ids, 0, n, &v, &neg);
@@ -1348,13 +1588,17 @@ int dds_combine_partials_device(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_
 
 int dds_col_fold_partial_device(dds_col* col, size_t first, size_t count, uint32_t* d_partial) {
   try {
-    if (!col || !d_partial || first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
+    if (!col || !d_partial) return fail(DDS_E_ARG, "bad arguments");
+    std::shared_lock<std::shared_mutex> lk(col->mu);
+    if (first + count > col->count) return fail(DDS_E_ARG, "bad arguments");
     ModConsts& mc = *col->mc;
     const size_t S2 = (size_t)mc.S2;
     WorkerLease wl(col->ctx);
     int rc;
     if ((rc = wl.acquire())) return rc;
     int64_t E = 0;
+    const uint32_t* d_ids = nullptr;
+    if ((rc = col_live_range(col, wl.w, wl.st, first, count, &d_ids, &count))) return rc;  // live rows only
     if (count == 0) {  // empty partial: prod = 1, E = 0
       HIP_TRY(hipMemsetAsync(d_partial, 0, S2 * 4, wl.st));
       const uint32_t one = 1;
@@ -1362,7 +1606,8 @@ int dds_col_fold_partial_device(dds_col* col, size_t first, size_t count, uint32
     } else {
       const uint32_t* part;
       size_t ps;
-      if ((rc = fold_partial_device(col->ctx, wl.w, wl.st, mc, col->d + first, col->stride, count, &part, &ps, &E)))
+      if ((rc = fold_partial_device(col->ctx, wl.w, wl.st, mc, col->d + first, col->stride, count, &part, &ps, &E,
+                                    d_ids)))
         return rc;
       HIP_TRY(launch_strided_copy(part, 0, ps, d_partial, 0, 1, 1, S2, wl.st));
     }
@@ -1667,7 +1912,7 @@ int col_fill_paillier_synth(dds_col* col, const uint8_t* n_be, size_t n_bytes, c
                             uint32_t shard) {
   try {
     if (!col || !n_be || !g_be || pool_size == 0 || shards == 0 || shard >= shards) return fail(DDS_E_ARG, "bad arguments");
-    std::lock_guard<std::mutex> lk(col->mu);
+    std::unique_lock<std::shared_mutex> lk(col->mu);
     if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
     ModConsts& mc = *col->mc;
     bn::Limbs n = bn::from_be(n_be, n_bytes), g = bn::from_be(g_be, g_bytes);
@@ -1785,7 +2030,7 @@ int dds_col_fill_table_synth(dds_col* col, const uint8_t* table_be, size_t width
                              uint64_t row0, size_t count) {
   try {
     if (!col || !table_be || width == 0 || tcount == 0 || tcount > 0xFFFFFFFFu) return fail(DDS_E_ARG, "bad arguments");
-    std::lock_guard<std::mutex> lk(col->mu);
+    std::unique_lock<std::shared_mutex> lk(col->mu);
     if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
     WorkerLease wl(col->ctx);
     int rc;
@@ -1808,7 +2053,7 @@ int dds_col_fill_table_synth(dds_col* col, const uint8_t* table_be, size_t width
 int dds_col_fill_random(dds_col* col, size_t bits, uint64_t seed, uint64_t row0, size_t count) {
   try {
     if (!col || bits == 0) return fail(DDS_E_ARG, "bad arguments");
-    std::lock_guard<std::mutex> lk(col->mu);
+    std::unique_lock<std::shared_mutex> lk(col->mu);
     if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
     if (bits >= col->mc->bits) return fail(DDS_E_RANGE, "random rows must stay below the modulus");
     WorkerLease wl(col->ctx);
@@ -1831,8 +2076,8 @@ int dds_col_encrypt_paillier(dds_col* out, dds_col* rcol, size_t r_first, const 
     if (!out || !rcol || !n_be || !g_be || (count && !d_m) || (!p_be) != (!q_be)) return fail(DDS_E_ARG, "bad args");
     if (count == 0) return DDS_OK;
     if (r_first + count > rcol->count) return fail(DDS_E_ARG, "r rows out of range");
-    std::unique_lock<std::mutex> lk(out->mu, std::defer_lock);
-    std::unique_lock<std::mutex> lr(rcol->mu, std::defer_lock);
+    std::unique_lock<std::shared_mutex> lk(out->mu, std::defer_lock);
+    std::unique_lock<std::shared_mutex> lr(rcol->mu, std::defer_lock);
     if (out == rcol) return fail(DDS_E_ARG, "out and r columns must differ");
     std::lock(lk, lr);
     if (out->count + count > out->capacity) return fail(DDS_E_ARG, "column capacity exceeded");

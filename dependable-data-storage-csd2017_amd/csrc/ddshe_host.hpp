@@ -15,6 +15,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -92,6 +93,7 @@ struct Worker {
   // per-row status bytes, and the event after each slot's last use
   HostBuf hch[2], hoff[2];
   HostBuf hstage;  // fold finalize: Y in, result out (pinned: no staging copies on the latency path)
+  HostBuf hbig;    // large read-backs (Search ids / match masks, Order permutations) before the caller's copy
   DevBuf dch[2], doff[2], rflags;
   hipEvent_t ev_dec[2] = {};
   ~Worker() {
@@ -232,7 +234,18 @@ struct dds_col {
   std::shared_ptr<ddshe::host::ModConsts> mc;
   size_t capacity = 0, count = 0, stride = 0;
   uint32_t* d = nullptr;
-  std::mutex mu;
+  // Folds and reads hold it shared (concurrent SumAll / MultAll requests run side by side); appends,
+  // row writes, liveness changes and truncation hold it exclusively, so a fold never sees a half-applied
+  // mutation (WriteElement / AddElement / RemoveSet, DDSRestServer.scala:207-321).
+  std::shared_mutex mu;
+  // Live mask (dds_col_set_live): dlive[r] = 1 when row r takes part in folds (device, capacity bytes,
+  // all 1 at creation); hlive its host mirror, allocated when the first row goes dead; ndead the number
+  // of dead rows among [0, count). Rows at or past `count` are always 1 (truncate resets them), so an
+  // append needs no mask update. With ndead == 0 a fold runs exactly as before (no mask pass).
+  uint8_t* dlive = nullptr;
+  std::vector<uint8_t> hlive;
+  size_t ndead = 0;
+  bool live(size_t r) const { return hlive.empty() || hlive[r]; }
   // Rows the column stores as a residue that differs from the operand the caller appended (operands
   // >= 2N, negative decimal rows): their original value. A one-operand fold returns the operand
   // itself, unreduced (DDSRestServer.scala:416-417); rows below 2N are stored verbatim.
@@ -243,6 +256,7 @@ struct dds_col {
   std::map<size_t, Orig> orig;
   ~dds_col() {
     if (d) (void)hipFree(d);
+    if (dlive) (void)hipFree(dlive);
   }
 };
 
@@ -479,8 +493,29 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
                size_t stride, uint32_t* orflags, std::vector<size_t>* long_rows);
 // indices of rows whose status has any bit of `mask` (after ingest_dec)
 int dec_rows_with(Worker* w, hipStream_t st, size_t count, uint32_t mask, std::vector<size_t>* rows);
-// SumAll/MultAll over resident rows: row_ids[0..n) or [first, first+n); value + sign of the result
+// SumAll/MultAll over the LIVE resident rows among row_ids[0..n) or [first, first+n); value + sign of
+// the result. The caller holds col->mu (shared).
 int col_fold_value(dds_col* col, const uint64_t* row_ids, size_t first, size_t n, bn::Limbs* v, bool* neg);
+// Live rows of [first, first+count) of a column (caller holds col->mu): *d_ids = nullptr and *n = count
+// when no row of the column is dead; else the live rows' offsets from `first`, ascending, compacted on
+// the GPU into w->ids, and their number (one small read-back).
+int col_live_range(dds_col* col, Worker* w, hipStream_t st, size_t first, size_t count, const uint32_t** d_ids,
+                   size_t* n);
+// Row ids of the list that are live (caller holds col->mu)
+std::vector<uint64_t> col_live_ids(const dds_col* col, const uint64_t* ids, size_t n);
+// dds_col_write_rows[_dec] in two phases (caller holds col->mu exclusively): prepare ingests and validates
+// the new operands into the lease's scratch (the column is untouched, so a failure anywhere — in any
+// shard of a dds_mcol — leaves every column unchanged); commit scatters them into the rows.
+struct RowWrite {
+  std::unique_ptr<WorkerLease> wl;
+  std::vector<uint32_t> ids32;                                 // distinct target rows
+  std::vector<std::pair<size_t, dds_col::Orig>> origs;         // (index into ids32, appended operand)
+  size_t ss = 0;                                               // scratch stride (rows)
+};
+int col_write_prepare(dds_col* col, const uint64_t* ids, size_t n, const uint8_t* ops, size_t width,
+                      const char* chars, const uint64_t* offsets, RowWrite* plan);
+int col_write_commit(dds_col* col, RowWrite& plan);
+int col_set_live(dds_col* col, const uint64_t* ids, size_t n, const uint8_t* live);
 int combine_partials(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, const uint32_t* h_parts,
                      const uint32_t* d_parts, const uint64_t* rows, size_t nparts, uint8_t* out, size_t out_cap,
                      size_t* out_len);

@@ -685,6 +685,56 @@ __global__ void __launch_bounds__(kOpeBlock) k_flag_count(const uint32_t* __rest
   ope_store_mask(m, masks, counts, blockIdx.x);
 }
 
+// Byte-mask compaction front end (live rows of a resident column, dds_col_set_live): same tile layout
+// and masks as k_ope_count, predicate (b[r] & vmask) != 0 on a byte per row. `bytes` may start at any
+// offset (a row range of the mask): 4-byte loads only when it is aligned.
+__global__ void __launch_bounds__(kOpeBlock) k_byte_count(const uint8_t* __restrict__ bytes, size_t n, uint32_t vmask,
+                                                          uint32_t* __restrict__ masks,
+                                                          uint32_t* __restrict__ counts) {
+  const size_t t0 = (size_t)blockIdx.x * kOpeTile + 4 * (size_t)threadIdx.x;
+  uint32_t v[kOpeGroups];
+  if ((uintptr_t)bytes % 4 == 0 && t0 + (kOpeGroups - 1) * 4 * kOpeBlock + 3 < n) {
+#pragma unroll
+    for (int k = 0; k < kOpeGroups; ++k)
+      v[k] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(bytes + t0 + (size_t)k * 4 * kOpeBlock));
+  } else {
+#pragma unroll
+    for (int k = 0; k < kOpeGroups; ++k) {
+      uint32_t vk = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t r = t0 + (size_t)k * 4 * kOpeBlock + j;
+        vk |= (r < n ? (uint32_t)bytes[r] : 0u) << (8 * j);
+      }
+      v[k] = vk;
+    }
+  }
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < kOpeGroups; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((v[k] >> (8 * j)) & vmask) m |= 1u << (4 * k + j);
+  ope_store_mask(m, masks, counts, blockIdx.x);
+}
+
+// Total of the per-tile match counts (one block): the match count of a bitmask-only Search
+// (dds_opecol_search_mask), written next to the mask words so one copy brings both back.
+__global__ void __launch_bounds__(1024) k_count_total(const uint32_t* __restrict__ counts, size_t ntiles,
+                                                      uint64_t* __restrict__ total) {
+  __shared__ uint64_t ws[16];
+  uint64_t s = 0;
+  for (size_t t = threadIdx.x; t < ntiles; t += 1024) s += counts[t];
+  for (int off = 32; off >= 1; off >>= 1) s += (uint64_t)__shfl_xor((long long)s, off);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < 16; ++w) t += ws[w];
+    *total = t;
+  }
+}
+
 // inclusive prefix sum over the 64 lanes of a wave (DPP row shifts + row broadcasts: no LDS round trips)
 __device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
@@ -1221,29 +1271,65 @@ hipError_t launch_flag_compact(const uint32_t* flags, size_t n, uint32_t req, vo
   return hipGetLastError();
 }
 
-hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
-                             uint64_t* total, uint32_t* out, hipStream_t st, uint32_t vmask, uint32_t vbad) {
+hipError_t launch_byte_compact(const uint8_t* bytes, size_t n, uint32_t vmask, void* scratch, uint64_t* total,
+                               uint32_t* out, hipStream_t st) {
   const size_t nb = ope_blocks(n);
   if (nb == 0) return hipSuccess;
   uint32_t* counts = (uint32_t*)scratch;
   uint32_t* masks = counts + nb;
-  // gt: c > b; le: !(c > b); ge: c > b-1; lt: !(c > b-1); b-1 underflows only for b = INT64_MIN, where
-  // ge keeps every row and lt none
-  int64_t t = bound;
-  int code = 0;
+  hipLaunchKernelGGL(k_byte_count, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, bytes, n, vmask, masks, counts);
+  hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, masks, counts, out, total);
+  return hipGetLastError();
+}
+
+namespace {
+// gt: c > b; le: !(c > b); ge: c > b-1; lt: !(c > b-1); b-1 underflows only for b = INT64_MIN, where
+// ge keeps every row and lt none
+void ope_code(int64_t bound, int op, int64_t* t, int* code) {
+  *t = bound;
+  *code = 0;
   switch (op) {
     case 0: break;
-    case 3: code = 1; break;
-    case 1: if (bound == INT64_MIN) code = 2; else t = bound - 1; break;
-    default: if (bound == INT64_MIN) code = 4; else { t = bound - 1; code = 1; } break;
+    case 3: *code = 1; break;
+    case 1: if (bound == INT64_MIN) *code = 2; else *t = bound - 1; break;
+    default: if (bound == INT64_MIN) *code = 4; else { *t = bound - 1; *code = 1; } break;
   }
+}
+void ope_count(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, uint32_t* masks,
+               uint32_t* counts, hipStream_t st, uint32_t vmask, uint32_t vbad) {
+  const size_t nb = ope_blocks(n);
+  int64_t t;
+  int code;
+  ope_code(bound, op, &t, &code);
   if (valid)
     hipLaunchKernelGGL(k_ope_count<true>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, t, code, vmask,
                        vbad, masks, counts);
   else
     hipLaunchKernelGGL(k_ope_count<false>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, t, code, vmask,
                        vbad, masks, counts);
+}
+}  // namespace
+
+hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
+                             uint64_t* total, uint32_t* out, hipStream_t st, uint32_t vmask, uint32_t vbad) {
+  const size_t nb = ope_blocks(n);
+  if (nb == 0) return hipSuccess;
+  uint32_t* counts = (uint32_t*)scratch;
+  uint32_t* masks = counts + nb;
+  ope_count(col, valid, n, bound, op, masks, counts, st, vmask, vbad);
   hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, masks, counts, out, total);
+  return hipGetLastError();
+}
+
+uint32_t* ope_mask_words(void* scratch, size_t n) { return (uint32_t*)scratch + ope_blocks(n); }
+
+hipError_t launch_ope_mask(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
+                           uint64_t* total, hipStream_t st, uint32_t vmask, uint32_t vbad) {
+  const size_t nb = ope_blocks(n);
+  if (nb == 0) return hipSuccess;
+  uint32_t* counts = (uint32_t*)scratch;
+  ope_count(col, valid, n, bound, op, counts + nb, counts, st, vmask, vbad);
+  hipLaunchKernelGGL(k_count_total, dim3(1), dim3(1024), 0, st, counts, nb, total);
   return hipGetLastError();
 }
 

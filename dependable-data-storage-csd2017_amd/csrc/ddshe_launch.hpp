@@ -110,6 +110,22 @@ hipError_t launch_flag_compact(const uint32_t* flags, size_t n, uint32_t req, vo
 hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
                              uint64_t* total, uint32_t* out, hipStream_t st, uint32_t vmask = 0xFFu,
                              uint32_t vbad = 0u);
+// Search as a row bitmask (no id scatter): after it, ope_mask_words(scratch, n)[w] bit b = row 32w + b
+// matches (words in row order; bits past n are 0) and *total (device) the number of matches
+hipError_t launch_ope_mask(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
+                           uint64_t* total, hipStream_t st, uint32_t vmask = 0xFFu, uint32_t vbad = 0u);
+uint32_t* ope_mask_words(void* scratch, size_t n);
+// rows i with (bytes[i] & vmask) != 0 -> ascending ids in out, count in *total (device); scratch as above
+hipError_t launch_byte_compact(const uint8_t* bytes, size_t n, uint32_t vmask, void* scratch, uint64_t* total,
+                               uint32_t* out, hipStream_t st);
+// resident-row mutations (ddshe_mutate.hip): rows ids[i] of dst (S limbs, stride dstride) <- column i of
+// src (stride sstride); dst[ids[i]] <- vals[i] for bytes / u64; keep[p] = !dead[perm[p]]; dst[i] = src[idx[i]]
+hipError_t launch_scatter_rows(const uint32_t* src, size_t sstride, const uint32_t* ids, size_t n, int S, uint32_t* dst,
+                               size_t dstride, hipStream_t st);
+hipError_t launch_scatter_bytes(const uint32_t* ids, const uint8_t* vals, size_t n, uint8_t* dst, hipStream_t st);
+hipError_t launch_scatter_u64(const uint32_t* ids, const uint64_t* vals, size_t n, uint64_t* dst, hipStream_t st);
+hipError_t launch_perm_keep(const uint32_t* perm, const uint8_t* dead, size_t n, uint8_t* keep, hipStream_t st);
+hipError_t launch_gather_u32(const uint32_t* src, const uint32_t* idx, size_t n, uint32_t* dst, hipStream_t st);
 // OPE ordering (ddshe_sort.hip): stable radix sort of the int64 column -> row ids
 size_t rs_scratch_bytes(size_t n);
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,

@@ -10,6 +10,12 @@
 //   kNotStr the element is not a String (Order's asInstanceOf[String] throws; Search's toString does not)
 // The reference throws lazily, inside the loop, only for rows the loop reaches; the column keeps the
 // counts needed to reproduce exactly when a request answers 500 instead of a key list.
+//
+// Rows follow the write routes (dds_opecol_write_rows*, dds_opecol_set_live): WriteElement / AddElement
+// change a row's element or class (:220-321), RemoveSet makes its set None (:207-218), which every
+// route filters out before its loop (filter(nonEmpty), :553, :586, :700). A dead row's device class
+// byte is 0 (no Search match, an Order non-holder) and d_dead marks it, so Order drops it from the
+// permutation; its host class stays in hflg for a later revival. The counts cover live rows only.
 #include "ddshe_host.hpp"
 
 using namespace ddshe;
@@ -24,8 +30,11 @@ struct dds_opecol {
   size_t capacity = 0, count = 0;
   int64_t* d_val = nullptr;
   uint8_t* d_flg = nullptr;
+  uint8_t* d_dead = nullptr;                            // 1 = removed set (allocated with the first one)
   std::mutex mu;
-  std::vector<uint8_t> hflg;                            // host mirror of the class bytes
+  std::vector<uint8_t> hflg;                            // host mirror of the class bytes (dead rows too)
+  std::vector<uint8_t> hdead;                           // host mirror of d_dead (empty: none dead yet)
+  size_t ndead = 0;
   std::map<size_t, std::pair<bn::Limbs, bool>> wide;  // kWide rows: exact value (magnitude, negative)
   size_t n_search = 0, n_hold = 0;
   size_t n_search_bad = 0;  // kSearch rows that Search's BigInteger parse rejects
@@ -33,7 +42,9 @@ struct dds_opecol {
   ~dds_opecol() {
     if (d_val) (void)hipFree(d_val);
     if (d_flg) (void)hipFree(d_flg);
+    if (d_dead) (void)hipFree(d_dead);
   }
+  bool dead(size_t r) const { return !hdead.empty() && hdead[r]; }
   void account(uint8_t f, int sign) {
     const size_t d = (size_t)1;
     auto upd = [&](size_t& c, bool on) {
@@ -113,6 +124,96 @@ int append_rows(dds_opecol* col, const int64_t* vals, const uint8_t* flg, size_t
 
 uint8_t class_bits(uint8_t cls) { return cls == 0 ? 0 : (cls == 1 ? kHold : (uint8_t)(kHold | kSearch)); }
 
+// Rows given as element text (append_dec / write_rows_dec): value, class byte, exact value if wide
+struct OpeRows {
+  std::vector<int64_t> v;
+  std::vector<uint8_t> f;
+  std::vector<std::pair<size_t, std::pair<bn::Limbs, bool>>> wide;  // (index in the batch, value)
+};
+int parse_rows(const char* const* values, const uint8_t* cls, const uint8_t* is_string, size_t count, OpeRows* out) {
+  out->v.assign(count, 0);
+  out->f.assign(count, 0);
+  for (size_t i = 0; i < count; ++i) {
+    const uint8_t c = cls ? cls[i] : 2;
+    if (c > 2) return fail(DDS_E_ARG, "row class must be 0, 1 or 2");
+    out->f[i] = class_bits(c);
+    if (!out->f[i]) continue;  // the row lacks the position: its element is never read
+    if (!values[i]) return fail(DDS_E_ARG, "NULL element for a row that holds the position");
+    if (is_string && !is_string[i]) out->f[i] |= kNotStr;
+    bn::Limbs mag;
+    bool neg = false;
+    const int k = parse_ope(values[i], &out->v[i], &mag, &neg);
+    if (k < 0) {
+      out->f[i] |= kBad;
+    } else if (k > 0) {
+      out->f[i] |= kWide;
+      out->wide.emplace_back(i, std::make_pair(std::move(mag), neg));
+    }
+  }
+  return DDS_OK;
+}
+
+int class_rows(const uint8_t* cls, size_t count, std::vector<uint8_t>* f) {
+  f->resize(count);
+  for (size_t i = 0; i < count; ++i) {
+    const uint8_t c = cls ? cls[i] : 2;
+    if (c > 2) return fail(DDS_E_ARG, "row class must be 0, 1 or 2");
+    (*f)[i] = class_bits(c);
+  }
+  return DDS_OK;
+}
+
+int check_ids(const dds_opecol* col, const uint64_t* ids, size_t n) {
+  for (size_t i = 0; i < n; ++i)
+    if (ids[i] >= col->count) return fail(DDS_E_ARG, "row id " + std::to_string(ids[i]) + " out of range");
+  return DDS_OK;
+}
+
+// Rows ids[i] take (vals[i], flg[i]); repeated ids: the last entry wins. Counts, wide values and the
+// device copies follow; a dead row keeps class byte 0 on the device.
+int write_rows(dds_opecol* col, const uint64_t* ids, const int64_t* vals, const uint8_t* flg, size_t n,
+               const std::map<size_t, std::pair<bn::Limbs, bool>>& wide_in) {
+  std::map<uint64_t, size_t> last;
+  for (size_t i = 0; i < n; ++i) last[ids[i]] = i;
+  const size_t m = last.size();
+  std::vector<uint32_t> id32;
+  std::vector<int64_t> v;
+  std::vector<uint8_t> df;
+  id32.reserve(m);
+  v.reserve(m);
+  df.reserve(m);
+  for (auto& kv : last) {
+    id32.push_back((uint32_t)kv.first);
+    v.push_back(vals[kv.second]);
+    df.push_back(col->dead(kv.first) ? 0 : flg[kv.second]);
+  }
+  WorkerLease wl(col->ctx);
+  int rc;
+  if ((rc = wl.acquire())) return rc;
+  Worker* w = wl.w;
+  HIP_TRY(w->ids.ensure(m * 4));
+  HIP_TRY(w->in.ensure(m * 8));
+  HIP_TRY(w->in2.ensure(m));
+  HIP_TRY(hipMemcpyAsync(w->ids.p, id32.data(), m * 4, hipMemcpyHostToDevice, wl.st));
+  HIP_TRY(hipMemcpyAsync(w->in.p, v.data(), m * 8, hipMemcpyHostToDevice, wl.st));
+  HIP_TRY(hipMemcpyAsync(w->in2.p, df.data(), m, hipMemcpyHostToDevice, wl.st));
+  HIP_TRY(launch_scatter_u64(w->ids.as<uint32_t>(), w->in.as<uint64_t>(), m, (uint64_t*)col->d_val, wl.st));
+  HIP_TRY(launch_scatter_bytes(w->ids.as<uint32_t>(), w->in2.as<uint8_t>(), m, col->d_flg, wl.st));
+  HIP_TRY(hipStreamSynchronize(wl.st));
+  for (auto& kv : last) {
+    const size_t r = (size_t)kv.first, i = kv.second;
+    if (!col->dead(r)) {
+      col->account(col->hflg[r], -1);
+      col->account(flg[i], +1);
+    }
+    col->hflg[r] = flg[i];
+    col->wide.erase(r);
+    auto it = wide_in.find(i);
+    if (it != wide_in.end()) col->wide.emplace(r, it->second);
+  }
+  return DDS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -148,7 +249,20 @@ int dds_opecol_truncate(dds_opecol* col, size_t count) {
   if (!col) return fail(DDS_E_ARG, "bad arguments");
   std::lock_guard<std::mutex> lk(col->mu);
   if (count > col->count) return fail(DDS_E_ARG, "truncate beyond the row count");
-  for (size_t i = count; i < col->count; ++i) col->account(col->hflg[i], -1);
+  size_t undead = 0;
+  for (size_t i = count; i < col->count; ++i) {
+    if (!col->dead(i)) {
+      col->account(col->hflg[i], -1);
+    } else {
+      col->hdead[i] = 0;
+      ++undead;
+    }
+  }
+  if (undead) {  // rows past the count are never dead
+    HIP_TRY(hipSetDevice(col->ctx->device));
+    HIP_TRY(hipMemset(col->d_dead + count, 0, col->count - count));
+    col->ndead -= undead;
+  }
   col->hflg.resize(count);
   col->wide.erase(col->wide.lower_bound(count), col->wide.end());
   col->count = count;
@@ -180,33 +294,171 @@ int dds_opecol_append_dec(dds_opecol* col, const char* const* values, const uint
     std::lock_guard<std::mutex> lk(col->mu);
     if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
     if (count == 0) return DDS_OK;
-    std::vector<int64_t> v(count, 0);
-    std::vector<uint8_t> f(count);
-    std::vector<std::pair<size_t, std::pair<bn::Limbs, bool>>> wide;
-    for (size_t i = 0; i < count; ++i) {
-      const uint8_t c = cls ? cls[i] : 2;
-      if (c > 2) return fail(DDS_E_ARG, "row class must be 0, 1 or 2");
-      f[i] = class_bits(c);
-      if (!f[i]) continue;  // the row lacks the position: its element is never read
-      if (!values[i]) return fail(DDS_E_ARG, "NULL element for a row that holds the position");
-      if (is_string && !is_string[i]) f[i] |= kNotStr;
-      bn::Limbs mag;
-      bool neg = false;
-      const int k = parse_ope(values[i], &v[i], &mag, &neg);
-      if (k < 0) {
-        f[i] |= kBad;
-      } else if (k > 0) {
-        f[i] |= kWide;
-        wide.emplace_back(col->count + i, std::make_pair(std::move(mag), neg));
-      }
-    }
-    int rc = append_rows(col, v.data(), f.data(), count);
+    OpeRows rows;
+    int rc = parse_rows(values, cls, is_string, count, &rows);
     if (rc) return rc;
-    for (auto& e : wide) col->wide.emplace(e.first, std::move(e.second));
+    const size_t base = col->count;
+    if ((rc = append_rows(col, rows.v.data(), rows.f.data(), count))) return rc;
+    for (auto& e : rows.wide) col->wide.emplace(base + e.first, std::move(e.second));
     return DDS_OK;
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");
   }
+}
+
+}  // extern "C"
+
+namespace {
+
+// Search prelude (:702-704): the bound is parsed inside the per-row condition, after the guard, i.e.
+// only if some live row passes the guard; any qualifying row the parse rejects fails the request
+// (500). *none: no row qualifies (no match, any bound). Else the GPU predicate: int64 rows against
+// the bound clamped to int64 (an equivalent predicate there), *b / *gop.
+struct SearchBound {
+  bool none = false;
+  bn::Limbs bmag;
+  bool bneg = false;
+  int64_t b = 0;
+  int gop = 0;
+};
+int search_bound(const dds_opecol* col, const char* bound_dec, int op, SearchBound* sb) {
+  if (col->n_search == 0) {
+    sb->none = true;
+    return DDS_OK;
+  }
+  if (!bound_dec) return fail(DDS_E_ARG, "bound missing");
+  if (!bn::from_dec(bound_dec, strlen(bound_dec), sb->bmag, &sb->bneg))
+    return fail(DDS_E_FORMAT, std::string("NumberFormatException: bound ") + bound_dec);
+  if (col->n_search_bad) return fail(DDS_E_FORMAT, "NumberFormatException: a qualifying row is not an integer");
+  sb->gop = op;
+  int64_t bv;
+  bn::Limbs m2;
+  bool n2;
+  const std::string bt = bn::to_dec(sb->bmag, sb->bneg);
+  if (parse_ope(bt.c_str(), &bv, &m2, &n2) == 0) {
+    sb->b = bv;
+  } else if (!sb->bneg) {  // bound > INT64_MAX: col > / >= bound never, col < / <= bound always
+    sb->gop = (op == DDS_OPE_GT || op == DDS_OPE_GE) ? DDS_OPE_GT : DDS_OPE_LE;
+    sb->b = INT64_MAX;
+  } else {                 // bound < INT64_MIN: col > / >= bound always, col < / <= bound never
+    sb->gop = (op == DDS_OPE_GT || op == DDS_OPE_GE) ? DDS_OPE_GE : DDS_OPE_LT;
+    sb->b = INT64_MIN;
+  }
+  return DDS_OK;
+}
+
+// live rows outside int64 that match: exact BigInteger compare on the host, ascending
+std::vector<uint32_t> wide_matches(const dds_opecol* col, const SearchBound& sb, int op) {
+  std::vector<uint32_t> extra;
+  for (const auto& e : col->wide)
+    if (!col->dead(e.first) && (col->hflg[e.first] & kSearch) &&
+        ope_pred(scmp(e.second.second, e.second.first, sb.bneg, sb.bmag), op))
+      extra.push_back((uint32_t)e.first);
+  return extra;
+}
+
+void add_filter_time(dds_ctx* ctx, Worker* w) {
+  if (!ctx->timing.load()) return;
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, w->ev[2], w->ev[3]) == hipSuccess) {
+    std::lock_guard<std::mutex> tk(ctx->tmu);
+    ctx->total_ms += ms;
+  }
+}
+
+int set_dead(dds_opecol* col, const uint64_t* ids, size_t n, const uint8_t* live) {
+  std::map<uint64_t, uint8_t> last;  // last flag of each id wins
+  for (size_t i = 0; i < n; ++i) last[ids[i]] = live[i] ? 0 : 1;
+  std::vector<uint32_t> id32;
+  std::vector<uint8_t> dead, flg;
+  for (auto& kv : last)
+    if (col->dead(kv.first) != (kv.second != 0)) {
+      id32.push_back((uint32_t)kv.first);
+      dead.push_back(kv.second);
+      flg.push_back(kv.second ? 0 : col->hflg[kv.first]);
+    }
+  if (id32.empty()) return DDS_OK;
+  if (!col->d_dead) {
+    HIP_TRY(hipSetDevice(col->ctx->device));
+    if (hipMalloc(&col->d_dead, col->capacity + 16) != hipSuccess) return fail(DDS_E_NOMEM, "OPE dead mask");
+    HIP_TRY(hipMemset(col->d_dead, 0, col->capacity + 16));
+  }
+  WorkerLease wl(col->ctx);
+  int rc;
+  if ((rc = wl.acquire())) return rc;
+  Worker* w = wl.w;
+  const size_t m = id32.size();
+  HIP_TRY(w->ids.ensure(m * 4));
+  HIP_TRY(w->in.ensure(m));
+  HIP_TRY(w->in2.ensure(m));
+  HIP_TRY(hipMemcpyAsync(w->ids.p, id32.data(), m * 4, hipMemcpyHostToDevice, wl.st));
+  HIP_TRY(hipMemcpyAsync(w->in.p, dead.data(), m, hipMemcpyHostToDevice, wl.st));
+  HIP_TRY(hipMemcpyAsync(w->in2.p, flg.data(), m, hipMemcpyHostToDevice, wl.st));
+  HIP_TRY(launch_scatter_bytes(w->ids.as<uint32_t>(), w->in.as<uint8_t>(), m, col->d_dead, wl.st));
+  HIP_TRY(launch_scatter_bytes(w->ids.as<uint32_t>(), w->in2.as<uint8_t>(), m, col->d_flg, wl.st));
+  HIP_TRY(hipStreamSynchronize(wl.st));
+  if (col->hdead.empty()) col->hdead.assign(col->capacity, 0);
+  for (size_t j = 0; j < m; ++j) {
+    const size_t r = id32[j];
+    col->account(col->hflg[r], dead[j] ? -1 : +1);
+    col->hdead[r] = dead[j];
+    col->ndead = dead[j] ? col->ndead + 1 : col->ndead - 1;
+  }
+  return DDS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dds_opecol_write_rows(dds_opecol* col, const uint64_t* row_ids, const int64_t* values, const uint8_t* cls,
+                          size_t n) {
+  try {
+    if (!col || (n && (!row_ids || !values))) return fail(DDS_E_ARG, "bad arguments");
+    std::lock_guard<std::mutex> lk(col->mu);
+    int rc = check_ids(col, row_ids, n);
+    if (rc || n == 0) return rc;
+    std::vector<uint8_t> f;
+    if ((rc = class_rows(cls, n, &f))) return rc;
+    return write_rows(col, row_ids, values, f.data(), n, {});
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_opecol_write_rows_dec(dds_opecol* col, const uint64_t* row_ids, const char* const* values,
+                              const uint8_t* cls, const uint8_t* is_string, size_t n) {
+  try {
+    if (!col || (n && (!row_ids || !values))) return fail(DDS_E_ARG, "bad arguments");
+    std::lock_guard<std::mutex> lk(col->mu);
+    int rc = check_ids(col, row_ids, n);
+    if (rc || n == 0) return rc;
+    OpeRows rows;
+    if ((rc = parse_rows(values, cls, is_string, n, &rows))) return rc;
+    std::map<size_t, std::pair<bn::Limbs, bool>> wide;
+    for (auto& e : rows.wide) wide.emplace(e.first, std::move(e.second));
+    return write_rows(col, row_ids, rows.v.data(), rows.f.data(), n, wide);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_opecol_set_live(dds_opecol* col, const uint64_t* row_ids, size_t n, const uint8_t* live) {
+  try {
+    if (!col || (n && (!row_ids || !live))) return fail(DDS_E_ARG, "bad arguments");
+    std::lock_guard<std::mutex> lk(col->mu);
+    int rc = check_ids(col, row_ids, n);
+    if (rc || n == 0) return rc;
+    return set_dead(col, row_ids, n, live);
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+size_t dds_opecol_live_count(dds_opecol* col) {
+  if (!col) return 0;
+  std::lock_guard<std::mutex> lk(col->mu);
+  return col->count - col->ndead;
 }
 
 int dds_opecol_search(dds_opecol* col, const char* bound_dec, int op, uint32_t* out_idx, size_t* out_n) {
@@ -214,36 +466,11 @@ int dds_opecol_search(dds_opecol* col, const char* bound_dec, int op, uint32_t* 
     if (!col || !out_n || op < 0 || op > 3 || (col->count && !out_idx)) return fail(DDS_E_ARG, "bad arguments");
     *out_n = 0;
     std::lock_guard<std::mutex> lk(col->mu);
-    // the bound is parsed inside the per-row condition, after the guard (:702-704): only if some row
-    // passes the guard; any qualifying row the parse rejects fails the whole request (500)
-    if (col->n_search == 0) return DDS_OK;
-    if (!bound_dec) return fail(DDS_E_ARG, "bound missing");
-    bn::Limbs bmag;
-    bool bneg = false;
-    if (!bn::from_dec(bound_dec, strlen(bound_dec), bmag, &bneg))
-      return fail(DDS_E_FORMAT, std::string("NumberFormatException: bound ") + bound_dec);
-    if (col->n_search_bad) return fail(DDS_E_FORMAT, "NumberFormatException: a qualifying row is not an integer");
-    // int64 rows on the GPU against the bound clamped to int64 (an equivalent predicate there)
-    int64_t b = 0;
-    int gop = op;
-    {
-      int64_t bv;
-      bn::Limbs m2;
-      bool n2;
-      const std::string bt = bn::to_dec(bmag, bneg);
-      if (parse_ope(bt.c_str(), &bv, &m2, &n2) == 0) {
-        b = bv;
-      } else if (!bneg) {  // bound > INT64_MAX: col > / >= bound never, col < / <= bound always
-        gop = (op == DDS_OPE_GT || op == DDS_OPE_GE) ? DDS_OPE_GT : DDS_OPE_LE;
-        b = INT64_MAX;
-      } else {             // bound < INT64_MIN: col > / >= bound always, col < / <= bound never
-        gop = (op == DDS_OPE_GT || op == DDS_OPE_GE) ? DDS_OPE_GE : DDS_OPE_LT;
-        b = INT64_MIN;
-      }
-    }
+    SearchBound sb;
+    int rc = search_bound(col, bound_dec, op, &sb);
+    if (rc || sb.none) return rc;
     dds_ctx* ctx = col->ctx;
     WorkerLease wl(ctx);
-    int rc;
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
     const size_t n = col->count;
@@ -251,25 +478,20 @@ int dds_opecol_search(dds_opecol* col, const char* bound_dec, int op, uint32_t* 
     HIP_TRY(w->flags.ensure(16));
     HIP_TRY(w->out.ensure(n * 4));
     record_time(ctx, w, wl.st, true, 2);
-    HIP_TRY(launch_ope_filter(col->d_val, col->d_flg, n, b, gop, w->misc.p, w->flags.as<uint64_t>(),
+    HIP_TRY(launch_ope_filter(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, w->flags.as<uint64_t>(),
                               w->out.as<uint32_t>(), wl.st, kSearch, kWide));
     record_time(ctx, w, wl.st, false, 2);
     uint64_t total = 0;
     HIP_TRY(read_sync(w, wl.st, w->flags.p, &total, 8));
-    if (total) HIP_TRY(hipMemcpy(out_idx, w->out.p, total * 4, hipMemcpyDeviceToHost));
-    if (ctx->timing.load()) {
-      float ms = 0;
-      if (hipEventElapsedTime(&ms, w->ev[2], w->ev[3]) == hipSuccess) {
-        std::lock_guard<std::mutex> tk(ctx->tmu);
-        ctx->total_ms += ms;
-      }
+    if (total) {  // through pinned staging (a pageable copy of ~20 MB runs at a fraction of the link)
+      HIP_TRY(w->hbig.ensure(total * 4));
+      HIP_TRY(hipMemcpyAsync(w->hbig.p, w->out.p, total * 4, hipMemcpyDeviceToHost, wl.st));
+      HIP_TRY(hipStreamSynchronize(wl.st));
+      CopyPool::get().copy(out_idx, w->hbig.p, total * 4);
     }
+    add_filter_time(ctx, w);
     size_t got = (size_t)total;
-    // rows outside int64: exact BigInteger compare here, merged in row order
-    std::vector<uint32_t> extra;
-    for (const auto& e : col->wide)
-      if ((col->hflg[e.first] & kSearch) && ope_pred(scmp(e.second.second, e.second.first, bneg, bmag), op))
-        extra.push_back((uint32_t)e.first);
+    const std::vector<uint32_t> extra = wide_matches(col, sb, op);  // merged in row order
     if (!extra.empty()) {
       std::vector<uint32_t> merged(got + extra.size());
       std::merge(out_idx, out_idx + got, extra.begin(), extra.end(), merged.begin());
@@ -283,11 +505,64 @@ int dds_opecol_search(dds_opecol* col, const char* bound_dec, int op, uint32_t* 
   }
 }
 
-int dds_opecol_order(dds_opecol* col, int descending, uint32_t* out_idx) {
+int dds_opecol_search_mask(dds_opecol* col, const char* bound_dec, int op, uint64_t* mask, size_t mask_words,
+                           size_t* out_n) {
+  try {
+    if (!col || !out_n || op < 0 || op > 3) return fail(DDS_E_ARG, "bad arguments");
+    *out_n = 0;
+    std::lock_guard<std::mutex> lk(col->mu);
+    const size_t n = col->count, words = (n + 63) / 64;
+    if (mask_words < words || (words && !mask)) return fail(DDS_E_BUFSIZE, "mask needs ceil(count / 64) words");
+    SearchBound sb;
+    int rc = search_bound(col, bound_dec, op, &sb);
+    if (rc) return rc;
+    if (sb.none || n == 0) {
+      if (words) memset(mask, 0, words * 8);
+      return DDS_OK;
+    }
+    dds_ctx* ctx = col->ctx;
+    WorkerLease wl(ctx);
+    if ((rc = wl.acquire())) return rc;
+    Worker* w = wl.w;
+    // match words in row order (u32 word k = rows [32k, 32k + 32), little-endian: two of them are the
+    // u64 word of the caller's layout) + the match count, back in one copy
+    const size_t bytes = words * 8;
+    HIP_TRY(w->misc.ensure(ope_scratch_bytes(n) + 64));
+    HIP_TRY(w->hbig.ensure(bytes + 8));
+    uint32_t* mw = ope_mask_words(w->misc.p, n);
+    uint64_t* dtotal = (uint64_t*)(((uintptr_t)w->misc.p + ope_scratch_bytes(n) + 7) & ~(uintptr_t)7);  // past the masks
+    record_time(ctx, w, wl.st, true, 2);
+    HIP_TRY(launch_ope_mask(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, dtotal, wl.st, kSearch, kWide));
+    record_time(ctx, w, wl.st, false, 2);
+    uint8_t* h = (uint8_t*)w->hbig.p;
+    HIP_TRY(hipMemcpyAsync(h, mw, bytes, hipMemcpyDeviceToHost, wl.st));
+    HIP_TRY(hipMemcpyAsync(h + bytes, dtotal, 8, hipMemcpyDeviceToHost, wl.st));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    uint64_t total = 0;
+    memcpy(&total, h + bytes, 8);
+    if (bytes >= ((size_t)1 << 20)) {
+      CopyPool::get().parallel_for(bytes, 4096, [&](size_t a, size_t e) { memcpy((char*)mask + a, h + a, e - a); });
+    } else {
+      memcpy(mask, h, bytes);
+    }
+    add_filter_time(ctx, w);
+    for (uint32_t r : wide_matches(col, sb, op)) {
+      mask[r / 64] |= 1ull << (r % 64);
+      ++total;
+    }
+    *out_n = (size_t)total;
+    return DDS_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(DDS_E_NOMEM, "host allocation");
+  }
+}
+
+int dds_opecol_order(dds_opecol* col, int descending, uint32_t* out_idx, size_t* out_n) {
   try {
     if (!col || (col->count && !out_idx)) return fail(DDS_E_ARG, "bad arguments");
     std::lock_guard<std::mutex> lk(col->mu);
     const size_t n = col->count;
+    if (out_n) *out_n = 0;
     if (n == 0) return DDS_OK;
     // sortWith parses only when comparing two holders, and every holder meets another one when there
     // are two or more: then one element that is not a String holding a Long fails the request
@@ -299,10 +574,31 @@ int dds_opecol_order(dds_opecol* col, int descending, uint32_t* out_idx) {
     Worker* w = wl.w;
     HIP_TRY(w->tab.ensure(rs_scratch_bytes(n)));
     HIP_TRY(w->out.ensure(n * 4));
-    // the sort's valid test is flag != 0, i.e. kHold (rows lacking the position have no other bit)
+    // the sort's valid test is flag != 0, i.e. kHold (rows lacking the position have no other bit; a
+    // removed set's device byte is 0, so it sorts with them)
     HIP_TRY(launch_ope_order(col->d_val, col->d_flg, n, descending ? 1 : 0, w->tab.p, w->out.as<uint32_t>(), wl.st));
-    HIP_TRY(hipMemcpyAsync(out_idx, w->out.p, n * 4, hipMemcpyDeviceToHost, wl.st));
+    const uint32_t* res = w->out.as<uint32_t>();
+    size_t m = n;
+    if (col->ndead) {  // drop removed sets from the permutation, order kept (filter(nonEmpty), :553, :586)
+      m = n - col->ndead;
+      HIP_TRY(w->in2.ensure(n));
+      HIP_TRY(w->misc.ensure(ope_scratch_bytes(n)));
+      HIP_TRY(w->ids.ensure(n * 4));
+      HIP_TRY(w->flags.ensure(16));
+      HIP_TRY(w->p1.ensure(n * 4));
+      HIP_TRY(launch_perm_keep(res, col->d_dead, n, w->in2.as<uint8_t>(), wl.st));
+      HIP_TRY(launch_byte_compact(w->in2.as<uint8_t>(), n, 1u, w->misc.p, w->flags.as<uint64_t>(),
+                                  w->ids.as<uint32_t>(), wl.st));
+      HIP_TRY(launch_gather_u32(res, w->ids.as<uint32_t>(), m, w->p1.as<uint32_t>(), wl.st));
+      res = w->p1.as<uint32_t>();
+    }
+    if (m) {
+      HIP_TRY(w->hbig.ensure(m * 4));
+      HIP_TRY(hipMemcpyAsync(w->hbig.p, res, m * 4, hipMemcpyDeviceToHost, wl.st));
+    }
     HIP_TRY(hipStreamSynchronize(wl.st));
+    if (m) CopyPool::get().copy(out_idx, w->hbig.p, m * 4);
+    if (out_n) *out_n = m;
     return DDS_OK;
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");

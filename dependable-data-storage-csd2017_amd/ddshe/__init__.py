@@ -55,6 +55,10 @@ EXPORTS = [
     "dds_mcol_destroy", "dds_mcol_count", "dds_mcol_append", "dds_mcol_append_dec", "dds_mcol_fill_paillier_synth",
     "dds_mcol_fold", "dds_mcol_fold_rows", "dds_mcol_fold_dec",
     "dds_pair_modmul_dec", "dds_pair_stats",
+    "dds_col_write_rows", "dds_col_write_rows_dec", "dds_col_set_live", "dds_col_live_count",
+    "dds_mcol_write_rows", "dds_mcol_write_rows_dec", "dds_mcol_set_live", "dds_mcol_live_count",
+    "dds_opecol_write_rows", "dds_opecol_write_rows_dec", "dds_opecol_set_live", "dds_opecol_live_count",
+    "dds_opecol_search_mask",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -133,7 +137,17 @@ _sig("dds_opecol_truncate", C.c_int, C.c_void_p, _sz)
 _sig("dds_opecol_append", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz)
 _sig("dds_opecol_append_dec", C.c_int, C.c_void_p, C.POINTER(C.c_char_p), C.c_void_p, C.c_void_p, _sz)
 _sig("dds_opecol_search", C.c_int, C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, _szp)
-_sig("dds_opecol_order", C.c_int, C.c_void_p, C.c_int, C.c_void_p)
+_sig("dds_opecol_order", C.c_int, C.c_void_p, C.c_int, C.c_void_p, _szp)
+_sig("dds_opecol_search_mask", C.c_int, C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, _sz, _szp)
+_sig("dds_opecol_write_rows", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, _sz)
+_sig("dds_opecol_write_rows_dec", C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_char_p), C.c_void_p, C.c_void_p, _sz)
+_sig("dds_opecol_set_live", C.c_int, C.c_void_p, C.c_void_p, _sz, C.c_void_p)
+_sig("dds_opecol_live_count", _sz, C.c_void_p)
+for _p in ("dds_col", "dds_mcol"):
+    _sig(_p + "_write_rows", C.c_int, C.c_void_p, C.c_void_p, _sz, C.c_void_p, _sz)
+    _sig(_p + "_write_rows_dec", C.c_int, C.c_void_p, C.c_void_p, _sz, C.c_char_p, C.c_void_p)
+    _sig(_p + "_set_live", C.c_int, C.c_void_p, C.c_void_p, _sz, C.c_void_p)
+    _sig(_p + "_live_count", _sz, C.c_void_p)
 _sig("dds_mctx_create", C.c_int, C.c_uint64, C.POINTER(C.c_void_p))
 _sig("dds_mctx_create_devices", C.c_int, C.POINTER(C.c_int), _sz, C.POINTER(C.c_void_p))
 _sig("dds_mctx_destroy", C.c_int, C.c_void_p)
@@ -178,6 +192,53 @@ def ints_to_be(xs, width: int) -> bytes:
 
 def nbytes(x: int) -> int:
     return max(1, (int(x).bit_length() + 7) // 8)
+
+
+def _ids(row_ids) -> np.ndarray:
+    return np.ascontiguousarray(row_ids, dtype=np.uint64)
+
+
+def _dec_rows(rows):
+    """(chars, uint64 offsets[len+1], count) of decimal rows (str / bytes) or an Arrow-style pair."""
+    if isinstance(rows, tuple):
+        chars, offs = rows
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        return chars, offs, len(offs) - 1
+    enc = [r.encode() if isinstance(r, str) else bytes(r) for r in rows]
+    offs = np.zeros(len(enc) + 1, dtype=np.uint64)
+    np.cumsum([len(e) for e in enc], out=offs[1:])
+    return b"".join(enc) or b"\0", offs, len(enc)
+
+
+class _Mutable:
+    """Row writes and the live mask of a resident ciphertext column (dds_col_* / dds_mcol_*): the
+    write routes WriteElement / AddElement / RemoveSet (DDSRestServer.scala:207-321) applied in place."""
+    _pre = ""
+
+    def write_rows(self, row_ids, ops):
+        ids = _ids(row_ids)
+        ops = [int(x) for x in ops]
+        assert len(ops) == len(ids)
+        width = max([self.mb] + [nbytes(x) for x in ops])
+        _check(getattr(_lib, self._pre + "_write_rows")(self._h, ids.ctypes.data, len(ids), ints_to_be(ops, width),
+                                                        width), self._pre + "_write_rows")
+
+    def write_rows_dec(self, row_ids, rows):
+        ids = _ids(row_ids)
+        chars, offs, n = _dec_rows(rows)
+        assert n == len(ids)
+        _check(getattr(_lib, self._pre + "_write_rows_dec")(self._h, ids.ctypes.data, n, chars, offs.ctypes.data),
+               self._pre + "_write_rows_dec")
+
+    def set_live(self, row_ids, live):
+        ids = _ids(row_ids)
+        flags = np.ascontiguousarray(np.broadcast_to(np.asarray(live, dtype=np.uint8), ids.shape))
+        _check(getattr(_lib, self._pre + "_set_live")(self._h, ids.ctypes.data, len(ids), flags.ctypes.data),
+               self._pre + "_set_live")
+
+    @property
+    def live_count(self) -> int:
+        return getattr(_lib, self._pre + "_live_count")(self._h)
 
 
 class Engine:
@@ -414,8 +475,9 @@ class Engine:
         return int.from_bytes(bytes(out[: olen.value]), "big")
 
 
-class Column:
+class Column(_Mutable):
     """Device-resident ciphertext column (dds_col)."""
+    _pre = "dds_col"
 
     def __init__(self, eng: Engine, modulus: int, capacity: int):
         self.eng, self.modulus, self.mb = eng, int(modulus), nbytes(modulus)
@@ -602,10 +664,46 @@ class OpeColumn:
                                       out.ctypes.data_as(C.c_void_p), C.byref(got)), "dds_opecol_search")
         return out[: got.value].copy()
 
+    def search_mask(self, bound, op: str):
+        """dds_opecol_search_mask: (uint64 words, bit r%64 of word r/64 = row r matches; match count)."""
+        words = np.zeros(max(1, (len(self) + 63) // 64), dtype=np.uint64)
+        got = C.c_size_t()
+        _check(_lib.dds_opecol_search_mask(self._h, None if bound is None else str(bound).encode(), OPE_OPS[op],
+                                           words.ctypes.data_as(C.c_void_p), len(words), C.byref(got)),
+               "dds_opecol_search_mask")
+        return words, got.value
+
     def order(self, descending: bool) -> np.ndarray:
         out = np.empty(max(1, len(self)), dtype=np.uint32)
-        _check(_lib.dds_opecol_order(self._h, int(descending), out.ctypes.data_as(C.c_void_p)), "dds_opecol_order")
-        return out[: len(self)].copy()
+        got = C.c_size_t()
+        _check(_lib.dds_opecol_order(self._h, int(descending), out.ctypes.data_as(C.c_void_p), C.byref(got)),
+               "dds_opecol_order")
+        return out[: got.value].copy()
+
+    def write_rows(self, row_ids, values, cls=None):
+        ids = _ids(row_ids)
+        v = np.ascontiguousarray(values, dtype=np.int64)
+        c = None if cls is None else np.ascontiguousarray(cls, dtype=np.uint8)
+        _check(_lib.dds_opecol_write_rows(self._h, ids.ctypes.data, v.ctypes.data,
+                                          None if c is None else c.ctypes.data, len(ids)), "dds_opecol_write_rows")
+
+    def write_rows_dec(self, row_ids, values, cls=None, is_string=None):
+        ids = _ids(row_ids)
+        n = len(ids)
+        arr = (C.c_char_p * max(1, n))(*[None if v is None else str(v).encode() for v in values])
+        c = None if cls is None else np.ascontiguousarray(cls, dtype=np.uint8)
+        st = None if is_string is None else np.ascontiguousarray(is_string, dtype=np.uint8)
+        _check(_lib.dds_opecol_write_rows_dec(self._h, ids.ctypes.data, arr, None if c is None else c.ctypes.data,
+                                              None if st is None else st.ctypes.data, n), "dds_opecol_write_rows_dec")
+
+    def set_live(self, row_ids, live):
+        ids = _ids(row_ids)
+        flags = np.ascontiguousarray(np.broadcast_to(np.asarray(live, dtype=np.uint8), ids.shape))
+        _check(_lib.dds_opecol_set_live(self._h, ids.ctypes.data, len(ids), flags.ctypes.data), "dds_opecol_set_live")
+
+    @property
+    def live_count(self) -> int:
+        return _lib.dds_opecol_live_count(self._h)
 
 
 class MultiEngine:
@@ -639,8 +737,9 @@ class MultiEngine:
         return MColumn(self, modulus, capacity)
 
 
-class MColumn:
+class MColumn(_Mutable):
     """dds_mcol: a column sharded over the devices of a MultiEngine (64-row blocks, round-robin)."""
+    _pre = "dds_mcol"
 
     def __init__(self, m: MultiEngine, modulus: int, capacity: int):
         self.m, self.modulus, self.mb = m, int(modulus), nbytes(modulus)

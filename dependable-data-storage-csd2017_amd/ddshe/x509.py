@@ -4,9 +4,12 @@ The route decodes it per use with ``KeyFactory.getInstance("RSA").generatePublic
 X509EncodedKeySpec(DatatypeConverter.parseHexBinary(pubkey)))`` (``DDSRestServer.scala:476-478,
 515-517``). This restates what that JDK chain accepts: an even-length hex string, a DER
 SubjectPublicKeyInfo { AlgorithmIdentifier { rsaEncryption, NULL }, BIT STRING { RSAPublicKey {
-modulus, publicExponent } } } with exact lengths and no trailing bytes, and a modulus of 512 to
-16384 bits (the JDK RSA key factory's limits). Anything else raises :class:`ValueError`, which the
-routes answer with 500 as the reference does.
+modulus, publicExponent } } } with exact lengths and no trailing bytes, and the JDK RSA key factory's
+length check (``RSAKeyFactory.checkRSAProviderKeyLengths``, called by the RSAPublicKeyImpl constructor):
+the modulus length rounded up to a multiple of 8 must be 512 to 16384 bits, and a modulus above 3072
+bits may not carry an exponent wider than 64 bits. Anything else raises :class:`ValueError`, which the
+routes answer with 500 as the reference does. (No JVM here: the check is restated from the JDK 8
+source, and the fixtures cover its edges; parity with a particular JDK build is unpinned.)
 """
 from __future__ import annotations
 
@@ -63,6 +66,16 @@ def rsa_modulus(pubkey_hex: str) -> int:
     e, k = _integer(key, k)
     if k != len(key) or n <= 0 or e <= 0:
         raise ValueError("DER: bad RSAPublicKey")
-    if not 512 <= n.bit_length() <= 16384:
-        raise ValueError("RSA modulus length outside [512, 16384] bits")
+    check_key_lengths(n, e)
     return n
+
+
+def check_key_lengths(n: int, e: int):
+    """RSAKeyFactory.checkRSAProviderKeyLengths(n.bitLength(), e)"""
+    mlen = (n.bit_length() + 7) & ~7
+    if mlen < 512:
+        raise ValueError("RSA keys must be at least 512 bits long")
+    if mlen > 16384:
+        raise ValueError("RSA keys must be no longer than 16384 bits")
+    if mlen > 3072 and e.bit_length() > 64:
+        raise ValueError("RSA exponents can be no more than 64 bits if modulus is greater than 3072 bits")

@@ -135,6 +135,25 @@ int dds_col_append_dec(dds_col* col, const char* chars, const uint64_t* offsets,
 size_t dds_col_count(const dds_col* col);
 /* drop rows [count, dds_col_count) (the storage is kept for later appends) */
 int dds_col_truncate(dds_col* col, size_t count);
+/* ---- resident rows follow the reference's write routes --------------------------------------
+ * The reference changes stored sets in place and re-fetches them on every request
+ * (DDSRestServer.scala:401-403): WriteElement overwrites contents(position) (:281-321), AddElement
+ * appends an element (:220-255), RemoveSet writes None (:207-218), PutSet of known contents rewrites
+ * its key (:170-188). A column row stands for one stored key; these keep it bit-exact without a
+ * re-upload:
+ *   dds_col_write_rows[_dec]: rows row_ids[0..n) (< dds_col_count) take new operands (validated and
+ *     stored exactly as dds_col_append / dds_col_append_dec would; a one-row fold then returns the new
+ *     operand unreduced). A repeated id takes its last value. On error the column is unchanged.
+ *   dds_col_set_live: live[i] == 0 takes row row_ids[i] out of every fold (a removed set, or a set
+ *     whose length no longer passes the route's guard), != 0 puts it back. Appended rows are live.
+ *   Every fold (dds_col_fold, _rows, _dec, _partial, _partial_device) folds the LIVE rows of its range
+ *   or id list; the 404 / one-operand rules apply to the live rows (a partial reports their number).
+ * Mutations wait for folds in flight on the column and folds wait for them (readers/writer lock). */
+int dds_col_write_rows(dds_col* col, const uint64_t* row_ids, size_t n, const uint8_t* operands_be, size_t width);
+int dds_col_write_rows_dec(dds_col* col, const uint64_t* row_ids, size_t n, const char* chars,
+                           const uint64_t* offsets);
+int dds_col_set_live(dds_col* col, const uint64_t* row_ids, size_t n, const uint8_t* live);
+size_t dds_col_live_count(dds_col* col);
 /* download rows [first, first+count) as canonical residues (x mod N), big-endian, mod_bytes each */
 int dds_col_read(dds_col* col, size_t first, size_t count, uint8_t* out);
 /* fold rows [first, first+count) (SumAll/MultAll semantics as dds_modmul_fold). A one-row fold returns
@@ -195,6 +214,13 @@ int dds_mcol_fold(dds_mcol* col, uint8_t* out, size_t out_cap, size_t* out_len);
 int dds_mcol_fold_rows(dds_mcol* col, const uint64_t* row_ids, size_t n, uint8_t* out, size_t out_cap,
                        size_t* out_len);
 int dds_mcol_fold_dec(dds_mcol* col, const uint64_t* row_ids, size_t n, char* out, size_t out_cap, size_t* out_len);
+/* dds_col_write_rows[_dec] / dds_col_set_live / dds_col_live_count on a sharded column (global row ids;
+ * a failed write leaves every shard unchanged; folds above honour the live mask of every shard) */
+int dds_mcol_write_rows(dds_mcol* col, const uint64_t* row_ids, size_t n, const uint8_t* operands_be, size_t width);
+int dds_mcol_write_rows_dec(dds_mcol* col, const uint64_t* row_ids, size_t n, const char* chars,
+                            const uint64_t* offsets);
+int dds_mcol_set_live(dds_mcol* col, const uint64_t* row_ids, size_t n, const uint8_t* live);
+size_t dds_mcol_live_count(dds_mcol* col);
 /* Synthetic Paillier rows for benchmarks/tests (config 2 of BASELINE.json):
  * c_i = g^m_i * r_a^n * r_b^n mod n^2 with m_i, a, b from splitmix64(seed, row0+i);
  * m_i = splitmix64(seed ^ splitmix64(row0+i)) % 10000 (DDSDataGenerator.scala:274).
@@ -227,7 +253,7 @@ int dds_ope_filter_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_v
  *   dds_opecol_search: the bound (item.value.toString) is parsed only when some row passes the guard
  *     (:702-704): no class-2 row -> 0 matches, any bound; a malformed bound or class-2 element -> 
  *     DDS_E_FORMAT (500). out_idx (capacity dds_opecol_count) receives ascending row ids.
- *   dds_opecol_order: a permutation of all rows, as dds_ope_order with valid = cls != 0; with two or
+ *   dds_opecol_order: a permutation of the rows, as dds_ope_order with valid = cls != 0; with two or
  *     more holders every holder is parsed by the comparator: a holder that is not a Long String ->
  *     DDS_E_FORMAT; a lone holder is never parsed. */
 typedef struct dds_opecol dds_opecol;
@@ -241,7 +267,25 @@ int dds_opecol_append(dds_opecol* col, const int64_t* values, const uint8_t* cls
 int dds_opecol_append_dec(dds_opecol* col, const char* const* values, const uint8_t* cls, const uint8_t* is_string,
                           size_t count);
 int dds_opecol_search(dds_opecol* col, const char* bound_dec, int op, uint32_t* out_idx, size_t* out_n);
-int dds_opecol_order(dds_opecol* col, int descending, uint32_t* out_idx);
+/* The same Search answered as a row bitmask: bit (r % 64) of mask[r / 64] = row r matches (mask_words
+ * >= ceil(dds_opecol_count / 64); bits past the last row are 0), *out_n = matches. 1/32 of the bytes of
+ * the id list at 50 % selectivity: the form a route holding its keys in row order iterates. */
+int dds_opecol_search_mask(dds_opecol* col, const char* bound_dec, int op, uint64_t* mask, size_t mask_words,
+                           size_t* out_n);
+/* out_idx (capacity dds_opecol_count) receives the permutation of the live rows, *out_n (nullable) its
+ * length = dds_opecol_live_count. */
+int dds_opecol_order(dds_opecol* col, int descending, uint32_t* out_idx, size_t* out_n);
+/* Rows follow the write routes, as dds_col_write_rows / dds_col_set_live: rows row_ids[0..n) take a new
+ * element and class (WriteElement :281-321, AddElement :220-255: the class moves when the set grows),
+ * as Longs or as the element text (same parsing as dds_opecol_append[_dec]); live[i] == 0 marks the
+ * row's set removed (RemoveSet :207-218): no Search matches it and Order leaves it out (filter(nonEmpty),
+ * :553/:586/:700); != 0 restores it. Repeated ids: the last entry wins. */
+int dds_opecol_write_rows(dds_opecol* col, const uint64_t* row_ids, const int64_t* values, const uint8_t* cls,
+                          size_t n);
+int dds_opecol_write_rows_dec(dds_opecol* col, const uint64_t* row_ids, const char* const* values,
+                              const uint8_t* cls, const uint8_t* is_string, size_t n);
+int dds_opecol_set_live(dds_opecol* col, const uint64_t* row_ids, size_t n, const uint8_t* live);
+size_t dds_opecol_live_count(dds_opecol* col);
 
 /* ---- OPE ordering (OrderLS / OrderSL, DDSRestServer.scala:541-606) ------------
  * out_idx receives a permutation of [0, n): rows with valid[i] != 0 (the row holds the

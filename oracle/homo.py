@@ -155,8 +155,10 @@ def rsa_modulus_from_pubkey_hex(pubkey: str) -> int:
     """``KeyFactory.getInstance("RSA").generatePublic(new X509EncodedKeySpec(
     DatatypeConverter.parseHexBinary(pubkey)))`` (``DDSRestServer.scala:476-478,515-517``) → its
     modulus. parseHexBinary needs an even number of hex digits; the DER must be an X.509
-    SubjectPublicKeyInfo of rsaEncryption; the JDK's RSA key factory refuses moduli outside
-    [512, 16384] bits (``RSAKeyFactory.checkRSAProviderKeyLengths``). Failures → 500."""
+    SubjectPublicKeyInfo of rsaEncryption; the JDK's RSA key factory (``RSAKeyFactory.
+    checkRSAProviderKeyLengths``, JDK 8 source; unpinned against a running JVM) rounds the modulus
+    length up to a multiple of 8 and refuses it outside [512, 16384] bits, and refuses exponents wider
+    than 64 bits for moduli above 3072 bits. Failures → 500."""
     h = str(pubkey)
     if len(h) % 2 or any(c not in "0123456789abcdefABCDEF" for c in h):
         raise ServerError("IllegalArgumentException: parseHexBinary")
@@ -191,8 +193,12 @@ def rsa_modulus_from_pubkey_hex(pubkey: str) -> int:
     if tag != 0x02 or tag2 != 0x02 or j != len(key):
         raise ServerError("InvalidKeySpecException: bad RSAPublicKey")
     n = int.from_bytes(nb, "big", signed=True)
-    if not 512 <= n.bit_length() <= 16384 or n <= 0:
+    e = int.from_bytes(eb, "big", signed=True)
+    mlen = (n.bit_length() + 7) // 8 * 8
+    if n <= 0 or not 512 <= mlen <= 16384:
         raise ServerError("InvalidKeyException: RSA modulus length")
+    if mlen > 3072 and e.bit_length() > 64:
+        raise ServerError("InvalidKeyException: RSA exponent length")
     return n
 
 
@@ -371,6 +377,99 @@ def is_element(row, value) -> bool:
     if row is None:
         raise NotFound()
     return any(homo_det_compare(e, value) for e in row)
+
+
+# ---------------------------------------------------------------------------
+# The store the routes read: storedKeys + the replicated registers (write routes)
+# ---------------------------------------------------------------------------
+
+
+def element_to_string(v) -> str:
+    """``toString`` of a contents element as ``AnyJsonFormat`` reads it (``DDSJsonProtocol.scala:22-28``):
+    String as is, Int in decimal, Boolean ``true``/``false``, JsNull -> ``None``."""
+    if v is None:
+        return "None"
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    return str(v)
+
+
+def set_to_string(contents) -> str:
+    """``DDSSet(contents: List[Any]).toString`` (case class around a List, ``DDSSet.scala:3``)."""
+    return "DDSSet(List(" + ", ".join(element_to_string(v) for v in contents) + "))"
+
+
+def key_from_set(contents) -> str:
+    """``Utils.getKeyFromSet(set, "SHA-512")`` (``Utils.scala:15-18``, digest from
+    ``dds-system.conf:99``): upper-case hex of SHA-512 over ``set.toString.getBytes`` (UTF-8)."""
+    import hashlib
+    return hashlib.sha512(set_to_string(contents).encode("utf-8")).hexdigest().upper()
+
+
+class Store:
+    """The proxy's ``storedKeys`` (``DDSRestServer.scala:70``) and the value of each key's replicated
+    register, as the write routes leave them (the BFT-ABD write/read pair is assumed to succeed: it
+    returns the last value written, ``BFTABDNode.scala:103-363``). ``keyed_rows()`` is what the read
+    routes fetch (``storedKeys.map(fetchSet)``, ``:401-403``). Key order = insertion order (the
+    reference iterates an immutable HashSet: its order is unpinned; it matters only for Order's ties)."""
+
+    def __init__(self):
+        self.keys = []
+        self.val = {}
+
+    def _store(self, key):
+        if key not in self.val:
+            self.keys.append(key)
+
+    def put_set(self, contents) -> str:
+        """``POST /PutSet`` with a body (``:170-188``): key = SHA-512 of the set's text; the register is
+        (re)written, ``storedKeys += key``."""
+        key = key_from_set(contents)
+        self._store(key)
+        self.val[key] = list(contents)
+        return key
+
+    def put_empty(self, key: str) -> str:
+        """``POST /PutSet`` without a body (``:190-205``): a random key holding None (the key is the
+        caller's here, the reference draws it from SecureRandom)."""
+        self._store(key)
+        self.val[key] = None
+        return key
+
+    def remove_set(self, key: str):
+        """``DELETE /RemoveSet/{key}`` (``:207-218``): writes None; the key stays in storedKeys, and every
+        read route drops it (``filter(nonEmpty)``). 200 for any key."""
+        if key in self.val:
+            self.val[key] = None
+
+    def add_element(self, key: str, value):
+        """``PUT /AddElement/{key}`` (``:220-255``): append the item; 404 when the set is None."""
+        cur = self.val.get(key)
+        if cur is None:
+            raise NotFound()
+        self.val[key] = cur + [value]
+
+    def write_element(self, key: str, position: int, value):
+        """``PUT /WriteElement/{key}?position`` (``:281-321``): replace ``contents(position)``, or append
+        when ``position > size-1``; 404 when the set is None. A negative position throws
+        IndexOutOfBoundsException inside the callback (500) and writes nothing."""
+        cur = self.val.get(key)
+        if cur is None:
+            raise NotFound()
+        if position > len(cur) - 1:
+            self.val[key] = cur + [value]
+        elif position < 0:
+            raise ServerError("IndexOutOfBoundsException")
+        else:
+            nxt = list(cur)
+            nxt[position] = value
+            self.val[key] = nxt
+
+    def rows(self):
+        return [self.val[k] for k in self.keys]
+
+    def keyed_rows(self):
+        return [(k, self.val[k]) for k in self.keys]
 
 
 # ---------------------------------------------------------------------------

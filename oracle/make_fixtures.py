@@ -2,6 +2,7 @@
 """Generate the committed golden fixtures under tests/golden/ (TEST INFRASTRUCTURE ONLY).
 
     python oracle/make_fixtures.py            # needs /root/reference for keys.json
+    python oracle/make_fixtures.py mutations  # only tests/golden/mutations.json (from keys.json)
 
 * keys.json    — key material decoded from the reference's committed client.conf
                  (src/main/resources/client.conf:81-88) + seeded synthetic keys for
@@ -9,6 +10,9 @@
 * vectors.json — known-answer vectors produced by oracle/homo.py (Python ints):
                  encryptions with fixed (m, r), fold products, decryptions, pairwise
                  products, route-level SumAll/MultAll/Search cases incl. edge cases.
+* mutations.json — write-route sequences (PutSet / AddElement / WriteElement / RemoveSet,
+                 DDSRestServer.scala:170-321) replayed on oracle.homo.Store, with the read routes'
+                 replies (SumAll, MultAll, Search*, Order*) after every step.
 
 There are no reference-produced vectors to copy (the reference has no tests and its
 hlib jar is absent); see oracle/homo.py for how these are pinned.
@@ -214,6 +218,131 @@ def route_edge_vectors(pk, rsa):
     return cases
 
 
+MUT_SUM_POS, MUT_MULT_POS, MUT_OPE_POS = 2, 3, 0  # client.conf:55,60 schema [OPE, CHE, PSSE, MSE, ...]
+
+
+def _reads(st: homo.Store, nsq: int, pubkey: str, bound: str):
+    """The read routes after a step: replies or {"status": 404 | 500}; key lists as insertion indices."""
+    idx = {k: i for i, k in enumerate(st.keys)}
+    keyed = st.keyed_rows()
+    rows = st.rows()
+
+    def keys_of(v, as_set):  # a status dict, or the keys as insertion indices (Search: a set, ascending)
+        if isinstance(v, dict):
+            return v
+        ids = [idx[k] for k in v]
+        return sorted(ids) if as_set else ids
+
+    out = {
+        "SumAll": _outcome(homo.sum_all, rows, MUT_SUM_POS, str(nsq)),
+        "MultAll": _outcome(homo.mult_all, rows, MUT_MULT_POS, pubkey=pubkey),
+        "SumAllPlain": _outcome(homo.sum_all, rows, MUT_SUM_POS, None),
+    }
+    for route in ("SearchGt", "SearchLtEq"):
+        out[route] = keys_of(_outcome(homo.search, route, keyed, MUT_OPE_POS, bound), True)
+    for route in ("OrderLS", "OrderSL"):
+        out[route] = keys_of(_outcome(homo.order, route, keyed, MUT_OPE_POS), False)
+    return out
+
+
+def mutation_vectors(pk, rsa, seed=2026, n_random=240):
+    """Write-route sequences on homo.Store (VERDICT r02 "next" 1): a scripted sequence covering each
+    route's edge (append past the end, 404 on a removed set, revival by PutSet, dedup of equal sets,
+    the strict guard crossed by AddElement, a malformed element, k = 1 unreduced, negative position),
+    then a seeded random sequence; the read routes' replies after every step."""
+    rng = random.Random(seed)
+    nsq, n, xh = pk["nsquare"], rsa["n"], rsa["x509_hex"]
+    pc = [str(homo.paillier_encrypt(rng.randrange(10000), rng.randrange(1, pk["n"]), pk)) for _ in range(12)]
+    rc = [str(homo.rsa_encrypt(rng.randrange(1, 10000), rsa)) for _ in range(12)]
+    ope = [str(v) for v in (-5, 0, 7, 7, 12, 2 ** 40, -2 ** 62, 99, 12, 3)]
+
+    def full(i):
+        return [ope[i % len(ope)], "che%d" % i, pc[i % len(pc)], rc[i % len(rc)], "x", "y"]
+
+    st = homo.Store()
+    steps = []
+
+    def step(op, **kw):
+        status = 200
+        try:
+            if op == "put":
+                kw["key"] = st.put_set(kw["set"])
+            elif op == "put_empty":
+                st.put_empty(kw["key"])
+            elif op == "remove":
+                st.remove_set(kw["key"])
+            elif op == "add":
+                st.add_element(kw["key"], kw["value"])
+            elif op == "write":
+                st.write_element(kw["key"], kw["position"], kw["value"])
+        except homo.NotFound:
+            status = 404
+        except homo.ServerError:
+            status = 500
+        steps.append({"op": op, **kw, "status": status, "reads": _reads(st, nsq, xh, ope[2])})
+        return kw.get("key")
+
+    a = step("put", set=full(0))
+    b = step("put", set=full(1))
+    c = step("put", set=full(2))
+    d = step("put", set=full(3)[:3])             # PSSE is its last element: the strict guard skips it
+    e = step("put", set=[ope[4]])                # OPE only: Order holder, Search skips it (last element)
+    step("put_empty", key="E" * 128)             # PutSet without a body
+    step("write", key=a, position=2, value=pc[5])
+    step("add", key=d, value="tail")             # D crosses the guard: folds now
+    step("remove", key=b)
+    step("add", key=b, value="x")                # 404: removed
+    step("put", set=full(1))                     # same contents -> same key: B revived
+    f = step("put", set=full(0)[:2] + [pc[5]] + full(0)[3:])  # equal to A's current contents: dedup
+    step("write", key=f, position=5, value="zz")  # F differs again
+    step("write", key=c, position=0, value="x7")  # malformed OPE element: Search 500, Order 500
+    step("write", key=c, position=0, value=ope[9])
+    step("write", key=c, position=2, value="12ab")  # malformed PSSE element: SumAll 500
+    step("write", key=c, position=2, value=pc[7])
+    step("write", key=e, position=7, value=ope[3])  # past the end: appended at index 1
+    step("add", key="E" * 128, value="1")        # None set: 404
+    step("write", key="F" * 128, position=0, value="1")  # unknown key: 404
+    step("write", key=a, position=-1, value="1")  # IndexOutOfBounds: 500, nothing written
+    step("write", key=a, position=3, value=str(n + 17))  # RSA operand above n (reduced by the fold)
+    for k in (b, c, d, f):
+        step("remove", key=k)
+    step("write", key=a, position=2, value=str(nsq + 5))  # one live operand >= nsq: returned unreduced
+    step("remove", key=a)                        # nothing left: 404 / empty key lists
+    step("put", set=full(0))                     # A's original contents: its key again
+    # seeded random walk over ~40 keys
+    keys = [k for k in st.keys]
+    for _ in range(n_random):
+        u = rng.random()
+        live = [k for k in keys if st.val.get(k) is not None]
+        if u < 0.25 or not live:
+            i = rng.randrange(40)
+            length = rng.choice([1, 2, 3, 4, 5, 6, 6, 6])
+            row = full(i)[:length]
+            if rng.random() < 0.3:
+                row = list(st.val[rng.choice(live)]) if live else row  # equal contents (dedup / same key)
+            k = step("put", set=row)
+            if k not in keys:
+                keys.append(k)
+        elif u < 0.45:
+            k = rng.choice(keys)
+            at = len(st.val[k]) if st.val.get(k) is not None else 1  # the appended element's position
+            step("add", key=k, value={0: ope[rng.randrange(10)], 2: pc[rng.randrange(12)],
+                                      3: rc[rng.randrange(12)]}.get(at, "w"))
+        elif u < 0.8:
+            pos = rng.choice([0, 0, 2, 2, 2, 3, 3, 1, 6])
+            k = rng.choice(keys)
+            cur = st.val.get(k)
+            at = pos if cur is None or pos < len(cur) else len(cur)  # past the end: appended
+            val = {0: ope[rng.randrange(10)], 2: pc[rng.randrange(12)], 3: rc[rng.randrange(12)]}.get(at, "v")
+            if rng.random() < 0.03:
+                val = "bad"
+            step("write", key=k, position=pos, value=val)
+        else:
+            step("remove", key=rng.choice(keys))
+    return {"positions": {"sum": MUT_SUM_POS, "mult": MUT_MULT_POS, "ope": MUT_OPE_POS},
+            "nsquare": str(nsq), "pubkey": xh, "n": str(n), "bound": ope[2], "steps": steps}
+
+
 def main():
     os.makedirs(GOLDEN, exist_ok=True)
     kpath = os.path.join(GOLDEN, "keys.json")
@@ -243,5 +372,16 @@ def main():
     print("wrote", kpath, os.path.join(GOLDEN, "vectors.json"))
 
 
+def main_mutations():
+    keys = json.load(open(os.path.join(GOLDEN, "keys.json")))
+    vec = mutation_vectors(load_key(keys, "paillier2048_committed"), load_key(keys, "rsa1024_committed"))
+    path = os.path.join(GOLDEN, "mutations.json")
+    json.dump(vec, open(path, "w"), separators=(",", ":"))
+    print("wrote", path, len(vec["steps"]), "steps")
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["mutations"]:
+        main_mutations()
+    else:
+        main()

@@ -299,3 +299,97 @@ def test_x509_product_decoder_matches_oracle(keys):
             x509.rsa_modulus(junk)
         with pytest.raises(homo.ServerError):
             homo.rsa_modulus_from_pubkey_hex(junk)
+
+
+def test_store_write_routes():
+    """oracle Store: the write routes' effects (DDSRestServer.scala:170-321) on what the read routes see."""
+    st = homo.Store()
+    a = st.put_set(["1", "x", "7", "z"])
+    assert a == homo.key_from_set(["1", "x", "7", "z"]) and len(a) == 128 and a == a.upper()
+    b = st.put_set(["2", "y", "7"])                          # PSSE is its last element: skipped by SumAll
+    assert homo.sum_all(st.rows(), 2, "1000") == "7"
+    st.add_element(b, "t")                                   # crosses the strict guard
+    assert homo.sum_all(st.rows(), 2, "1000") == "49"
+    st.write_element(b, 9, "u")                              # past the end: appended
+    assert st.val[b] == ["2", "y", "7", "t", "u"]
+    st.remove_set(a)
+    assert homo.sum_all(st.rows(), 2, "1000") == "7"
+    with pytest.raises(homo.NotFound):
+        st.add_element(a, "q")                               # removed: 404
+    with pytest.raises(homo.NotFound):
+        st.write_element("nope", 0, "q")                     # unknown key: 404
+    with pytest.raises(homo.ServerError):
+        st.write_element(b, -1, "q")                         # IndexOutOfBounds: 500, unchanged
+    assert st.val[b] == ["2", "y", "7", "t", "u"]
+    assert st.put_set(["1", "x", "7", "z"]) == a             # same contents, same key: revived
+    c = st.put_set(list(st.val[b]))                          # equal to b's current contents: collapses
+    assert c != b and homo.sum_all(st.rows(), 2, "1000") == "49"
+    st.put_empty("K" * 128)
+    assert st.val["K" * 128] is None and "K" * 128 in st.keys
+    assert homo.set_to_string(["a", 5, True, None]) == "DDSSet(List(a, 5, true, None))"
+
+
+def test_mutation_vectors_recompute():
+    """tests/golden/mutations.json is what the oracle Store answers (guards fixture / oracle drift)."""
+    import json
+    from oracle import make_fixtures as mf
+    fx = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mutations.json")))
+    nsq = int(fx["nsquare"])
+    st = homo.Store()
+    for i, step in enumerate(fx["steps"]):
+        try:
+            if step["op"] == "put":
+                assert st.put_set(step["set"]) == step["key"]
+            elif step["op"] == "put_empty":
+                st.put_empty(step["key"])
+            elif step["op"] == "remove":
+                st.remove_set(step["key"])
+            elif step["op"] == "add":
+                st.add_element(step["key"], step["value"])
+            else:
+                st.write_element(step["key"], step["position"], step["value"])
+            status = 200
+        except homo.NotFound:
+            status = 404
+        except homo.ServerError:
+            status = 500
+        assert status == step["status"], i
+        assert mf._reads(st, nsq, fx["pubkey"], fx["bound"]) == step["reads"], i
+
+
+def test_store_key_derivation_product_matches_oracle():
+    from ddshe.store import key_from_set
+    for s in (["1"], [], ["a", 5, True, None], ["٤", "x" * 300]):
+        assert key_from_set(s) == homo.key_from_set(s)
+
+
+def _spki(n: int, e: int) -> str:
+    def der(tag, body):
+        ln = len(body)
+        enc = bytes([ln]) if ln < 0x80 else bytes([0x80 | ((ln.bit_length() + 7) // 8)]) + ln.to_bytes(
+            (ln.bit_length() + 7) // 8, "big")
+        return bytes([tag]) + enc + body
+
+    def integer(x):
+        return der(0x02, x.to_bytes(x.bit_length() // 8 + 1, "big"))
+    alg = der(0x30, der(0x06, bytes.fromhex("2a864886f70d010101")) + der(0x05, b""))
+    key = der(0x30, integer(n) + integer(e))
+    return der(0x30, alg + der(0x03, b"\0" + key)).hex()
+
+
+def test_x509_jdk_key_length_check():
+    """RSAKeyFactory.checkRSAProviderKeyLengths: length rounded up to a multiple of 8 (505..511-bit
+    moduli pass), at most 16384, exponent <= 64 bits above 3072 bits; product and oracle agree."""
+    from ddshe import x509
+    cases = [((1 << 504) + 1, 65537, True), ((1 << 503) + 1, 65537, False), ((1 << 4095) + 1, (1 << 64) + 1, False),
+             ((1 << 4095) + 1, (1 << 63) + 1, True), ((1 << 3071) + 1, (1 << 100) + 1, True),
+             ((1 << 16383) + 1, 3, True), ((1 << 16384) + 1, 3, False)]
+    for n, e, ok in cases:
+        h = _spki(n, e)
+        if ok:
+            assert x509.rsa_modulus(h) == homo.rsa_modulus_from_pubkey_hex(h) == n
+        else:
+            with pytest.raises(ValueError):
+                x509.rsa_modulus(h)
+            with pytest.raises(homo.ServerError):
+                homo.rsa_modulus_from_pubkey_hex(h)
