@@ -423,6 +423,7 @@ class SumWorkload(_Workload):
         a, b = (str(x) for x in (self.col_sample[0], self.col_sample[1]))
         pair, pair_ms, pair_p99 = med(lambda: eng.pair_modmul_dec(a, b, str(k2["nsquare"])), 200)
         conc = self.concurrent_pairs(k2["nsquare"], threads=64, per_thread=32)
+        native = self.native_pairs(k2["nsquare"], threads=64, per_thread=200)
         rng = np.random.default_rng(5)
         n_pairs = 65536
         xa = [self.col_sample[i % len(self.col_sample)] for i in range(n_pairs)]
@@ -460,6 +461,7 @@ class SumWorkload(_Workload):
                                            "path": "dds_pair_modmul_dec, one caller (the /Sum route body)",
                                            "matches": pair == str(int(a) * int(b) % k2["nsquare"])},
                 "pair_sum_route_concurrent_2048bit": conc,
+                "pair_sum_route_native_threads_2048bit": native,
                 "pairs_batched_2048bit": {"pairs": n_pairs, "pairs_per_s": pairs_c_s,
                                           "path": "dds_modmul_pairs (k_pairs + k_egress_be), big-endian host buffers in and out",
                                           "pairs_per_s_with_python_int_marshalling": pairs_s,
@@ -504,6 +506,24 @@ class SumWorkload(_Workload):
                 "calls_per_launch": (c1 - c0) / max(1, l1 - l0),
                 "path": "dds_pair_modmul_dec from concurrent threads: one k_pairs launch per burst",
                 "matches": not bad}
+
+    def native_pairs(self, m, threads, per_thread):
+        """The same /Sum load from native threads (tools/native/pair_bench: C++ std::threads calling
+        dds_pair_modmul_dec, no interpreter lock), as the JVM's ForkJoin pool would (DDSRestServer.scala:21).
+        Runs as a child process on the same GPU; its samples are checked here with Python ints."""
+        exe = os.path.join(ROOT, "tools", "native", "pair_bench")
+        if not os.path.exists(exe):
+            return {"skipped": "tools/native/pair_bench not built"}
+        import subprocess
+        pr = subprocess.run([exe, str(m), str(threads), str(per_thread)], capture_output=True, text=True, timeout=300)
+        if pr.returncode != 0:
+            return {"error": pr.stderr[-400:]}
+        res = json.loads(pr.stdout.strip().splitlines()[-1])
+        samples = res.pop("samples")
+        res["matches"] = bool(samples) and all(int(r) == int(a) * int(b) % m for a, b, r in samples)
+        res["checked_samples"] = len(samples)
+        res["path"] = "tools/native/pair_bench: %d C++ threads x %d dds_pair_modmul_dec calls" % (threads, per_thread)
+        return res
 
     def end_to_end(self, res):
         """Host-boundary rates, outside the timed region (never `value`): (1) the binary boundary

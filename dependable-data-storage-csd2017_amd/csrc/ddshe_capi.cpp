@@ -61,6 +61,7 @@ int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_p
     std::lock_guard<std::mutex> lk(ctx->mu);
     auto it = ctx->mods.find(key);
     if (it != ctx->mods.end()) {
+      it->second->last_use = ++ctx->mod_tick;
       *out = it->second;
       return DDS_OK;
     }
@@ -155,9 +156,26 @@ int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_p
     *out = it->second;
     return DDS_OK;
   }
+  // bounded cache: the modulus comes with each request (nsqr / pubkey), so evict the least recently
+  // used constants past the cap; columns and calls in flight keep theirs alive (shared_ptr)
+  if (ctx->mods.size() >= max_cached_moduli()) {
+    auto lru = ctx->mods.begin();
+    for (auto i = ctx->mods.begin(); i != ctx->mods.end(); ++i)
+      if (i->second->last_use < lru->second->last_use) lru = i;
+    ctx->mods.erase(lru);
+  }
+  mc->last_use = ++ctx->mod_tick;
   ctx->mods.emplace(key, mc);
   *out = mc;
   return DDS_OK;
+}
+
+size_t max_cached_moduli() {
+  static const size_t n = [] {
+    const char* e = getenv("DDSHE_MAX_MODULI");
+    return e ? std::max<size_t>(1, (size_t)atoll(e)) : (size_t)64;
+  }();
+  return n;
 }
 
 void record_time(dds_ctx* ctx, Worker* w, hipStream_t st, bool begin, int slot) {

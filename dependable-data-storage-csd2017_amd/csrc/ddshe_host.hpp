@@ -113,6 +113,7 @@ struct Worker {
 struct ModConsts {
   int S = 0, TPI = 0, W = 0, S2 = 0;
   size_t bits = 0, bytes = 0;
+  uint64_t last_use = 0;         // ctx->mods LRU tick (under ctx->mu)
   uint32_t n0 = 0;
   bn::Limbs N, Rmod, half;       // half = (N+1)/2 = 2^-1 mod N
   bn::Limbs qbound;              // partials stay below 2*qbound: N~ = N·n0 when a QP shape is used, else N
@@ -139,7 +140,7 @@ struct ModConsts {
     if (dq) (void)hipFree(dq);
     if (dqm) (void)hipFree(dqm);
     if (d3) (void)hipFree(d3);
-    for (auto& kv : y3dev) (void)hipFree(kv.second);
+    if (y3slab) (void)hipFree(y3slab);
     if (dtab) (void)hipFree(dtab);
   }
   std::vector<uint32_t> rw(const bn::Limbs& v) const { return bn::to_rw(v, S, W); }
@@ -169,28 +170,27 @@ struct ModConsts {
     return y3cache.emplace(E, bn::to_rw(y, S3, W3)).first->second;
   }
   // device copy of y3_for(E), made on first use and kept until the constants go (a fold's finalize
-  // then needs no H2D copy on its critical path); nullptr once kYDev exponents are cached
+  // then needs no H2D copy on its critical path): slots of one device block of kYDev * S3 words;
+  // nullptr once every slot is taken (the caller then copies Y in its stream)
   static constexpr size_t kYDev = 256;
+  uint32_t* y3slab = nullptr;
   std::map<int64_t, uint32_t*> y3dev;
   const uint32_t* y3_device(int64_t E) {
-    {
-      std::lock_guard<std::mutex> lk(ymu);
-      auto it = y3dev.find(E);
-      if (it != y3dev.end()) return it->second;
-      if (y3dev.size() >= kYDev) return nullptr;
-    }
     const std::vector<uint32_t> y = y3_for(E);
-    uint32_t* d = nullptr;
-    if (hipMalloc(&d, y.size() * 4) != hipSuccess) return nullptr;
-    if (hipMemcpy(d, y.data(), y.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
-      (void)hipFree(d);
+    std::lock_guard<std::mutex> lk(ydmu);  // held over the copy: a slot is visible only once filled
+    auto it = y3dev.find(E);
+    if (it != y3dev.end()) return it->second;
+    if (y3dev.size() >= kYDev) return nullptr;
+    if (!y3slab && hipMalloc(&y3slab, kYDev * (size_t)S3 * 4) != hipSuccess) {
+      y3slab = nullptr;
       return nullptr;
     }
-    std::lock_guard<std::mutex> lk(ymu);
-    auto ins = y3dev.emplace(E, d);
-    if (!ins.second) (void)hipFree(d);  // a concurrent caller made it first
-    return ins.first->second;
+    uint32_t* d = y3slab + y3dev.size() * (size_t)S3;
+    if (hipMemcpy(d, y.data(), y.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    y3dev.emplace(E, d);
+    return d;
   }
+  std::mutex ydmu;
   int64_t wS3() const { return (int64_t)W3 * S3; }
   // bits of 2 contributed by one Montgomery product of the main / tail shape
   int64_t wS() const { return (int64_t)W * S; }
@@ -217,6 +217,7 @@ struct dds_ctx {
   // (modulus, limb count of its shape) -> constants; the shape is normally the narrowest that holds
   // the modulus, a wider one when operands must fit (the odd part of an even modulus)
   std::map<std::pair<ddshe::bn::Limbs, int>, std::shared_ptr<ddshe::host::ModConsts>> mods;
+  uint64_t mod_tick = 0;  // LRU clock of mods (under mu)
   std::map<std::pair<ddshe::bn::Limbs, ddshe::bn::Limbs>, std::shared_ptr<CrtKey>> crt_keys;
   hipStream_t ext_stream = nullptr;
   std::atomic<bool> timing{false};
@@ -447,6 +448,8 @@ constexpr size_t kDecChunkRows = (size_t)1 << 18;
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // rows of one rW matrix of this modulus' shape must stay addressable by the kernels (max_stride)
 int check_rows(const ModConsts& mc, size_t rows);
+// cap on the per-context modulus-constant cache (DDSHE_MAX_MODULI, default 64; LRU eviction)
+size_t max_cached_moduli();
 // constants of an odd modulus > 1 in the shape for max(bits(N), min_bits)
 int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_ptr<ModConsts>* out,
             size_t min_bits = 0);

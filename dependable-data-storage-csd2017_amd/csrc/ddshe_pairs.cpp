@@ -5,7 +5,11 @@
 // one Montgomery product; the proxy runs routes concurrently on its pool (DDSRestServer.scala:21), so
 // concurrent requests under one modulus share a queue and the first caller to find it idle runs ONE
 // k_pairs launch over every pair queued so far (the others sleep on the queue's condition variable
-// and wake with their result). A lone request pays no batching wait.
+// and wake with their result). A lone request pays no batching wait. A burst of up to kTailPairs
+// pairs runs in the latency shape straight from the parsed limbs (one pinned H2D, one k_pairs launch,
+// one D2H, one synchronisation); larger ones take the batched dds_modmul_pairs path. A queue lives
+// while it has work: the last caller out of an idle queue drops it, so moduli sent once by clients
+// leave nothing behind.
 #include <string.h>
 
 #include <condition_variable>
@@ -21,9 +25,54 @@ using namespace ddshe::host;
 
 namespace {
 
+constexpr size_t kTailPairs = 256;
+
+// the batch in the tail (latency) shape from limbs already < M
+int tail_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& batch) {
+  const size_t mb = bn::byte_length(M), n = batch.size();
+  std::vector<uint8_t> mbe(mb);
+  bn::to_be(M, mbe.data(), mb);
+  std::shared_ptr<ModConsts> mcp;
+  int rc = get_mod(ctx, mbe.data(), mb, &mcp);
+  if (rc) return rc;
+  ModConsts& mc = *mcp;
+  WorkerLease wl(ctx);
+  if ((rc = wl.acquire())) return rc;
+  Worker* w = wl.w;
+  const int S2 = mc.S2;
+  const size_t words = (size_t)S2 * n;
+  HIP_TRY(w->hch[1].ensure(3 * words * 4));
+  HIP_TRY(w->x2.ensure(3 * words * 4));
+  uint32_t* h = (uint32_t*)w->hch[1].p;
+  for (size_t i = 0; i < n; ++i) {
+    const std::vector<uint32_t> ra = bn::to_rw(batch[i]->a, S2, mc.W), rb = bn::to_rw(batch[i]->b, S2, mc.W);
+    for (int l = 0; l < S2; ++l) {
+      h[(size_t)l * n + i] = ra[l];
+      h[words + (size_t)l * n + i] = rb[l];
+    }
+  }
+  uint32_t* d = w->x2.as<uint32_t>();
+  HIP_TRY(hipMemcpyAsync(d, h, 2 * words * 4, hipMemcpyHostToDevice, wl.st));
+  HIP_TRY(launch_pairs_tail(S2, d, d + words, n, n, mc.d2, mc.n0, d + 2 * words, wl.st));
+  HIP_TRY(hipMemcpyAsync(h + 2 * words, d + 2 * words, words * 4, hipMemcpyDeviceToHost, wl.st));
+  HIP_TRY(hipStreamSynchronize(wl.st));
+  std::vector<uint32_t> limbs(S2);
+  for (size_t i = 0; i < n; ++i) {
+    for (int l = 0; l < S2; ++l) limbs[l] = h[2 * words + (size_t)l * n + i];
+    batch[i]->r = mc.value2(limbs.data());
+  }
+  return DDS_OK;
+}
+
 // one k_pairs launch for the batch: results into each request (rc on failure)
 void run_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& batch) {
   const size_t mb = bn::byte_length(M), n = batch.size();
+  if (n <= kTailPairs) {
+    const int rc = tail_batch(ctx, M, batch);
+    ctx->pair_launches.fetch_add(1);
+    for (PairReq* r : batch) r->rc = rc;
+    return;
+  }
   std::vector<uint8_t> mbe(mb), A(n * mb), B(n * mb), O(n * mb);
   bn::to_be(M, mbe.data(), mb);
   for (size_t i = 0; i < n; ++i) {
@@ -67,6 +116,16 @@ int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req) {
     for (PairReq* r : batch) r->done = true;
     q->busy = false;
     q->cv.notify_all();  // finished requests return; a queued one becomes the next leader
+  }
+  const bool idle = !q->busy && q->pending.empty();
+  lk.unlock();
+  if (idle) {  // drop the idle queue (a caller that still holds it just runs as its own leader)
+    std::lock_guard<std::mutex> g(ctx->pmu);
+    auto it = ctx->pair_queues.find(M);
+    if (it != ctx->pair_queues.end() && it->second == q) {
+      std::lock_guard<std::mutex> ql(q->mu);
+      if (!q->busy && q->pending.empty()) ctx->pair_queues.erase(it);
+    }
   }
   return req->rc;
 }
@@ -116,6 +175,19 @@ int dds_pair_stats(dds_ctx* ctx, uint64_t* calls, uint64_t* launches) {
   if (!ctx) return fail(DDS_E_ARG, "bad arguments");
   if (calls) *calls = ctx->pair_calls.load();
   if (launches) *launches = ctx->pair_launches.load();
+  return DDS_OK;
+}
+
+int dds_ctx_cache_stats(dds_ctx* ctx, size_t* moduli, size_t* pair_queues) {
+  if (!ctx) return fail(DDS_E_ARG, "bad arguments");
+  if (moduli) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    *moduli = ctx->mods.size();
+  }
+  if (pair_queues) {
+    std::lock_guard<std::mutex> lk(ctx->pmu);
+    *pair_queues = ctx->pair_queues.size();
+  }
   return DDS_OK;
 }
 

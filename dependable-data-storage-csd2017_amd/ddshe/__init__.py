@@ -58,7 +58,7 @@ EXPORTS = [
     "dds_col_write_rows", "dds_col_write_rows_dec", "dds_col_set_live", "dds_col_live_count",
     "dds_mcol_write_rows", "dds_mcol_write_rows_dec", "dds_mcol_set_live", "dds_mcol_live_count",
     "dds_opecol_write_rows", "dds_opecol_write_rows_dec", "dds_opecol_set_live", "dds_opecol_live_count",
-    "dds_opecol_search_mask",
+    "dds_opecol_search_mask", "dds_ctx_cache_stats",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -126,6 +126,7 @@ for _n in ("dds_sum_all_dec", "dds_mult_all_dec"):
 _u64p = C.POINTER(C.c_uint64)
 _sig("dds_pair_modmul_dec", C.c_int, C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, _sz, _szp)
 _sig("dds_pair_stats", C.c_int, C.c_void_p, _u64p, _u64p)
+_sig("dds_ctx_cache_stats", C.c_int, C.c_void_p, _szp, _szp)
 _sig("dds_col_fold_rows", C.c_int, C.c_void_p, _u64p, _sz, _u8p, _sz, _szp)
 _sig("dds_col_fold_dec", C.c_int, C.c_void_p, _u64p, _sz, C.c_char_p, _sz, _szp)
 _sig("dds_col_fold_partial_device", C.c_int, C.c_void_p, _sz, _sz, C.c_void_p)
@@ -372,6 +373,12 @@ class Engine:
         calls, launches = C.c_uint64(), C.c_uint64()
         _check(_lib.dds_pair_stats(self._h, C.byref(calls), C.byref(launches)), "dds_pair_stats")
         return calls.value, launches.value
+
+    def cache_stats(self):
+        """(cached modulus constants, live pairwise queues) of this engine"""
+        m, q = C.c_size_t(), C.c_size_t()
+        _check(_lib.dds_ctx_cache_stats(self._h, C.byref(m), C.byref(q)), "dds_ctx_cache_stats")
+        return m.value, q.value
 
     # ---- OPE filter ----
     def ope_filter(self, col, valid, bound: int, op: str) -> np.ndarray:

@@ -105,6 +105,9 @@ int dds_pair_modmul_dec(dds_ctx* ctx, const char* op1_dec, const char* op2_dec, 
                         size_t out_cap, size_t* out_len);
 /* Counters of dds_pair_modmul_dec on this context: calls, and k_pairs launches that served them. */
 int dds_pair_stats(dds_ctx* ctx, uint64_t* calls, uint64_t* launches);
+/* Sizes of the per-request caches: modulus constants (LRU, at most DDSHE_MAX_MODULI, default 64) and
+ * pairwise queues (one per modulus with calls in flight; dropped when idle). */
+int dds_ctx_cache_stats(dds_ctx* ctx, size_t* moduli, size_t* pair_queues);
 /* SumAll without nsqr (plain BigInteger add, DDSRestServer.scala:425): sum of count
  * operands; result big-endian in out (min(out_cap) = width + 8 is always enough). */
 int dds_bigint_sum(dds_ctx* ctx, const uint8_t* operands_be, size_t width, size_t count, uint8_t* out,

@@ -1,0 +1,109 @@
+// /Sum coalescing under native threads (VERDICT r02 "next" 5): T threads call dds_pair_modmul_dec
+// concurrently on one context, as the proxy's ForkJoin pool runs /Sum routes (DDSRestServer.scala:21,
+// 355-395), with no interpreter lock between them. Reports calls per k_pairs launch, pairs/s and the
+// per-call latency distribution as one JSON line, plus a few (a, b, result) samples for the caller to
+// check (bench.py verifies them with Python ints).
+//
+//   pair_bench <modulus_dec> <threads> <calls_per_thread> [seed]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+#include <algorithm>
+#include <atomic>
+
+#include "ddshe.h"
+
+int main(int argc, char** argv) {
+  if (argc < 4) {
+    fprintf(stderr, "usage: %s <modulus_dec> <threads> <calls_per_thread> [seed]\n", argv[0]);
+    return 2;
+  }
+  const std::string mod = argv[1];
+  const int T = atoi(argv[2]), K = atoi(argv[3]);
+  const unsigned seed = argc > 4 ? (unsigned)atoi(argv[4]) : 7u;
+  dds_ctx* ctx = nullptr;
+  if (dds_ctx_create(0, &ctx)) {
+    fprintf(stderr, "dds_ctx_create: %s\n", dds_last_error());
+    return 1;
+  }
+  // operands: random decimals one digit shorter than the modulus (so below it), per thread
+  std::vector<std::vector<std::string>> A(T), B(T), R(T);
+  std::mt19937_64 rng(seed);
+  auto rnd = [&](size_t digits) {
+    std::string s(digits, '0');
+    s[0] = (char)('1' + rng() % 9);
+    for (size_t i = 1; i < digits; ++i) s[i] = (char)('0' + rng() % 10);
+    return s;
+  };
+  for (int t = 0; t < T; ++t)
+    for (int i = 0; i < K + 1; ++i) {
+      A[t].push_back(rnd(mod.size() - 1));
+      B[t].push_back(rnd(mod.size() - 1));
+    }
+  const size_t cap = 2 * mod.size() + 64;
+  // warm-up (modulus constants, streams, pinned buffers), then a barrier and the timed phase
+  {
+    std::vector<char> out(cap);
+    size_t len = 0;
+    if (dds_pair_modmul_dec(ctx, A[0][K].c_str(), B[0][K].c_str(), mod.c_str(), out.data(), cap, &len)) {
+      fprintf(stderr, "warm-up: %s\n", dds_last_error());
+      return 1;
+    }
+  }
+  uint64_t c0 = 0, l0 = 0, c1 = 0, l1 = 0;
+  dds_pair_stats(ctx, &c0, &l0);
+  std::vector<std::vector<double>> lat(T);
+  std::atomic<int> ready{0}, errors{0};
+  std::atomic<bool> go{false};
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([&, t] {
+      std::vector<char> out(cap);
+      size_t len = 0;
+      ready.fetch_add(1);
+      while (!go.load()) std::this_thread::yield();
+      for (int i = 0; i < K; ++i) {
+        const auto s = std::chrono::steady_clock::now();
+        const int rc = dds_pair_modmul_dec(ctx, A[t][i].c_str(), B[t][i].c_str(), mod.c_str(), out.data(), cap, &len);
+        const auto e = std::chrono::steady_clock::now();
+        if (rc) {
+          errors.fetch_add(1);
+          continue;
+        }
+        lat[t].push_back(std::chrono::duration<double, std::milli>(e - s).count());
+        if (i < 2) R[t].push_back(std::string(out.data(), len));
+      }
+    });
+  while (ready.load() < T) std::this_thread::yield();
+  const auto t0 = std::chrono::steady_clock::now();
+  go.store(true);
+  for (auto& x : th) x.join();
+  const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  dds_pair_stats(ctx, &c1, &l1);
+  std::vector<double> all;
+  for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
+  std::sort(all.begin(), all.end());
+  auto pct = [&](double p) { return all.empty() ? 0.0 : all[std::min(all.size() - 1, (size_t)(p * all.size()))]; };
+  size_t moduli = 0, queues = 0;
+  dds_ctx_cache_stats(ctx, &moduli, &queues);
+  printf("{\"threads\": %d, \"calls\": %llu, \"launches\": %llu, \"calls_per_launch\": %.2f, \"pairs_per_s\": %.1f, "
+         "\"p50_ms\": %.4f, \"p99_ms\": %.4f, \"max_ms\": %.4f, \"errors\": %d, \"modulus_digits\": %zu, "
+         "\"cached_moduli\": %zu, \"pair_queues_after\": %zu, \"hw_threads\": %u, \"samples\": [",
+         T, (unsigned long long)(c1 - c0), (unsigned long long)(l1 - l0),
+         (l1 > l0) ? (double)(c1 - c0) / (double)(l1 - l0) : 0.0, (double)all.size() / secs, pct(0.5), pct(0.99),
+         all.empty() ? 0.0 : all.back(), errors.load(), mod.size(), moduli, queues, std::thread::hardware_concurrency());
+  bool first = true;
+  for (int t = 0; t < std::min(T, 4); ++t)
+    for (size_t i = 0; i < R[t].size(); ++i) {
+      printf("%s[\"%s\", \"%s\", \"%s\"]", first ? "" : ", ", A[t][i].c_str(), B[t][i].c_str(), R[t][i].c_str());
+      first = false;
+    }
+  printf("]}\n");
+  dds_ctx_destroy(ctx);
+  return errors.load() ? 1 : 0;
+}
