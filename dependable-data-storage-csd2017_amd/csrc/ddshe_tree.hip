@@ -30,6 +30,19 @@ namespace ddshe {
 
 constexpr int kTreeThreads = 1024;
 
+// Phase stamps (profiling aid, DDSHE_TREE_STAMPS=<file>; off: a null pointer and no cost): thread 0 of
+// the first and the last block of a launch records the shader clock (s_memtime) after every barrier
+// of its product(s) into LDS; wave 0 copies them out at the end (lane-divergent vector stores).
+constexpr int kStamps = 48;
+struct Stamps {
+  uint64_t* sh = nullptr;  // LDS slots; null when off
+  int k = 0;
+  __device__ __forceinline__ void mark() {
+    if (sh && threadIdx.x == 0 && k < kStamps - 2) sh[2 + k] = __builtin_amdgcn_s_memtime();
+    ++k;
+  }
+};
+
 template <int S, int W>
 struct Sos {
   static_assert(S % 2 == 0 && S >= 4, "even limb count");
@@ -109,21 +122,27 @@ struct Sos {
   // Ends with a barrier.
   template <int NT>
   __device__ static void monpro(uint32_t* a, const uint32_t* by, const uint32_t* ny, const uint32_t* npy, uint64_t* T,
-                                uint32_t* d, uint64_t* M) {
+                                uint32_t* d, uint64_t* M, Stamps& sp) {
     const int tid = threadIdx.x;
     for (int j = tid; j < 2 * S; j += NT) T[j] = 0;
     for (int j = tid; j < S; j += NT) M[j] = 0;
     __syncthreads();
+    sp.mark();
     conv<NT>(a, by, T, 2 * S);  // T = a*b
     __syncthreads();
+    sp.mark();
     for (int p = tid; p < S; p += NT) d[p] = split3(T, p);
     __syncthreads();
+    sp.mark();
     conv<NT>(d, npy, M, S);  // m = d * n' mod R (low columns)
     __syncthreads();
+    sp.mark();
     for (int p = tid; p < S; p += NT) d[p] = split3(M, p);  // d now holds m (< 3*2^W limbs)
     __syncthreads();
+    sp.mark();
     conv<NT>(d, ny, T, 2 * S);  // V = T + m*N
     __syncthreads();
+    sp.mark();
     if (tid == 0) {  // carry out of the low half (see the header): ceil(X / 2^3W), X < 2^(64+2W+1)
       const uint64_t v2 = T[S - 1], v1 = T[S - 2], v0 = T[S - 3];
       unsigned __int128 x = ((unsigned __int128)v2 << (2 * W)) + ((unsigned __int128)v1 << W) + v0;
@@ -135,6 +154,7 @@ struct Sos {
     __syncthreads();
     for (int j = tid; j < S; j += NT) a[j] = (d[j] & kMask) + (j >= 1 ? d[j - 1] >> W : 0u);
     __syncthreads();
+    sp.mark();
   }
 
   // carry-in bit of every limb for a generate/propagate pattern over S positions (wave 0, all lanes
@@ -231,7 +251,7 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
                                                        const uint32_t* __restrict__ Y, uint32_t* __restrict__ nodes,
                                                        uint32_t* __restrict__ flags, uint32_t* __restrict__ out, int Sout,
                                                        int Wout, int max_levels, uint32_t* __restrict__ lvl_out,
-                                                       int fence_mode) {
+                                                       int fence_mode, uint64_t* __restrict__ stamps) {
   using O = Sos<S, W>;
   constexpr int NT = kTreeThreads;
   // y operands (b, N, n') zero-padded around y[0] (Sos::conv); x operands (a, d) zero past S
@@ -239,6 +259,17 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
   __shared__ uint32_t stmp[S + 64], stmp2[S + 64];
   __shared__ uint64_t sT[2 * S], sM[S];
   __shared__ int s_go;
+  __shared__ uint64_t s_stamps[kStamps];
+  Stamps sp;
+  const bool stamped = stamps && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1);
+  if (stamped) {
+    sp.sh = s_stamps;
+    if (threadIdx.x == 0) {
+      s_stamps[0] = __builtin_amdgcn_s_memrealtime();
+      s_stamps[2] = __builtin_amdgcn_s_memtime();
+    }
+    sp.k = 1;
+  }
   uint32_t* const sb = byp + O::YL;
   const uint32_t* const ny = nyp + O::YL;
   const uint32_t* const npy = npyp + O::YL;
@@ -277,13 +308,20 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
     }
     __syncthreads();
   }
-  if (pair) O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM);
+  sp.mark();  // leaves loaded
+  if (pair) O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM, sp);
   // walk up: node (h, i) holds this block's value
   int h = 1;
   size_t i = b;
   while (((size_t)1 << h) < nleaves) {
     if (max_levels > 0 && h >= max_levels) {  // hand the node to the next launch
       for (int j = tid; j < S; j += kTreeThreads) lvl_out[i * S + j] = sa[j];
+      if (stamped) {
+        sp.mark();
+        if (threadIdx.x == 0) s_stamps[1] = __builtin_amdgcn_s_memrealtime() | ((uint64_t)sp.k << 56);
+        __syncthreads();
+        if (threadIdx.x < kStamps) stamps[(blockIdx.x == 0 ? 0 : kStamps) + threadIdx.x] = s_stamps[threadIdx.x];
+      }
       return;
     }
     const size_t sib = i ^ 1u;
@@ -323,7 +361,7 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
         for (int j = tid; j < S; j += kTreeThreads) sb[j] = __builtin_nontemporal_load(other + j);
       }
       __syncthreads();
-      O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM);
+      O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM, sp);
     }
     i >>= 1;
     ++h;
@@ -332,14 +370,21 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
   if (Y) {
     for (int j = tid; j < S; j += kTreeThreads) sb[j] = Y[j];
     __syncthreads();
-    O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM);
+    sp.mark();
+    O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM, sp);
   }
   if (tid < 64) O::canon(sa, consts + 2 * S);
   __syncthreads();
+  sp.mark();
   if (Y) {
     for (int j = tid; j < S; j += kTreeThreads) out[j] = sa[j];
   } else {
     for (int j = tid; j < Sout; j += kTreeThreads) out[j] = repack_limb(sa, S, W, Wout, j);
+  }
+  if (stamped) {
+    if (threadIdx.x == 0) s_stamps[1] = __builtin_amdgcn_s_memrealtime() | ((uint64_t)sp.k << 56);
+    __syncthreads();
+    if (threadIdx.x < kStamps) stamps[(blockIdx.x == 0 ? 0 : kStamps) + threadIdx.x] = s_stamps[threadIdx.x];
   }
 }
 
@@ -373,7 +418,8 @@ Shape tree_shape(size_t mod_bits) {
 
 // DDSHE_TREE_LEVELS (default 1; 0 = one launch walks to the root through in-kernel hand-offs, whose
 // agent-scope L2 writeback/invalidate fences measured far slower than a launch per level): levels per launch;
-// DDSHE_TREE_FENCE (default 1): hand-off fence style (k_tree); 2 = no cache maintenance (sc1 write-through
+// DDSHE_TREE_FENCE (default 1; with LEVELS != 1 only 0 or 2 are accepted): hand-off fence style (k_tree);
+// 2 = no cache maintenance (sc1 write-through
 // node stores and loads, relaxed flag): bit-exact on the GPU suite, and with it 2-5 levels per launch are
 // within run-to-run noise of one level per launch (10M-row tail 0.24-0.25 ms, 10k-row fold 0.12-0.13 ms)
 static int tree_env(const char* name, int dflt) {
@@ -381,11 +427,37 @@ static int tree_env(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
+// DDSHE_TREE_STAMPS=<file>: after every tree launch, synchronise and append one line per stamped block:
+// "S nleaves blocks block memtime_at_entry realtime_entry realtime_exit nmarks d1 d2 ..." (d = shader-clock
+// deltas between consecutive marks). Profiling only: it serialises the stream.
+static void dump_stamps(uint64_t* d_st, int S, size_t nleaves, size_t blocks, hipStream_t st) {
+  static const char* path = getenv("DDSHE_TREE_STAMPS");
+  uint64_t h[2 * kStamps];
+  if (hipStreamSynchronize(st) != hipSuccess || hipMemcpy(h, d_st, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
+    return;
+  FILE* f = fopen(path, "a");
+  if (!f) return;
+  for (int b = 0; b < (blocks > 1 ? 2 : 1); ++b) {
+    const uint64_t* v = h + b * kStamps;
+    const int nm = (int)(v[1] >> 56);
+    fprintf(f, "%d %zu %zu %s %llu %llu %llu %d", S, nleaves, blocks, b ? "last" : "first", (unsigned long long)v[2],
+            (unsigned long long)v[0], (unsigned long long)(v[1] & ((1ull << 56) - 1)), nm);
+    for (int k = 1; k < nm && k + 2 < kStamps; ++k) fprintf(f, " %llu", (unsigned long long)(v[2 + k] - v[1 + k]));
+    fprintf(f, "\n");
+  }
+  fclose(f);
+}
+
 hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Win, size_t nleaves, const uint32_t* ids,
                        const uint32_t* consts, const uint32_t* Y, uint32_t* nodes, uint32_t* flags, uint32_t* out,
                        int Sout, int Wout, hipStream_t st) {
   static const int levels = tree_env("DDSHE_TREE_LEVELS", 1), fence = tree_env("DDSHE_TREE_FENCE", 1);
+  static uint64_t* d_st = nullptr;
+  static const bool stamping = getenv("DDSHE_TREE_STAMPS") && hipMalloc(&d_st, 2 * kStamps * 8) == hipSuccess;
   if (nleaves == 0 || Sin > S + 64) return hipErrorInvalidValue;
+  // in-kernel hand-offs with wave-0-only fences rely on cache side effects the memory model does not
+  // promise: only the every-wave (0) and sc1 write-through (2) styles may hand off in-kernel
+  if (levels != 1 && fence == 1) return hipErrorInvalidValue;
   // level buffers for multi-launch trees live after the nodes: two ping-pong halves of nleaves rows
   uint32_t* lvl[2] = {nodes + (2 * nleaves + 2) * (size_t)S, nodes + (3 * nleaves + 2) * (size_t)S};
   size_t gstride = 1;
@@ -399,8 +471,10 @@ hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Wi
     }
     DDSHE_TREE_SWITCH(S, hipLaunchKernelGGL((k_tree<S, W>), dim3((unsigned)blocks), dim3(kTreeThreads), 0, st, X,
                                             xstride, gstride, Sin, Win, nleaves, ids, consts, Y, nodes, flags, out,
-                                            Sout, Wout, last ? 0 : levels, lvl[flip], fence));
+                                            Sout, Wout, last ? 0 : levels, lvl[flip], fence,
+                                            stamping ? d_st : nullptr));
     hipError_t e = hipGetLastError();
+    if (stamping && e == hipSuccess) dump_stamps(d_st, S, nleaves, blocks, st);
     if (e != hipSuccess || last) return e;
     X = lvl[flip];
     flip ^= 1;
