@@ -6,8 +6,10 @@
 // scala's sortWith is a stable merge sort, so equal keys keep their input order: LSD radix with
 // a stable per-tile rank reproduces that. Descending order sorts ~key (still stable for ties).
 //
-// Per 8-bit digit pass (8 passes; the last one has 257 buckets: the validity of the row moves it
-// to the end / front): k_rs_hist (per-tile digit counts, digit-major) -> k_rs_scan_digits (per-digit
+// Keys are offset by the smallest key of a holder (k_rs_prep / k_rs_red: min and max over the rows that
+// hold the position), so only the bytes of (max - min) are sorted: ceil(bits(max - min) / 8) passes
+// (an OPE column spanning 2^54 values needs 7, not 8). Per 8-bit digit pass (the last executed one
+// has 257 buckets: the validity of the row moves it to the end / front): k_rs_hist (per-tile digit counts, digit-major) -> k_rs_scan_digits (per-digit
 // scan over tiles, one block per digit, coalesced 1024-count chunks; the scatter blocks scan the 257
 // digit totals themselves) -> k_rs_scatter (stable rank inside the tile: each wave walks a contiguous
 // quarter of the tile, peers with equal digits are found with 9 ballots, per-wave digit counters in
@@ -30,73 +32,69 @@ constexpr int kRsDigits = 257;                    // 256 + the validity bucket o
 constexpr uint32_t kRsNone = 511;                 // digit of a lane past the end (never counted)
 constexpr uint64_t kSign = 0x8000000000000000ull;
 
-// rows lacking the position get key 0 so that earlier passes keep them in input order; the last
-// pass moves them to their bucket (256 / 0). The first executed pass derives the keys from the
-// column itself (no separate key buffer is written up front).
-__device__ __forceinline__ uint64_t rs_key_of(uint64_t raw, const uint8_t* __restrict__ valid, size_t i, int desc) {
+// Sort key of a holder: its value in unsigned order (descending: complemented), minus the smallest
+// such key (kmin). Rows lacking the position get key 0 so that earlier passes keep them in input
+// order; the last pass moves them to their bucket (256 / 0). The first executed pass derives the keys
+// from the column itself (no separate key buffer is written up front).
+__device__ __forceinline__ uint64_t rs_ukey(uint64_t raw, int desc) {
   const uint64_t u = raw ^ kSign;  // signed order -> unsigned order
-  return (valid && !valid[i]) ? 0ull : (desc ? ~u : u);
+  return desc ? ~u : u;
+}
+__device__ __forceinline__ uint64_t rs_key_of(uint64_t raw, const uint8_t* __restrict__ valid, size_t i, int desc,
+                                              uint64_t kmin) {
+  return (valid && !valid[i]) ? 0ull : rs_ukey(raw, desc) - kmin;
 }
 
-// OR / AND of all keys (per block, then k_rs_red): a byte where they agree is the same digit for
-// every row, and its pass is skipped. Reads the column once, writes nothing per row.
+// min / max of the holders' keys (per block, then k_rs_red): only the bytes of max - min are sorted.
+// Reads the column once, writes nothing per row.
 constexpr int kRsPrepRows = 16;  // rows per thread of k_rs_prep
+
+__device__ __forceinline__ void rs_minmax_block(uint64_t lo, uint64_t hi, uint64_t* __restrict__ out) {
+  __shared__ uint64_t slo[16], shi[16];
+  for (int off = 32; off >= 1; off >>= 1) {
+    lo = min(lo, (uint64_t)__shfl_xor((long long)lo, off));
+    hi = max(hi, (uint64_t)__shfl_xor((long long)hi, off));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    slo[threadIdx.x >> 6] = lo;
+    shi[threadIdx.x >> 6] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+      lo = min(lo, slo[w]);
+      hi = max(hi, shi[w]);
+    }
+    out[0] = min(lo, slo[0]);
+    out[1] = max(hi, shi[0]);
+  }
+}
 
 __global__ void __launch_bounds__(256) k_rs_prep(const int64_t* __restrict__ col, const uint8_t* __restrict__ valid,
                                                  size_t n, int desc, uint64_t* __restrict__ part) {
-  __shared__ uint64_t so[4], sa[4];
-  uint64_t o = 0, a = ~0ull;
+  uint64_t lo = ~0ull, hi = 0;
   const size_t base = (size_t)blockIdx.x * 256 * kRsPrepRows + threadIdx.x;
 #pragma unroll 4
   for (int k = 0; k < kRsPrepRows; ++k) {
     const size_t i = base + (size_t)k * 256;
-    if (i < n) {
-      const uint64_t key = rs_key_of((uint64_t)col[i], valid, i, desc);
-      o |= key;
-      a &= key;
+    if (i < n && (!valid || valid[i])) {
+      const uint64_t key = rs_ukey((uint64_t)col[i], desc);
+      lo = min(lo, key);
+      hi = max(hi, key);
     }
   }
-  for (int off = 32; off >= 1; off >>= 1) {
-    o |= (uint64_t)__shfl_xor((long long)o, off);
-    a &= (uint64_t)__shfl_xor((long long)a, off);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    so[threadIdx.x >> 6] = o;
-    sa[threadIdx.x >> 6] = a;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = so[0] | so[1] | so[2] | so[3];
-    part[2 * blockIdx.x + 1] = sa[0] & sa[1] & sa[2] & sa[3];
-  }
+  rs_minmax_block(lo, hi, part + 2 * blockIdx.x);
 }
 
-// OR / AND of the per-block partials -> red[0..1] (one block)
+// min / max of the per-block partials -> red[0..1] (one block; no holder at all: red[0] > red[1])
 __global__ void __launch_bounds__(1024) k_rs_red(const uint64_t* __restrict__ part, size_t nparts,
                                                  uint64_t* __restrict__ red) {
-  __shared__ uint64_t so[16], sa[16];
-  uint64_t o = 0, a = ~0ull;
+  uint64_t lo = ~0ull, hi = 0;
   for (size_t i = threadIdx.x; i < nparts; i += 1024) {
-    o |= part[2 * i];
-    a &= part[2 * i + 1];
+    lo = min(lo, part[2 * i]);
+    hi = max(hi, part[2 * i + 1]);
   }
-  for (int off = 32; off >= 1; off >>= 1) {
-    o |= (uint64_t)__shfl_xor((long long)o, off);
-    a &= (uint64_t)__shfl_xor((long long)a, off);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    so[threadIdx.x >> 6] = o;
-    sa[threadIdx.x >> 6] = a;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < 16; ++w) {
-      o |= so[w];
-      a &= sa[w];
-    }
-    red[0] = so[0] | o;
-    red[1] = sa[0] & a;
-  }
+  rs_minmax_block(lo, hi, red);
 }
 
 __global__ void k_rs_iota(uint32_t* __restrict__ ids, size_t n) {
@@ -115,9 +113,9 @@ __device__ __forceinline__ uint32_t rs_load_id(const uint32_t* __restrict__ ids,
 }
 
 __device__ __forceinline__ uint32_t rs_digit(uint64_t k, uint32_t id, const uint8_t* __restrict__ valid, int pass,
-                                             int desc, bool vbit) {
+                                             bool last, int desc, bool vbit) {
   uint32_t d = (uint32_t)(k >> (8 * pass)) & 0xFFu;
-  if (pass == 7 && valid) {
+  if (last && valid) {
     const bool v = vbit ? (id & kRsLack) == 0 : valid[id] != 0;
     d = desc ? (v ? d : 256u) : (v ? d + 1u : 0u);
   }
@@ -132,27 +130,27 @@ __device__ __forceinline__ size_t rs_row(size_t tile, int wid, int k, int lane) 
 __global__ void __launch_bounds__(kRsBlock) k_rs_hist(const uint64_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ ids,
                                                       const uint8_t* __restrict__ valid, size_t n, int pass,
-                                                      int desc, bool vbit, uint32_t* __restrict__ hist,
-                                                      size_t nblocks) {
+                                                      bool last, int desc, bool vbit, uint64_t kmin,
+                                                      uint32_t* __restrict__ hist, size_t nblocks) {
   __shared__ uint32_t cnt[kRsDigits];
   for (int d = threadIdx.x; d < kRsDigits; d += kRsBlock) cnt[d] = 0;
   __syncthreads();
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t lt = (1ull << lane) - 1ull;
-  const bool need_id = pass == 7 && valid;
+  const bool need_id = last && valid;
   // all loads first (independent, in flight together), then the LDS counting
   uint64_t key[kRsItems];
   uint32_t id[kRsItems];
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {  // unconditional loads (index clamped), masked below
     const size_t i = min(rs_row(blockIdx.x, wid, k, lane), n - 1);
-    key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc);  // first pass: keys = the column
+    key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc, kmin);  // first pass: keys = the column
     id[k] = need_id ? rs_load_id(ids, i, valid, vbit) : 0u;
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
     const size_t i = rs_row(blockIdx.x, wid, k, lane);
-    const uint32_t d = i < n ? rs_digit(key[k], id[k], valid, pass, desc, vbit) : kRsNone;
+    const uint32_t d = i < n ? rs_digit(key[k], id[k], valid, pass, last, desc, vbit) : kRsNone;
     // one LDS atomic per distinct digit of the wave (OPE columns repeat digits a lot; measured
     // faster than per-wave histograms with one atomic per row)
     uint64_t peers = ~0ull;
@@ -219,7 +217,7 @@ __global__ void __launch_bounds__(256) k_rs_scan_digits(uint32_t* __restrict__ h
 __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ ids,
                                                          const uint8_t* __restrict__ valid, size_t n, int pass,
-                                                         int desc, bool vbit, bool last,
+                                                         int desc, bool vbit, bool last, uint64_t kmin,
                                                          const uint32_t* __restrict__ hist,
                                                          const uint32_t* __restrict__ dtot, size_t nblocks,
                                                          uint64_t* __restrict__ keys_out,
@@ -262,13 +260,13 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {  // all loads first, unconditional (index clamped), masked below
     const size_t i = min(rs_row(blockIdx.x, wid, k, lane), n - 1);
-    key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc);  // first pass: keys = the column
+    key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc, kmin);  // first pass: keys = the column
     id[k] = rs_load_id(ids, i, valid, vbit);  // ids == nullptr: first executed pass, identity
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
     const size_t i = rs_row(blockIdx.x, wid, k, lane);
-    dr[k] = i < n ? rs_digit(key[k], id[k], valid, pass, desc, vbit) : kRsNone;
+    dr[k] = i < n ? rs_digit(key[k], id[k], valid, pass, last, desc, vbit) : kRsNone;
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
@@ -347,10 +345,12 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   hipError_t e = hipMemcpyAsync(hred, red, sizeof(hred), hipMemcpyDeviceToHost, st);
   if (e != hipSuccess) return e;
   if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-  // passes whose byte differs between keys (+ the last one when rows may lack the position)
+  // the bytes of max - min (at least one pass when rows may lack the position: its last pass buckets them)
+  const uint64_t kmin = hred[0] <= hred[1] ? hred[0] : 0ull;
+  const uint64_t span = hred[0] <= hred[1] ? hred[1] - hred[0] : 0ull;
   int passes[8], np = 0;
-  for (int p = 0; p < 8; ++p)
-    if ((((hred[0] ^ hred[1]) >> (8 * p)) & 0xFFu) || (p == 7 && valid)) passes[np++] = p;
+  for (int p = 0; p < 8 && (span >> (8 * p)) != 0; ++p) passes[np++] = p;
+  if (np == 0 && valid) passes[np++] = 0;
   if (np == 0) {
     hipLaunchKernelGGL(k_rs_iota, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out_ids, n);
     return hipGetLastError();
@@ -364,11 +364,11 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     uint32_t* ids_out = ((np - 1 - j) % 2 == 0) ? out_ids : ib;
     const bool last = j == np - 1;
     const bool vbit = valid && n <= (size_t)kRsLack;
-    hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)nb), dim3(kRsBlock), 0, st, kin, ids_in, valid, n, pass, desc, vbit,
-                       hist, nb);
+    hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)nb), dim3(kRsBlock), 0, st, kin, ids_in, valid, n, pass, last, desc,
+                       vbit, kmin, hist, nb);
     hipLaunchKernelGGL(k_rs_scan_digits, dim3(kRsDigits), dim3(256), 0, st, hist, nb, dtot);
     hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)nb), dim3(kRsBlock), 0, st, kin, ids_in, valid, n, pass, desc,
-                       vbit, last, hist, dtot, nb, last ? nullptr : kout, ids_out);
+                       vbit, last, kmin, hist, dtot, nb, last ? nullptr : kout, ids_out);
     kin = kout;
     kout = kout == ka ? kb : ka;
     ids_in = ids_out;

@@ -77,3 +77,45 @@ def test_order_skipped_passes(eng, kind):
     for desc in (True, False):
         assert np.array_equal(eng.ope_order(col, valid, desc), expected(col, valid, desc)), (kind, desc)
         assert np.array_equal(eng.ope_order(col, None, desc), expected(col, np.ones(n, np.uint8), desc)), (kind, desc)
+
+
+@pytest.mark.parametrize("kind", ["cross_sign_2p54", "no_holder", "one_holder", "extremes_only"])
+def test_order_key_span(eng, kind):
+    """Only the bytes of (max - min) of the holders' keys are sorted: a 2^54-wide range crossing zero
+    (the bench's OPE map) needs 7 passes, the validity bucket rides on the last executed one; columns
+    with no holder, one holder, or just INT64_MIN / INT64_MAX (a full 64-bit span) stay exact."""
+    rng = np.random.default_rng(17)
+    n = 200_003
+    if kind == "cross_sign_2p54":
+        col = rng.integers(-(1 << 52), 1 << 53, size=n, dtype=np.int64)
+        valid = (rng.random(n) > 0.05).astype(np.uint8)
+    elif kind == "no_holder":
+        col = rng.integers(-2**63, 2**63 - 1, size=n, dtype=np.int64)
+        valid = np.zeros(n, np.uint8)
+    elif kind == "one_holder":
+        col = rng.integers(-2**63, 2**63 - 1, size=n, dtype=np.int64)
+        valid = np.zeros(n, np.uint8)
+        valid[n // 3] = 1
+    else:
+        col = np.where(rng.random(n) > 0.5, np.int64(-2**63), np.int64(2**63 - 1))
+        valid = (rng.random(n) > 0.3).astype(np.uint8)
+    for desc in (True, False):
+        assert np.array_equal(eng.ope_order(col, valid, desc), expected(col, valid, desc)), (kind, desc)
+
+
+def test_order_sl_non_holders_32_rows(eng):
+    """OrderSL's comparator is not a strict order between two non-holders (DDSRestServer.scala:589-592:
+    lt is true both ways), so the JVM's TimSort may reorder them (or throw "Comparison method violates
+    its general contract") once its merge runs begin (>= 32 rows). Unpinned: the oracle keeps non-holders
+    in input order (a stable choice), and this pins the engine to that choice at 40+ rows."""
+    from ddshe import routes
+    rng = random.Random(40)
+    keyed = []
+    for i in range(96):
+        holds = rng.random() < 0.6
+        keyed.append((f"k{i:03d}", [str(rng.randrange(-9, 9)), "x"] if holds else []))
+    for route in ("OrderSL", "OrderLS"):
+        got = routes.order(eng, route, keyed, 0)
+        assert got == homo.order(route, keyed, 0), route
+        lack = [k for k, r in keyed if len(r) == 0]
+        assert [k for k in got if k in set(lack)] == lack  # non-holders keep their input order
