@@ -283,18 +283,19 @@ class SumWorkload(_Workload):
                 print("VERIFY FAILED: Dec(fold) != sum(m)", file=sys.stderr)
         roof = self.fold_roofline(S_32)
         roof["kernel"] = "k_fold<148,4,28> (first fold level over the rows)"
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-        if os.path.exists(tf):  # HBM bytes per launch from the committed rocprofv3 PMC passes, per row
-            pm = json.load(open(tf))
-            traffic = pm["hbm_bytes_per_launch"] / pm["rows_per_launch"] * self.mine  # each row read once
-        roof.update(traffic=traffic, traffic_unit="bytes/launch (PMC, profiles/r01_pmc_traffic.json)")
-        vf = os.path.join(ROOT, "profiles", "r01_pmc_valu_fold.json")
-        if os.path.exists(vf):  # rocprofv3 VALU counters of the same kernel (north star: VALU-roofline fraction)
-            dv = json.load(open(vf))["derived"]
-            roof["valu_pmc"] = {"mad_issue_frac_at_measured_clock": dv["mad_issue_frac_of_half_rate_peak_at_measured_clock"],
-                                "int64_share_of_valu": dv["valu_int64_share_of_valu"], "clock_GHz": dv["clock_GHz_est"],
-                                "source": "profiles/r01_pmc_valu_fold.json"}
+        # HBM bytes per launch from the committed rocprofv3 PMC passes of this kernel (10M rows, each read once)
+        traffic = pmc_traffic("sum", ("k_fold<148, 4, 28, true, false>",))
+        if traffic is not None:
+            traffic *= self.mine / 1e7
+        roof.update(traffic=traffic, traffic_unit=f"HBM bytes per launch (PMC, profiles/{PMC_FILE})")
+        for vname in ("r03_pmc_valu_fold.json", "r01_pmc_valu_fold.json"):
+            vf = os.path.join(ROOT, "profiles", vname)
+            if os.path.exists(vf):  # rocprofv3 VALU counters of the same kernel (north star: VALU-roofline fraction)
+                dv = json.load(open(vf))["derived"]
+                roof["valu_pmc"] = {"mad_issue_frac_at_measured_clock": dv["mad_issue_frac_of_half_rate_peak_at_measured_clock"],
+                                    "int64_share_of_valu": dv.get("valu_int64_share_of_valu", dv.get("mad_share_of_valu")),
+                                    "clock_GHz": dv["clock_GHz_est"], "source": "profiles/" + vname}
+                break
         cpu = None
         if self.world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(self.col, nsq, (nsq.bit_length() + 7) // 8, a.cpu_seconds)
@@ -621,7 +622,9 @@ def run_extra_configs(main_wl):
     return out
 
 
-PMC_FILE = "r02_pmc_filter_order.json"  # tools/profile_all.sh passes, summarised by tools/rocpd_stats.py
+# tools/profile_all.sh passes, summarised by tools/pmc_summary.py (newest round first)
+PMC_FILE = next((f for f in ("r03_pmc.json", "r02_pmc_filter_order.json")
+                 if os.path.exists(os.path.join(ROOT, "profiles", f))), "r02_pmc_filter_order.json")
 
 
 def pmc_traffic(workload, kernels, per_step=False):
@@ -638,6 +641,19 @@ def pmc_traffic(workload, kernels, per_step=False):
             return None
         tot += d["hbm_bytes_per_dispatch"] * (d["dispatches"] if per_step else 1)
     return tot
+
+
+def pmc_entry(workloads, kernel):
+    """(bytes per dispatch, dispatches) of `kernel` under the first of `workloads` that has it"""
+    tf = os.path.join(ROOT, "profiles", PMC_FILE)
+    if not os.path.exists(tf):
+        return None
+    ks = json.load(open(tf))["kernels"]
+    for w in workloads:
+        d = ks.get(f"{w}:{kernel}")
+        if d is not None:
+            return d["hbm_bytes_per_dispatch"], d["dispatches"]
+    return None
 
 
 def load_keyset(name):
@@ -856,6 +872,13 @@ class EncryptSumWorkload(_Workload):
                 "mac_per_encrypt_issued": mac_issued, "mac_per_encrypt_binary_ladder_n2": binary_mac,
                 "effective_vs_binary_ladder_n2": binary_mac * self.mine / enc_s / 1e12,
                 "avg_encrypt_ms": enc_s * 1e3, "traffic": None}
+        if not a.public:  # the ladder's HBM bytes (PMC), per dispatch: one dispatch per CRT half and 1M-row chunk
+            lad = pmc_entry(("encrypt_sum", "sum"), "k_modexp_ladder<112, 4, 28, true>")
+            if lad is not None:
+                roof["traffic"] = lad[0]
+                roof["traffic_unit"] = (f"HBM bytes per k_modexp_ladder<112,4,28> dispatch (PMC, profiles/{PMC_FILE});"
+                                        " the per-row window tables are streamed from HBM")
+                roof["traffic_rows_per_dispatch"] = self.mine
         cpu = None
         if self.world == 1 and not a.no_cpu_baseline:
             cpu = cpu_encrypt_baseline(k, self.rcol, self.ms, a.cpu_seconds, self.out)
