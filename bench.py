@@ -772,7 +772,7 @@ class ProductFilterWorkload(_Workload):
                 res_ok = res_ok and len(ids) == counts[op] and (len(ids) == 0 or bool(f(self.ope_host[ids], self.bound).all()))
         res_ms.sort()
         filt["resident_opecol_search"] = {"median_ms": res_ms[len(res_ms) // 2], "matches": res_ok,
-                                          "path": "dds_opecol_search (device filter + pinned D2H of the matching row ids)"}
+                                          "path": "dds_opecol_search (device filter + D2H of the matching row ids)"}
         # the route-shaped answer as a row bitmask (dds_opecol_search_mask): 1 bit per row crosses PCIe
         mk_ms, mk_ok = [], True
         for op, f in (("gt", np.greater), ("ge", np.greater_equal), ("lt", np.less), ("le", np.less_equal)):

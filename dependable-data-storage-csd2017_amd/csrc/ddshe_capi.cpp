@@ -138,7 +138,8 @@ int get_mod(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, std::shared_p
     bn::trim(inv);
     const bn::Limbs np = bn::sub(bn::pow2(k3), inv);  // -N^-1 mod R3 (inv != 0: N odd)
     std::vector<uint32_t> h3;
-    for (const bn::Limbs& v : {N, np, N, bn::add(N, N), bn::add(bn::add(N, N), N)}) {
+    const bn::Limbs r3 = bn::mod(bn::pow2(k3), N);
+    for (const bn::Limbs& v : {N, np, N, bn::add(N, N), bn::add(bn::add(N, N), N), bn::mod(bn::mul(r3, r3), N)}) {
       const std::vector<uint32_t> r = bn::to_rw(v, mc->S3, mc->W3);
       h3.insert(h3.end(), r.begin(), r.end());
     }
@@ -1142,34 +1143,30 @@ int dds_rsa_product(dds_ctx* ctx, const uint8_t* n, size_t n_bytes, const uint8_
 constexpr size_t kSmallPairs = 8;
 int small_pairs(Worker* w, hipStream_t st, ModConsts& mc, const uint8_t* a, const uint8_t* b, size_t width, size_t n,
                 size_t mod_bytes, uint8_t* out) {
-  const int S2 = mc.S2;
-  const size_t words = (size_t)S2 * n;
+  const int S3 = mc.S3;  // one workgroup per pair in the tree shape (k_pairs_sos)
+  const size_t words = (size_t)S3 * n;
   HIP_TRY(w->hch[0].ensure(3 * words * 4));
   HIP_TRY(w->x.ensure(3 * words * 4));
   uint32_t* h = (uint32_t*)w->hch[0].p;
-  const bn::Limbs twoN = bn::add(mc.N, mc.N);
   for (int k = 0; k < 2; ++k) {
     const uint8_t* src = k ? b : a;
     for (size_t i = 0; i < n; ++i) {
       bn::Limbs v = bn::from_be(src + i * width, width);
       if (bn::bit_length(v) > (size_t)mc.W * mc.S)  // as the lane-group path's ingest (k_ingest_be flag 2)
         return fail(DDS_E_RANGE, "operand wider than the modulus limb width");
-      if (bn::cmp(v, twoN) >= 0) v = bn::mod(v, mc.N);
-      const std::vector<uint32_t> rw = bn::to_rw(v, S2, mc.W);
-      for (int l = 0; l < S2; ++l) h[k * words + (size_t)l * n + i] = rw[l];
+      if (bn::cmp(v, mc.N) >= 0) v = bn::mod(v, mc.N);
+      const std::vector<uint32_t> rw = bn::to_rw(v, S3, mc.W3);
+      std::copy(rw.begin(), rw.end(), h + k * words + i * S3);
     }
   }
   uint32_t* d = w->x.as<uint32_t>();
   HIP_TRY(hipMemcpyAsync(d, h, 2 * words * 4, hipMemcpyHostToDevice, st));
-  HIP_TRY(launch_pairs_tail(S2, d, d + words, n, n, mc.d2, mc.n0, d + 2 * words, st));
+  HIP_TRY(launch_pairs_sos(S3, d, d + words, n, mc.d3, mc.d3 + 5 * (size_t)S3, d + 2 * words, st));
   HIP_TRY(hipMemcpyAsync(h + 2 * words, d + 2 * words, words * 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  std::vector<uint32_t> limbs(S2);
-  for (size_t i = 0; i < n; ++i) {
-    for (int l = 0; l < S2; ++l) limbs[l] = h[2 * words + (size_t)l * n + i];
-    if (!bn::to_be(mc.value2(limbs.data()), out + i * mod_bytes, mod_bytes))
+  for (size_t i = 0; i < n; ++i)
+    if (!bn::to_be(bn::from_rw(h + 2 * words + i * S3, S3, mc.W3), out + i * mod_bytes, mod_bytes))
       return fail(DDS_E_RANGE, "result does not fit");
-  }
   return DDS_OK;
 }
 

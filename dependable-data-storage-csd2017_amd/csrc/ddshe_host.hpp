@@ -125,7 +125,7 @@ struct ModConsts {
   uint32_t* dqm = nullptr;       // N~ in main limbs when R > 4N~ holds for the main shape, else null
   int S3 = 0, W3 = 0;            // reduction-tree shape (ddshe_tree.hip), R3 = 2^(W3*S3)
   bool tree_direct = false;      // raw rows (< 2^(W*S)) may be tree leaves: 2^(2WS) <= R3 * 2^(bits(N)-1)
-  uint32_t* d3 = nullptr;        // tree constants: N | n' = -N^-1 mod R3 | N | 2N | 3N
+  uint32_t* d3 = nullptr;        // tree constants: N | n' = -N^-1 mod R3 | N | 2N | 3N | R3^2 mod N
   std::map<int64_t, std::vector<uint32_t>> y3cache;  // E -> 2^(W3*S3 - E) mod N, tree limbs
   std::mutex ymu;
   std::map<int64_t, std::vector<uint32_t>> ycache;  // E -> 2^(W*S2 - E) mod N, tail limbs
@@ -266,19 +266,23 @@ namespace ddshe {
 namespace host {
 
 // Coalescing queue of the pairwise routes for one modulus: a caller queues its pair; whoever finds
-// the queue idle becomes the leader and runs one k_pairs launch over everything queued so far (group
-// commit: no added wait when calls arrive one at a time, one launch per burst under load).
+// a batch slot free becomes a leader and runs one k_pairs launch over everything queued so far (group
+// commit: no added wait when calls arrive one at a time, one launch per burst under load). Up to
+// kPairInflight batches run at once, each on its own stream, so one batch's host round trip overlaps
+// the next; a finished leader wakes exactly the callers it served and the oldest waiter (no herd).
+constexpr int kPairInflight = 2;
 struct PairReq {
   bn::Limbs a, b;  // magnitudes, already < N
   bn::Limbs r;     // a*b mod N
   int rc = 0;
   bool done = false;
+  bool taken = false;  // in a batch (no longer in pending)
+  std::condition_variable cv;
 };
 struct PairQueue {
   std::mutex mu;
-  std::condition_variable cv;
   std::vector<PairReq*> pending;
-  bool busy = false;
+  int inflight = 0;
 };
 
 // pinned staging of a worker (fixed 16 KiB, allocated once: pointers into it stay valid across a call):

@@ -66,6 +66,10 @@ Shape tree_shape(size_t mod_bits);
 hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Win, size_t nleaves, const uint32_t* ids,
                        const uint32_t* consts, const uint32_t* Y, uint32_t* nodes, uint32_t* flags, uint32_t* out,
                        int Sout, int Wout, hipStream_t st);
+// out[i] = A[i] * B[i] mod N in the tree shape (S limbs of W bits, row-major, operands < N, canonical
+// results): one workgroup per pair (k_pairs_sos). consts as launch_tree, R2 = R^2 mod N (R = 2^(W S)).
+hipError_t launch_pairs_sos(int S, const uint32_t* A, const uint32_t* B, size_t n, const uint32_t* consts,
+                            const uint32_t* R2, uint32_t* out, hipStream_t st);
 hipError_t launch_finalize_tail(int S, const uint32_t* P, size_t pstride, const uint32_t* consts, const uint32_t* Y,
                                 uint32_t n0, uint32_t* out, hipStream_t st);
 hipError_t launch_pairs(int S, const uint32_t* A, const uint32_t* B, size_t stride, size_t count,

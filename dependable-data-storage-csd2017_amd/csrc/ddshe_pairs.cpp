@@ -5,7 +5,9 @@
 // one Montgomery product; the proxy runs routes concurrently on its pool (DDSRestServer.scala:21), so
 // concurrent requests under one modulus share a queue and the first caller to find it idle runs ONE
 // k_pairs launch over every pair queued so far (the others sleep on the queue's condition variable
-// and wake with their result). A lone request pays no batching wait. A burst of up to kTailPairs
+// and wake with their result). A lone request pays no batching wait. Up to kPairInflight batches of
+// one modulus run at once (own streams): while one waits for its GPU round trip the next gathers and
+// launches. A burst of up to kTailPairs
 // pairs runs in the latency shape straight from the parsed limbs (one pinned H2D, one k_pairs launch,
 // one D2H, one synchronisation); larger ones take the batched dds_modmul_pairs path. A queue lives
 // while it has work: the last caller out of an idle queue drops it, so moduli sent once by clients
@@ -27,7 +29,7 @@ namespace {
 
 constexpr size_t kTailPairs = 256;
 
-// the batch in the tail (latency) shape from limbs already < M
+// the batch in the tree (latency) shape from limbs already < M: one workgroup product per pair
 int tail_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& batch) {
   const size_t mb = bn::byte_length(M), n = batch.size();
   std::vector<uint8_t> mbe(mb);
@@ -39,28 +41,22 @@ int tail_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& ba
   WorkerLease wl(ctx);
   if ((rc = wl.acquire())) return rc;
   Worker* w = wl.w;
-  const int S2 = mc.S2;
-  const size_t words = (size_t)S2 * n;
+  const int S3 = mc.S3;  // one workgroup per pair in the tree shape (k_pairs_sos)
+  const size_t words = (size_t)S3 * n;
   HIP_TRY(w->hch[1].ensure(3 * words * 4));
   HIP_TRY(w->x2.ensure(3 * words * 4));
   uint32_t* h = (uint32_t*)w->hch[1].p;
   for (size_t i = 0; i < n; ++i) {
-    const std::vector<uint32_t> ra = bn::to_rw(batch[i]->a, S2, mc.W), rb = bn::to_rw(batch[i]->b, S2, mc.W);
-    for (int l = 0; l < S2; ++l) {
-      h[(size_t)l * n + i] = ra[l];
-      h[words + (size_t)l * n + i] = rb[l];
-    }
+    const std::vector<uint32_t> ra = bn::to_rw(batch[i]->a, S3, mc.W3), rb = bn::to_rw(batch[i]->b, S3, mc.W3);
+    std::copy(ra.begin(), ra.end(), h + i * S3);
+    std::copy(rb.begin(), rb.end(), h + words + i * S3);
   }
   uint32_t* d = w->x2.as<uint32_t>();
   HIP_TRY(hipMemcpyAsync(d, h, 2 * words * 4, hipMemcpyHostToDevice, wl.st));
-  HIP_TRY(launch_pairs_tail(S2, d, d + words, n, n, mc.d2, mc.n0, d + 2 * words, wl.st));
+  HIP_TRY(launch_pairs_sos(S3, d, d + words, n, mc.d3, mc.d3 + 5 * (size_t)S3, d + 2 * words, wl.st));
   HIP_TRY(hipMemcpyAsync(h + 2 * words, d + 2 * words, words * 4, hipMemcpyDeviceToHost, wl.st));
   HIP_TRY(hipStreamSynchronize(wl.st));
-  std::vector<uint32_t> limbs(S2);
-  for (size_t i = 0; i < n; ++i) {
-    for (int l = 0; l < S2; ++l) limbs[l] = h[2 * words + (size_t)l * n + i];
-    batch[i]->r = mc.value2(limbs.data());
-  }
+  for (size_t i = 0; i < n; ++i) batch[i]->r = bn::from_rw(h + 2 * words + i * S3, S3, mc.W3);
   return DDS_OK;
 }
 
@@ -98,14 +94,15 @@ int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req) {
   std::unique_lock<std::mutex> lk(q->mu);
   q->pending.push_back(req);
   while (!req->done) {
-    if (q->busy) {
-      q->cv.wait(lk);
+    if (req->taken || q->inflight >= kPairInflight) {
+      req->cv.wait(lk);
       continue;
     }
     // leader: take everything queued (this request included) and launch once
-    q->busy = true;
+    ++q->inflight;
     std::vector<PairReq*> batch;
     batch.swap(q->pending);
+    for (PairReq* r : batch) r->taken = true;
     lk.unlock();
     try {
       run_batch(ctx, M, batch);
@@ -113,18 +110,21 @@ int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req) {
       for (PairReq* r : batch) r->rc = DDS_E_NOMEM;
     }
     lk.lock();
-    for (PairReq* r : batch) r->done = true;
-    q->busy = false;
-    q->cv.notify_all();  // finished requests return; a queued one becomes the next leader
+    --q->inflight;
+    for (PairReq* r : batch) {
+      r->done = true;
+      if (r != req) r->cv.notify_one();
+    }
+    if (!q->pending.empty()) q->pending.front()->cv.notify_one();  // the oldest waiter leads next
   }
-  const bool idle = !q->busy && q->pending.empty();
+  const bool idle = q->inflight == 0 && q->pending.empty();
   lk.unlock();
   if (idle) {  // drop the idle queue (a caller that still holds it just runs as its own leader)
     std::lock_guard<std::mutex> g(ctx->pmu);
     auto it = ctx->pair_queues.find(M);
     if (it != ctx->pair_queues.end() && it->second == q) {
       std::lock_guard<std::mutex> ql(q->mu);
-      if (!q->busy && q->pending.empty()) ctx->pair_queues.erase(it);
+      if (q->inflight == 0 && q->pending.empty()) ctx->pair_queues.erase(it);
     }
   }
   return req->rc;

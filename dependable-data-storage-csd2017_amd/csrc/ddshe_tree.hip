@@ -118,16 +118,18 @@ struct Sos {
   }
 
   // a <- a * b * R^-1 (mod N), redundant limbs < 2^W + 3, value < 4N. LDS: by, ny, npy = b, N, n' at
-  // their y[0] (zero-padded, see conv); a, d: XL words (zero past S); T: 2S words, M: S words.
-  // Ends with a barrier.
+  // their y[0] (zero-padded, see conv); a, d: XL words (zero past S); T2: two column buffers of 2S words
+  // (the product sums into T2[par] and zeroes T2[par ^ 1] for the next product), M: S words. T2[par]
+  // and M must be zero on entry (the kernel zeroes all three while it loads its leaves); par flips.
+  // Ends with a barrier. 6 barriers: the carry out of the low half is recomputed by every thread of the
+  // last phase instead of by one thread between two extra barriers.
   template <int NT>
-  __device__ static void monpro(uint32_t* a, const uint32_t* by, const uint32_t* ny, const uint32_t* npy, uint64_t* T,
-                                uint32_t* d, uint64_t* M, Stamps& sp) {
+  __device__ static void monpro(uint32_t* a, const uint32_t* by, const uint32_t* ny, const uint32_t* npy, uint64_t* T2,
+                                uint32_t* d, uint64_t* M, int& par, Stamps& sp) {
     const int tid = threadIdx.x;
-    for (int j = tid; j < 2 * S; j += NT) T[j] = 0;
-    for (int j = tid; j < S; j += NT) M[j] = 0;
-    __syncthreads();
-    sp.mark();
+    uint64_t* T = T2 + (size_t)par * 2 * S;
+    uint64_t* Tn = T2 + (size_t)(par ^ 1) * 2 * S;
+    par ^= 1;
     conv<NT>(a, by, T, 2 * S);  // T = a*b
     __syncthreads();
     sp.mark();
@@ -143,16 +145,23 @@ struct Sos {
     conv<NT>(d, ny, T, 2 * S);  // V = T + m*N
     __syncthreads();
     sp.mark();
-    if (tid == 0) {  // carry out of the low half (see the header): ceil(X / 2^3W), X < 2^(64+2W+1)
+    {
+      // carry out of the low half (see the header): ceil(X / 2^3W), X < 2^(64+2W+1); it lands in column S
       const uint64_t v2 = T[S - 1], v1 = T[S - 2], v0 = T[S - 3];
       unsigned __int128 x = ((unsigned __int128)v2 << (2 * W)) + ((unsigned __int128)v1 << W) + v0;
       x += ((unsigned __int128)1 << (3 * W)) - 1;
-      T[S] += (uint64_t)(x >> (3 * W));
+      const uint64_t cy = (uint64_t)(x >> (3 * W));
+      const uint64_t* U = T + S;
+      // limb j of U = split3 of the high columns (column 0 plus the carry), then one normalising step
+      auto col = [&](int p) -> uint64_t { return p < 0 ? 0ull : U[p] + (p == 0 ? cy : 0ull); };
+      auto sp3 = [&](int p) -> uint32_t {
+        if (p < 0) return 0u;
+        return ((uint32_t)col(p) & kMask) + ((uint32_t)(col(p - 1) >> W) & kMask) + (uint32_t)(col(p - 2) >> (2 * W));
+      };
+      for (int j = tid; j < S; j += NT) a[j] = (sp3(j) & kMask) + (sp3(j - 1) >> W);
+      for (int j = tid; j < 2 * S; j += NT) Tn[j] = 0;  // the next product's column sums
+      for (int j = tid; j < S; j += NT) M[j] = 0;       // M was last read before the previous barrier
     }
-    __syncthreads();
-    for (int j = tid; j < S; j += NT) d[j] = split3(T + S, j);
-    __syncthreads();
-    for (int j = tid; j < S; j += NT) a[j] = (d[j] & kMask) + (j >= 1 ? d[j - 1] >> W : 0u);
     __syncthreads();
     sp.mark();
   }
@@ -257,7 +266,8 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
   // y operands (b, N, n') zero-padded around y[0] (Sos::conv); x operands (a, d) zero past S
   __shared__ __attribute__((aligned(16))) uint32_t sa[O::XL], sd[O::XL], byp[O::YTOT], nyp[O::YTOT], npyp[O::YTOT];
   __shared__ uint32_t stmp[S + 64], stmp2[S + 64];
-  __shared__ uint64_t sT[2 * S], sM[S];
+  __shared__ uint64_t sT[2 * 2 * S], sM[S];
+  int par = 0;
   __shared__ int s_go;
   __shared__ uint64_t s_stamps[kStamps];
   Stamps sp;
@@ -285,6 +295,8 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
     sa[j] = 0u;
     sd[j] = 0u;
   }
+  for (int j = tid; j < 4 * S; j += NT) sT[j] = 0;  // both column buffers (Sos::monpro)
+  for (int j = tid; j < S; j += NT) sM[j] = 0;
   const size_t b = blockIdx.x;
   const bool pair = 2 * b + 1 < nleaves;
   {  // both leaves at once
@@ -309,7 +321,7 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
     __syncthreads();
   }
   sp.mark();  // leaves loaded
-  if (pair) O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM, sp);
+  if (pair) O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM, par, sp);
   // walk up: node (h, i) holds this block's value
   int h = 1;
   size_t i = b;
@@ -361,7 +373,7 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
         for (int j = tid; j < S; j += kTreeThreads) sb[j] = __builtin_nontemporal_load(other + j);
       }
       __syncthreads();
-      O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM, sp);
+      O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM, par, sp);
     }
     i >>= 1;
     ++h;
@@ -371,7 +383,7 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
     for (int j = tid; j < S; j += kTreeThreads) sb[j] = Y[j];
     __syncthreads();
     sp.mark();
-    O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM, sp);
+    O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM, par, sp);
   }
   if (tid < 64) O::canon(sa, consts + 2 * S);
   __syncthreads();
@@ -386,6 +398,48 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
     __syncthreads();
     if (threadIdx.x < kStamps) stamps[(blockIdx.x == 0 ? 0 : kStamps) + threadIdx.x] = s_stamps[threadIdx.x];
   }
+}
+
+// Pairwise products in the latency shape of the tree: block b computes out_b = A_b * B_b mod N
+// (canonical, S limbs of W bits, row-major like A and B; operands < N) as MonPro(MonPro(a, b), R^2):
+// two workgroup products of ~4 us each instead of two lane-group CIOS products of ~15 us (the /Sum and
+// /Mult routes, DDSRestServer.scala:385, :479, coalesced by ddshe_pairs.cpp).
+template <int S, int W>
+__global__ void __launch_bounds__(kTreeThreads) k_pairs_sos(const uint32_t* __restrict__ A, const uint32_t* __restrict__ B,
+                                                            const uint32_t* __restrict__ consts,
+                                                            const uint32_t* __restrict__ R2, uint32_t* __restrict__ out) {
+  using O = Sos<S, W>;
+  constexpr int NT = kTreeThreads;
+  __shared__ __attribute__((aligned(16))) uint32_t sa[O::XL], sd[O::XL], byp[O::YTOT], nyp[O::YTOT], npyp[O::YTOT];
+  __shared__ uint64_t sT[2 * 2 * S], sM[S];
+  uint32_t* const sb = byp + O::YL;
+  const uint32_t* const ny = nyp + O::YL;
+  const uint32_t* const npy = npyp + O::YL;
+  const int tid = threadIdx.x;
+  const size_t b = blockIdx.x;
+  for (int j = tid; j < O::YTOT; j += NT) {
+    const int k = j - O::YL;
+    const bool in = k >= 0 && k < S;
+    byp[j] = in ? B[b * S + k] : 0u;
+    nyp[j] = in ? consts[k] : 0u;
+    npyp[j] = in ? consts[S + k] : 0u;
+  }
+  for (int j = tid; j < O::XL; j += NT) {
+    sa[j] = j < S ? A[b * S + j] : 0u;
+    sd[j] = 0u;
+  }
+  for (int j = tid; j < 4 * S; j += NT) sT[j] = 0;
+  for (int j = tid; j < S; j += NT) sM[j] = 0;
+  __syncthreads();
+  int par = 0;
+  Stamps sp;
+  O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM, par, sp);  // a b R^-1
+  for (int j = tid; j < S; j += NT) sb[j] = R2[j];
+  __syncthreads();
+  O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM, par, sp);  // a b
+  if (tid < 64) O::canon(sa, consts + 2 * S);
+  __syncthreads();
+  for (int j = tid; j < S; j += NT) out[b * S + j] = sa[j];
 }
 
 #define DDSHE_TREE_SWITCH(S_RT, ...)                 \
@@ -446,6 +500,14 @@ static void dump_stamps(uint64_t* d_st, int S, size_t nleaves, size_t blocks, hi
     fprintf(f, "\n");
   }
   fclose(f);
+}
+
+hipError_t launch_pairs_sos(int S, const uint32_t* A, const uint32_t* B, size_t n, const uint32_t* consts,
+                            const uint32_t* R2, uint32_t* out, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  DDSHE_TREE_SWITCH(S, hipLaunchKernelGGL((k_pairs_sos<S, W>), dim3((unsigned)n), dim3(kTreeThreads), 0, st, A, B,
+                                          consts, R2, out));
+  return hipGetLastError();
 }
 
 hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Win, size_t nleaves, const uint32_t* ids,

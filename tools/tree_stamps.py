@@ -22,7 +22,7 @@ os.environ["DDSHE_TREE_STAMPS"] = PATH
 
 import ddshe  # noqa: E402
 
-PHASES = ["load", "zero", "T=a*b", "split", "m=d*n'", "split", "V=T+m*N", "carry+split+norm", "handoff"]
+PHASES = ["load", "T=a*b", "split_T", "m=d*n'", "split_m", "V=T+m*N", "carry+split+norm", "handoff"]
 
 
 def main():
