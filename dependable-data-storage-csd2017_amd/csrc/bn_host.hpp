@@ -5,6 +5,7 @@
 // new BigInteger(String), DDSRestServer.scala:417,419,422). No per-row
 // arithmetic of the hot path runs here: that is on the GPU.
 #pragma once
+#include <cstdio>
 #include <stdint.h>
 
 #include <algorithm>
@@ -214,6 +215,7 @@ inline bool from_dec(const char* s, size_t len, Limbs& out, bool* neg) {
   }
   if (i == len) return false;
   Limbs r;
+  r.reserve((len - i) / 9 + 2);  // > log2(10^9)/32 limbs per 9 digits: no reallocation below
   while (i < len) {
     uint32_t chunk = 0, mulv = 1;
     int k = 0;
@@ -222,7 +224,13 @@ inline bool from_dec(const char* s, size_t len, Limbs& out, bool* neg) {
       chunk = chunk * 10 + (uint32_t)(s[i] - '0');
       mulv *= 10;
     }
-    r = mul_small_add(r, mulv, chunk);
+    uint64_t c = chunk;  // r = r * mulv + chunk, in place
+    for (auto& x : r) {
+      c += (uint64_t)x * mulv;
+      x = (uint32_t)c;
+      c >>= 32;
+    }
+    if (c) r.push_back((uint32_t)c);
   }
   trim(r);
   if (r.empty()) *neg = false;
@@ -230,20 +238,50 @@ inline bool from_dec(const char* s, size_t len, Limbs& out, bool* neg) {
   return true;
 }
 
-inline std::string to_dec(Limbs a, bool neg = false) {
-  if (a.empty()) return "0";
-  std::string s;
-  while (!a.empty()) {
-    uint32_t rem = divmod_small(a, 1000000000u);
-    for (int k = 0; k < 9; ++k) {
-      s.push_back((char)('0' + rem % 10));
-      rem /= 10;
-      if (a.empty() && rem == 0) break;
+// BigInteger.toString: repeated division by 10^18 over 64-bit words, each step a two-word by one-word
+// division with a precomputed reciprocal (Moller-Granlund, divisor normalised to 2^63..2^64): about a
+// quarter of the steps of dividing 32-bit limbs by 10^9 (the /Sum reply, DDSRestServer.scala:385-387,
+// is a 1233-digit number for the committed key).
+inline std::string to_dec(const Limbs& a32, bool neg = false) {
+  if (a32.empty()) return "0";
+  constexpr uint64_t D = 1000000000000000000ull;  // 10^18 < 2^60
+  constexpr int SH = 4;                            // D << 4 in [2^63, 2^64)
+  constexpr uint64_t DN = D << SH;
+  const uint64_t DINV = (uint64_t)((~(unsigned __int128)0) / DN - ((unsigned __int128)1 << 64));
+  std::vector<uint64_t> w((a32.size() + 1) / 2);
+  for (size_t i = 0; i < a32.size(); ++i) w[i / 2] |= (uint64_t)a32[i] << (32 * (i % 2));
+  while (!w.empty() && w.back() == 0) w.pop_back();
+  std::vector<uint64_t> chunks;  // base-10^18 digits, least significant first
+  while (!w.empty()) {
+    uint64_t rem = 0;
+    for (size_t i = w.size(); i-- > 0;) {
+      const uint64_t x = w[i];
+      const uint64_t nh = (rem << SH) | (x >> (64 - SH)), nl = x << SH;  // nh < DN since rem < D
+      const unsigned __int128 p = (unsigned __int128)nh * DINV + (((unsigned __int128)(nh + 1) << 64) | nl);
+      uint64_t q = (uint64_t)(p >> 64);
+      uint64_t r = nl - q * DN;
+      if (r > (uint64_t)p) {
+        --q;
+        r += DN;
+      }
+      if (r >= DN) {
+        ++q;
+        r -= DN;
+      }
+      w[i] = q;
+      rem = r >> SH;
     }
+    chunks.push_back(rem);
+    while (!w.empty() && w.back() == 0) w.pop_back();
   }
-  while (s.size() > 1 && s.back() == '0') s.pop_back();
+  std::string s;
   if (neg) s.push_back('-');
-  std::reverse(s.begin(), s.end());
+  s += std::to_string(chunks.back());
+  char buf[24];
+  for (size_t i = chunks.size() - 1; i-- > 0;) {
+    snprintf(buf, sizeof(buf), "%018llu", (unsigned long long)chunks[i]);
+    s += buf;
+  }
   return s;
 }
 

@@ -275,8 +275,9 @@ struct PairReq {
   bn::Limbs a, b;  // magnitudes, already < N
   bn::Limbs r;     // a*b mod N
   int rc = 0;
-  bool done = false;
-  bool taken = false;  // in a batch (no longer in pending)
+  std::atomic<bool> done{false};  // release-stored by the leader after r / rc
+  bool taken = false;     // in a batch (no longer in pending); under the queue mutex
+  bool sleeping = false;  // blocked on cv (else spinning on `done`: the leader must not touch it after)
   std::condition_variable cv;
 };
 struct PairQueue {

@@ -14,7 +14,9 @@
 // leave nothing behind.
 #include <string.h>
 
+#include <chrono>
 #include <condition_variable>
+#include <thread>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -93,9 +95,24 @@ int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req) {
   }
   std::unique_lock<std::mutex> lk(q->mu);
   q->pending.push_back(req);
-  while (!req->done) {
-    if (req->taken || q->inflight >= kPairInflight) {
+  while (!req->done.load(std::memory_order_acquire)) {
+    if (req->taken) {
+      // in another leader's batch: spin briefly without the lock (a batch takes tens of µs), then sleep
+      lk.unlock();
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(400);
+      while (!req->done.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < until)
+        std::this_thread::yield();
+      lk.lock();
+      if (req->done.load(std::memory_order_acquire)) break;
+      req->sleeping = true;
       req->cv.wait(lk);
+      req->sleeping = false;
+      continue;
+    }
+    if (q->inflight >= kPairInflight) {
+      req->sleeping = true;
+      req->cv.wait(lk);
+      req->sleeping = false;
       continue;
     }
     // leader: take everything queued (this request included) and launch once
@@ -111,11 +128,16 @@ int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req) {
     }
     lk.lock();
     --q->inflight;
+    if (!q->pending.empty() && q->pending.front()->sleeping) q->pending.front()->cv.notify_one();  // next leader
     for (PairReq* r : batch) {
-      r->done = true;
-      if (r != req) r->cv.notify_one();
+      if (r == req) continue;
+      // a spinning waiter may return (and free r) as soon as `done` is set: read `sleeping` first; a
+      // sleeping one cannot return before we release the mutex
+      const bool sl = r->sleeping;
+      r->done.store(true, std::memory_order_release);
+      if (sl) r->cv.notify_one();
     }
-    if (!q->pending.empty()) q->pending.front()->cv.notify_one();  // the oldest waiter leads next
+    req->done.store(true, std::memory_order_release);
   }
   const bool idle = q->inflight == 0 && q->pending.empty();
   lk.unlock();
@@ -144,7 +166,19 @@ int dds_pair_modmul_dec(dds_ctx* ctx, const char* a_dec, const char* b_dec, cons
     bool an = false, bneg = false, mneg = false;
     if (!bn::from_dec(a_dec, strlen(a_dec), a, &an)) return fail(DDS_E_FORMAT, "NumberFormatException: operand1");
     if (!bn::from_dec(b_dec, strlen(b_dec), b, &bneg)) return fail(DDS_E_FORMAT, "NumberFormatException: operand2");
-    if (!bn::from_dec(mod_dec, strlen(mod_dec), M, &mneg)) return fail(DDS_E_FORMAT, "NumberFormatException: modulus");
+    {  // the route passes the same nsqr / pubkey modulus with every request: keep the last parse per thread
+      thread_local std::string last_text;
+      thread_local bn::Limbs last_mod;
+      thread_local bool last_neg = false, last_ok = false;
+      const size_t ml = strlen(mod_dec);
+      if (!(last_text.size() == ml && memcmp(last_text.data(), mod_dec, ml) == 0)) {
+        last_text.assign(mod_dec, ml);
+        last_ok = bn::from_dec(mod_dec, ml, last_mod, &last_neg);
+      }
+      if (!last_ok) return fail(DDS_E_FORMAT, "NumberFormatException: modulus");
+      M = last_mod;
+      mneg = last_neg;
+    }
     if (mneg || M.empty()) return fail(DDS_E_FORMAT, "ArithmeticException: BigInteger: modulus not positive");
     if (!(M[0] & 1u) || bn::bit_length(M) < 2) {  // even modulus or 1: the fold's CRT path, uncoalesced
       const char* vals[2] = {a_dec, b_dec};
