@@ -10,6 +10,11 @@ branch, :class:`ServerError` the 500 branch.
 Element values are Python objects standing for what ``AnyJsonFormat`` reads
 (``DDSJsonProtocol.scala:22-28``): ``str`` (JsString), ``int`` (JsNumber → Int), ``bool``,
 ``None`` (JsNull). A route that parses an element uses its ``toString``.
+
+These functions take the fetched rows of ONE request, as the reference route does, and are the
+parity form of each route: ``search`` / ``order`` / ``search_eq`` build a device table for the
+request and free it afterwards. The serving form keeps the columns resident across requests and
+follows the write routes: ``ddshe.store.ResidentStore``.
 """
 from __future__ import annotations
 
