@@ -58,38 +58,42 @@ struct Sos {
 
   // Column sums as a register-blocked convolution. Work unit = (chunk of C consecutive x limbs,
   // block of 4 consecutive columns): the lane loads the C + 4 y words its 4 columns meet in the chunk
-  // once (aligned 128-bit reads), the chunk's x words as 128-bit broadcasts, and runs 4 C mads on 4
-  // independent accumulators, then adds its 4 sums into the columns (LDS 64-bit atomics: the chunks
-  // of one column land from different waves). A wave holds one chunk and the 64 column blocks from
-  // the chunk's first column on: the band of S + C - 1 columns the chunk reaches (one wave for
-  // S <= 240), so the ~S / C chunks of a pass fit the 16 waves in about one round.
+  // once (128-bit reads of a native 4-vector: as 32-bit words the compiler pairs them into read2 with
+  // 8-way bank conflicts, 1.7x slower), the chunk's x words as 128-bit reads, and runs 4 C mads on 4
+  // independent accumulators, then adds its 4 sums into the columns (LDS 64-bit atomics: the chunks of
+  // one column land from different lanes). Only the units that reach the requested columns
+  // [c_lo, c_hi) work, flattened over all the workgroup's lanes (a lane per unit: S = 162 has 630 for a
+  // full product, 1024 lanes), so a pass is one round of at most 4 C mads per lane; the m*N pass asks
+  // only for the high half (+3 columns for the carry), about half the units.
+  // tools/microbench/tree_conv.hip: 2700 -> 1420 cycles per full S = 162 pass (one chunk per wave with
+  // 32-bit y reads before).
   static constexpr int C = S <= 64 ? 4 : S <= 128 ? 8 : S <= 192 ? 12 : S <= 256 ? 16 : S <= 384 ? 24 : 48;
   static constexpr int NCH = (S + C - 1) / C;    // chunks
   static constexpr int XL = (NCH * C + 3) / 4 * 4;    // x operands: zero words up to XL
   static constexpr int YL = (C + 8 + 3) / 4 * 4;      // zero words before y[0] (multiple of 4: aligned strips)
   static constexpr int YTOT = YL + S + S + 8;         // ... and S + 8 after y[S-1]
   static constexpr int BAND = (S + C + 2) / 4 + 1;    // column blocks a chunk can reach
-  static constexpr int NGR = (BAND + 63) / 64;
   static_assert(YL % 4 == 0 && C % 4 == 0, "aligned strips");
 
-  // acc[col] += sum_i x[i] * y[col - i] for col < ncols; x: XL words (16-byte aligned, zero past S);
-  // yz: y[0] (16-byte aligned), zero for indices in [-YL, 0) and [S, 2S + 8)
+  // acc[col] += sum_i x[i] * y[col - i] for c_lo <= col < c_hi; x: XL words (16-byte aligned, zero past
+  // S); yz: y[0] (16-byte aligned), zero for indices in [-YL, 0) and [S, 2S + 8)
   template <int NT>
   __device__ static __forceinline__ void conv(const uint32_t* __restrict__ x, const uint32_t* __restrict__ yz,
-                                              uint64_t* acc, int ncols) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ncb = (ncols + 3) / 4;
-    for (int u = wave; u < NCH * NGR; u += NT / 64) {
-      const int ch = u / NGR, g = u - ch * NGR;
+                                              uint64_t* acc, int c_lo, int c_hi) {
+    const int cb_lo = c_lo / 4, cb_hi = (c_hi + 3) / 4;
+    const u32x4* const y4 = reinterpret_cast<const u32x4*>(yz);
+    const u32x4* const x4 = reinterpret_cast<const u32x4*>(x);
+    for (int u = threadIdx.x; u < NCH * BAND; u += NT) {
+      // unit u -> (chunk, column block): a chunk reaches BAND blocks from i0/4 on; blocks outside the
+      // requested columns or past the band's end (every term there has col - i >= S) are idle lanes
+      const int ch = u / BAND, cb = ch * C / 4 + (u - ch * BAND);
+      if (cb < cb_lo || cb >= cb_hi || 4 * cb > ch * C + C + S - 2) continue;
       const int i0 = ch * C;
-      const int cb = i0 / 4 + g * 64 + lane;
-      // past the columns asked for, or past the band (every term has col - i >= S)
-      if (cb >= ncb || 4 * cb > i0 + C + S - 2) continue;
       const int base = 4 * cb - i0 - C;  // ys[q] = y[base + q]; term (i0 + r, 4 cb + j) is ys[C + j - r]
       uint32_t ys[C + 4];
 #pragma unroll
       for (int q = 0; q < C + 4; q += 4) {
-        const uint4 v = *(const uint4*)(yz + base + q);
+        const u32x4 v = y4[(base + q) >> 2];
         ys[q] = v.x;
         ys[q + 1] = v.y;
         ys[q + 2] = v.z;
@@ -98,7 +102,7 @@ struct Sos {
       uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
 #pragma unroll
       for (int r4 = 0; r4 < C; r4 += 4) {
-        const uint4 xv = *(const uint4*)(x + i0 + r4);
+        const u32x4 xv = x4[(i0 + r4) >> 2];
         const uint32_t xr[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -110,10 +114,10 @@ struct Sos {
         }
       }
       const int col = 4 * cb;
-      if (c0) atomicAdd((unsigned long long*)&acc[col], (unsigned long long)c0);
-      if (c1 && col + 1 < ncols) atomicAdd((unsigned long long*)&acc[col + 1], (unsigned long long)c1);
-      if (c2 && col + 2 < ncols) atomicAdd((unsigned long long*)&acc[col + 2], (unsigned long long)c2);
-      if (c3 && col + 3 < ncols) atomicAdd((unsigned long long*)&acc[col + 3], (unsigned long long)c3);
+      if (c0 && col >= c_lo) atomicAdd((unsigned long long*)&acc[col], (unsigned long long)c0);
+      if (c1 && col + 1 >= c_lo && col + 1 < c_hi) atomicAdd((unsigned long long*)&acc[col + 1], (unsigned long long)c1);
+      if (c2 && col + 2 >= c_lo && col + 2 < c_hi) atomicAdd((unsigned long long*)&acc[col + 2], (unsigned long long)c2);
+      if (c3 && col + 3 >= c_lo && col + 3 < c_hi) atomicAdd((unsigned long long*)&acc[col + 3], (unsigned long long)c3);
     }
   }
 
@@ -130,19 +134,19 @@ struct Sos {
     uint64_t* T = T2 + (size_t)par * 2 * S;
     uint64_t* Tn = T2 + (size_t)(par ^ 1) * 2 * S;
     par ^= 1;
-    conv<NT>(a, by, T, 2 * S);  // T = a*b
+    conv<NT>(a, by, T, 0, 2 * S);  // T = a*b
     __syncthreads();
     sp.mark();
     for (int p = tid; p < S; p += NT) d[p] = split3(T, p);
     __syncthreads();
     sp.mark();
-    conv<NT>(d, npy, M, S);  // m = d * n' mod R (low columns)
+    conv<NT>(d, npy, M, 0, S);  // m = d * n' mod R (low columns)
     __syncthreads();
     sp.mark();
     for (int p = tid; p < S; p += NT) d[p] = split3(M, p);  // d now holds m (< 3*2^W limbs)
     __syncthreads();
     sp.mark();
-    conv<NT>(d, ny, T, 2 * S);  // V = T + m*N
+    conv<NT>(d, ny, T, S - 3, 2 * S);  // V = T + m*N: the high half and the 3 columns of the carry
     __syncthreads();
     sp.mark();
     {
@@ -284,6 +288,19 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
   const uint32_t* const ny = nyp + O::YL;
   const uint32_t* const npy = npyp + O::YL;
   const int tid = threadIdx.x;
+  const size_t b = blockIdx.x;
+  const bool pair = 2 * b + 1 < nleaves;
+  // the leaves' words first (Sin <= S + 64 < kTreeThreads: one per thread), so their global loads are in
+  // flight together with the constants' below: one memory round trip instead of two
+  uint32_t lw0 = 0, lw1 = 0;
+  {
+    const size_t r0 = ids ? (size_t)ids[2 * b] : 2 * b;
+    const size_t r1 = pair ? (ids ? (size_t)ids[2 * b + 1] : 2 * b + 1) : r0;
+    if (tid < Sin) {
+      lw0 = X[(size_t)tid * xstride + r0 * gstride];
+      if (pair) lw1 = X[(size_t)tid * xstride + r1 * gstride];
+    }
+  }
   for (int j = tid; j < O::YTOT; j += NT) {
     const int k = j - O::YL;  // logical index
     const bool in = k >= 0 && k < S;
@@ -297,14 +314,10 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
   }
   for (int j = tid; j < 4 * S; j += NT) sT[j] = 0;  // both column buffers (Sos::monpro)
   for (int j = tid; j < S; j += NT) sM[j] = 0;
-  const size_t b = blockIdx.x;
-  const bool pair = 2 * b + 1 < nleaves;
   {  // both leaves at once
-    const size_t r0 = ids ? (size_t)ids[2 * b] : 2 * b;
-    const size_t r1 = pair ? (ids ? (size_t)ids[2 * b + 1] : 2 * b + 1) : r0;
-    for (int l = tid; l < Sin; l += kTreeThreads) {
-      stmp[l] = X[(size_t)l * xstride + r0 * gstride];
-      if (pair) stmp2[l] = X[(size_t)l * xstride + r1 * gstride];
+    if (tid < Sin) {
+      stmp[tid] = lw0;
+      stmp2[tid] = lw1;
     }
     __syncthreads();
     if (Sin == S && Win == W) {  // a previous launch's nodes: redundant limbs (< 2^W + 3), kept as they are
