@@ -191,6 +191,37 @@ class _Workload:
     def reset_timers(self):
         pass
 
+    def strong_split_line(self, full, parts=8):
+        """The 8-GPU strong split stated on one GPU: one rank's share (rows/8) folded to a device partial
+        (dds_col_fold_partial_device) and the combine of 8 such partials (dds_combine_partials_device) timed
+        separately; the 8 partials cover all rows, so the combine must equal the full fold."""
+        torch = self.torch
+        pw = self.col.partial_words
+        cnt = self.mine // parts
+        buf = torch.empty(parts * pw, dtype=torch.int32, device="cuda")
+
+        def fold_share(i):
+            self.col.fold_partial_device(buf.data_ptr() + 4 * i * pw, i * cnt, cnt)
+            torch.cuda.synchronize()
+
+        def med(fn, reps=9):
+            ts = []
+            for _ in range(reps):
+                t = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t)
+            return sorted(ts)[reps // 2] * 1e3
+        for i in range(parts):
+            fold_share(i)
+        share_ms = med(lambda: fold_share(0))
+        rows = [cnt] * parts
+        got = self.eng.combine_partials_device(self.nsq, buf.data_ptr(), rows)
+        comb_ms = med(lambda: self.eng.combine_partials_device(self.nsq, buf.data_ptr(), rows))
+        return {"rows_per_share": cnt, "shares": parts, "share_fold_partial_ms": share_ms,
+                "combine_ms": comb_ms, "combined_equals_full_fold": got == full if cnt * parts == self.mine else None,
+                "note": "an 8-GPU strong-split step is about share_fold_partial_ms + one all-gather of "
+                        f"{parts}x{4 * pw} B + combine_ms (host wall clock, each call synchronised)"}
+
     def extra_distributed(self):
         return {}
 
@@ -284,7 +315,7 @@ class SumWorkload(_Workload):
         roof = self.fold_roofline(S_32)
         roof["kernel"] = "k_fold<148,4,28> (first fold level over the rows)"
         # HBM bytes per launch from the committed rocprofv3 PMC passes of this kernel (10M rows, each read once)
-        traffic = pmc_traffic("sum", ("k_fold<148, 4, 28, true, false>",))
+        traffic = pmc_traffic("sum", ("k_fold<148, 4, 28, true, false>",), largest=True)
         if traffic is not None:
             traffic *= self.mine / 1e7
         roof.update(traffic=traffic, traffic_unit=f"HBM bytes per launch (PMC, profiles/{PMC_FILE})")
@@ -302,12 +333,13 @@ class SumWorkload(_Workload):
         e2e = None
         if self.world == 1 and not a.no_e2e:
             e2e = self.end_to_end(res)
+        split = self.strong_split_line(res) if self.world == 1 else None
         out = self.common("Paillier homomorphic adds/sec (2048-bit key, mod n^2)",
                           (self.total - 1) * a.steps / elapsed, "HomoAdd/s", elapsed,
                           "paillier_sumall_fold_10M_2048bit",
                           {"key_bits": key["n"].bit_length(), "modulus_bits": nsq.bit_length()})
         out.update(data="synthetic (seeded Paillier ciphertexts, committed key)", roofline=roof, cpu_baseline=cpu,
-                   end_to_end=e2e, verified=ok,
+                   end_to_end=e2e, verified=ok, strong_split_1gpu=split,
                    fold_tail_ms=elapsed / a.steps * 1e3 - roof["avg_launch_ms"] if roof["achieved"] else None)
         return out
 
@@ -627,9 +659,10 @@ PMC_FILE = next((f for f in ("r03_pmc.json", "r02_pmc_filter_order.json")
                  if os.path.exists(os.path.join(ROOT, "profiles", f))), "r02_pmc_filter_order.json")
 
 
-def pmc_traffic(workload, kernels, per_step=False):
+def pmc_traffic(workload, kernels, per_step=False, largest=False):
     """HBM bytes per call from the committed rocprofv3 PMC passes (10M rows): the sum over `kernels`
-    of bytes per dispatch (times dispatches per call when per_step: the PMC run did one call)."""
+    of bytes per dispatch (times dispatches per call when per_step: the PMC run did one call; the
+    largest dispatch when `largest`: the 10M-row launch among the extra lines' smaller ones)."""
     tf = os.path.join(ROOT, "profiles", PMC_FILE)
     if not os.path.exists(tf):
         return None
@@ -639,7 +672,10 @@ def pmc_traffic(workload, kernels, per_step=False):
         d = ks.get(f"{workload}:{k}")
         if d is None:
             return None
-        tot += d["hbm_bytes_per_dispatch"] * (d["dispatches"] if per_step else 1)
+        if largest and "hbm_bytes_max_dispatch" in d:
+            tot += d["hbm_bytes_max_dispatch"]
+        else:
+            tot += d["hbm_bytes_per_dispatch"] * (d["dispatches"] if per_step else 1)
     return tot
 
 
@@ -932,7 +968,7 @@ class OrderWorkload(_Workload):
                 print("VERIFY FAILED", file=sys.stderr)
         step_s = elapsed / a.steps
         alg = 13 * self.mine  # read key + valid byte, write one row id
-        roof = {"bound": "hbm", "kernel": "k_rs_hist/k_rs_scan/k_rs_scatter (8 LSD passes)",
+        roof = {"bound": "hbm", "kernel": "k_rs_hist/k_rs_scan/k_rs_scatter (LSD passes over the bytes of the key span: 7 here)",
                 "achieved": alg / step_s / 1e9, "peak": 8000.0, "unit": "GB/s", "frac": alg / step_s / 1e9 / 8000.0,
                 "algorithmic_bytes": alg, "issued_bytes_est": self.mine * (8 * 32 + 9),  # 8 passes x (hist 8 + scatter 24) + prep
                 "traffic": pmc_traffic("order", ("k_rs_prep", "k_rs_red", "k_rs_hist", "k_rs_scan_digits", "k_rs_scatter"),
