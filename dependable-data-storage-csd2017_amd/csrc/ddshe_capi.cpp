@@ -230,6 +230,16 @@ size_t tree_switch_leaves() {
   return n;
 }
 
+// DDSHE_NARROW_ROWS (rows, default 65536; 0 disables): folds of up to that many rows run their first
+// level in the latency (tail) shape, one product per group, straight from the main-shape rows
+size_t narrow_fold_rows() {
+  static const size_t n = [] {
+    const char* e = getenv("DDSHE_NARROW_ROWS");
+    return e ? (size_t)atoll(e) : (size_t)65536;
+  }();
+  return n;
+}
+
 // Level 1 (throughput shape, G groups: group g holds prod_g * R^(1 - c_g)) over `count` rows of X (or
 // rows d_ids[0..count)), unless the fold is small enough for the tree alone.
 int fold_level1(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
@@ -237,6 +247,17 @@ int fold_level1(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const ui
   const int S = mc.S, S2 = mc.S2;
   if (use_tree() && mc.tree_direct && count <= tree_direct_rows()) {
     *lv = Leaves{X, xstride, S, mc.W, count, 0, d_ids};
+    return DDS_OK;
+  }
+  // small folds: the first level in the latency shape S2 straight from the rows (one product per group)
+  if (!d_ids && S2 > S && S % 4 == 0 && fold_narrow_shape(S2) && count <= narrow_fold_rows()) {
+    const size_t G = std::max<size_t>(1, count / 2), ps = round_up(G, 64);
+    const bool rowmajor = use_tree() && G <= tree_switch_leaves();  // straight to the tree
+    HIP_TRY(w->p0.ensure((size_t)S2 * ps * 4));
+    HIP_TRY(launch_fold_narrow(S2, X, xstride, count, S, mc.d2, mc.dq, mc.n0, w->p0.as<uint32_t>(), rowmajor ? 1 : ps,
+                               G, st, rowmajor ? (size_t)S2 : 1));
+    *lv = Leaves{w->p0.as<uint32_t>(), rowmajor ? 1 : ps, S2, mc.W, G, mc.wS2() * ((int64_t)G - (int64_t)count),
+                 nullptr, rowmajor ? (size_t)S2 : 1};
     return DDS_OK;
   }
   // one bignum per lane for long folds of the narrow shapes (k_fold1), lane groups otherwise
@@ -312,17 +333,20 @@ int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const 
     return DDS_OK;
   }
   Leaves lt = lv;
-  if (lv.Sin == S2 && !lv.ids && lv.n > tree_switch_leaves()) {  // wide levels: tail-shape launches
+  if (lv.Sin == S2 && !lv.ids && lv.gs == 1 && lv.n > tree_switch_leaves()) {  // wide levels: tail-shape launches
     HIP_TRY(w->p1.ensure((size_t)S2 * round_up((lv.n + 1) / 2, 64) * 4));
     HIP_TRY(w->x2.ensure((size_t)S2 * round_up((lv.n + 1) / 2, 64) * 4));
     uint32_t* bufs[2] = {w->p1.as<uint32_t>(), w->x2.as<uint32_t>()};
     int flip = 0;
     while (lt.n > tree_switch_leaves()) {
       const size_t ng = (lt.n + 1) / 2, ns = round_up(ng, 64);
-      HIP_TRY(launch_fold_tail(S2, lt.X, lt.xs, lt.n, mc.d2, mc.dq, mc.n0, bufs[flip], ns, ng, st));
+      const bool rowmajor = ng <= tree_switch_leaves();  // the last lane-group level: the tree's leaf layout
+      HIP_TRY(launch_fold_tail(S2, lt.X, lt.xs, lt.n, mc.d2, mc.dq, mc.n0, bufs[flip], rowmajor ? 1 : ns, ng, st,
+                               rowmajor ? (size_t)S2 : 1));
       lt.E -= mc.wS2() * (int64_t)(lt.n - ng);  // n - ng products, R2^-1 each
       lt.X = bufs[flip];
-      lt.xs = ns;
+      lt.xs = rowmajor ? 1 : ns;
+      lt.gs = rowmajor ? (size_t)S2 : 1;
       lt.n = ng;
       flip ^= 1;
     }
@@ -348,14 +372,14 @@ int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const 
       dY = w->y.as<uint32_t>();
     }
   }
+  // finalize: the root block writes the result straight into the pinned stage (no copy launch after it)
   HIP_TRY(launch_tree(S3, lt.X, lt.xs, lt.Sin, lt.Win, lt.n, lt.ids, mc.d3, finalize ? dY : nullptr,
-                      nodes, tflags, w->out.as<uint32_t>(), S2, mc.W, st));
+                      nodes, tflags, finalize ? hy + S3 : w->out.as<uint32_t>(), S2, mc.W, st, lt.gs));
   if (!finalize) {
     *part = w->out.as<uint32_t>();
     *Eout = E;
     return DDS_OK;
   }
-  HIP_TRY(hipMemcpyAsync(hy + S3, w->out.p, (size_t)S3 * 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   account_fold(ctx, w);
   *value = bn::from_rw(hy + S3, S3, mc.W3);

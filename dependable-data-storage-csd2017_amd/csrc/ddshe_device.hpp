@@ -277,10 +277,13 @@ struct Mont {
       for (int q = 0; q < kPF; ++q) pre[d][q] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, q * sstride, 0);
     }
   }
+  // Narrow: X holds only its first `sin` limbs (sin a multiple of kPF, >= 2 kPF; a main-shape column
+  // read in a wider shape): blocks from sin on get an empty descriptor, so their loads return 0
+  template <bool Narrow = false>
   __device__ __forceinline__ static void mul_col_chain(uint32_t (&a)[L], const uint32_t (&n)[L],
                                                        const uint32_t* __restrict__ X, size_t stride, uint32_t row,
                                                        uint32_t next, uint32_t (&pre)[2][kPF], uint32_t n0,
-                                                       bool top, bool bottom) {
+                                                       bool top, bool bottom, int sin = S) {
     constexpr int PF = kPF;
     static_assert(S % PF == 0 && S >= 2 * PF, "S % PF");
     uint64_t t[L];
@@ -289,8 +292,8 @@ struct Mont {
     const uint32_t voff = row * 4u;
     const uint32_t sstride = (uint32_t)stride * 4u;
     auto block_rsrc = [&](int i) {
-      return __builtin_amdgcn_make_buffer_rsrc((void*)(X + (size_t)i * stride), (short)0, (int)(PF * sstride),
-                                               0x00020000);
+      const int bytes = (!Narrow || i < sin) ? (int)(PF * sstride) : 0;
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(X + (size_t)i * stride), (short)0, bytes, 0x00020000);
     };
     uint32_t bq[PF], bm[PF];
 #pragma unroll

@@ -30,6 +30,12 @@ struct Grp {
 #pragma unroll
     for (int l = 0; l < L; ++l) a[l] = col[(size_t)(r * L + l) * stride + row];
   }
+  // the column holds only its first `sin` limbs (the rest read as 0)
+  __device__ __forceinline__ void load_col_narrow(uint32_t (&a)[L], const uint32_t* __restrict__ col, size_t stride,
+                                                  size_t row, int sin) const {
+#pragma unroll
+    for (int l = 0; l < L; ++l) a[l] = r * L + l < sin ? col[(size_t)(r * L + l) * stride + row] : 0u;
+  }
   __device__ __forceinline__ void store_col(const uint32_t (&a)[L], uint32_t* __restrict__ col, size_t stride,
                                             size_t row) const {
 #pragma unroll
@@ -87,11 +93,16 @@ struct Grp {
 // Idx: the fold runs over the rows ids[0..count) of X instead of rows [0, count) (row-subset folds:
 // the rows that pass a route's guard / dedup, DDSRestServer.scala:401-415). Sorted ids keep the
 // lanes of a wave on nearby rows, so the limb loads stay mostly coalesced.
-template <int S, int TPI, int W, bool QP = false, bool Idx = false>
+// Narrow: X is a column of a narrower shape holding `sin` limbs per row (small folds run their first
+// level in the latency shape straight from the main-shape rows; the missing top limbs read as 0).
+// Partial g goes to P[l * pstride + g * pgs] (limb-major by default; row-major for a launch that hands
+// its partials to the reduction tree, whose blocks then read each leaf as one contiguous run).
+template <int S, int TPI, int W, bool QP = false, bool Idx = false, bool Narrow = false>
 __global__ void __launch_bounds__(256, 2) k_fold(const uint32_t* __restrict__ X, size_t xstride, size_t count,
                                               const uint32_t* __restrict__ consts, uint32_t n0,
                                               uint32_t* __restrict__ P, size_t pstride, size_t ngroups,
-                                              const uint32_t* __restrict__ ids = nullptr) {
+                                              const uint32_t* __restrict__ ids = nullptr, int sin = S,
+                                              size_t pgs = 1) {
   using G = Grp<S, TPI, W>;
   using M = Mont<S, TPI, W, QP>;
   constexpr int L = G::L;
@@ -101,19 +112,22 @@ __global__ void __launch_bounds__(256, 2) k_fold(const uint32_t* __restrict__ X,
   auto rowat = [&](size_t pos) -> uint32_t { return Idx ? ids[pos] : (uint32_t)pos; };
   uint32_t n[L], a[L];
   g.load_vec(n, consts + kConstN * S);
-  g.load_col(a, X, xstride, rowat(grp));
+  if constexpr (Narrow)
+    g.load_col_narrow(a, X, xstride, rowat(grp), sin);
+  else
+    g.load_col(a, X, xstride, rowat(grp));
   if (grp + ngroups < count) {
     uint32_t pre[2][M::kPF];  // first limb blocks of the next row, requested one row ahead
     uint32_t row = rowat(grp + ngroups);
     M::load_blocks2(pre, X, xstride, row);
     for (size_t pos = grp + ngroups; pos < count; pos += ngroups) {
       const uint32_t nxt = pos + ngroups < count ? rowat(pos + ngroups) : row;  // last row: a harmless re-read
-      M::mul_col_chain(a, n, X, xstride, row, nxt, pre, n0, g.top, g.bottom);
+      M::template mul_col_chain<Narrow>(a, n, X, xstride, row, nxt, pre, n0, g.top, g.bottom, sin);
       row = nxt;
     }
   }
   M::normalize(a, g.bottom);
-  g.store_col(a, P, pstride, grp);
+  g.store_col(a, P, pstride, grp * pgs);  // pstride = 1, pgs = S: row-major partials (the tree's leaves)
 }
 
 // ------------------------------------------------------------------------------

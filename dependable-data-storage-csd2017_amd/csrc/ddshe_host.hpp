@@ -468,8 +468,9 @@ int fold_even_modulus(dds_ctx* ctx, const bn::Limbs& M, const std::vector<bn::Li
 void record_time(dds_ctx* ctx, Worker* w, hipStream_t st, bool begin, int slot);
 int pick_tpi(int S);
 size_t max_fold_groups(dds_ctx* ctx, int S);
-// Leaves of the reduction tree: X[l * xs + g] (g = ids[k] when ids), l < Sin limbs of Win bits, holding
-// prod * 2^E over n leaves
+// Leaves of the reduction tree: X[l * xs + g * gs] (g = ids[k] when ids), l < Sin limbs of Win bits,
+// holding prod * 2^E over n leaves (gs = 1: limb-major, as lane-group launches read them; xs = 1,
+// gs = Sin: row-major, written by the launch that hands its partials to the tree)
 struct Leaves {
   const uint32_t* X;
   size_t xs;
@@ -477,6 +478,7 @@ struct Leaves {
   size_t n;
   int64_t E;
   const uint32_t* ids;
+  size_t gs = 1;
 };
 int fold_level1(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
                 size_t count, const uint32_t* d_ids, Leaves* lv);

@@ -1102,43 +1102,81 @@ static int tail80_tpi(int S, size_t ngroups) {
   return ngroups >= 32768 ? 4 : ngroups >= 16384 ? 8 : 0;
 }
 
+// First fold level of a small fold in the latency shape S2, straight from a main-shape column holding
+// `sin` limbs per row (k_fold<..., Narrow>): one launch of wide lane groups instead of a main-shape level
+// with one or two rows per group (long per-product latency at 2-4 lanes) plus the zeroing of the
+// partials' extra limbs. TPI by the number of groups, as the tail levels choose it.
+bool fold_narrow_shape(int S2) { return S2 == 48 || S2 == 80 || S2 == 160; }
+hipError_t launch_fold_narrow(int S2, const uint32_t* X, size_t xstride, size_t count, int sin, const uint32_t* consts,
+                              const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups,
+                              hipStream_t st, size_t pgs) {
+  if (ngroups == 0 || ngroups > count || !fold_narrow_shape(S2) || sin < 8 || sin % 4 || sin > S2)
+    return hipErrorInvalidValue;
+#define DDSHE_NARROW(S_, TPI_, QP_, C_)                                                                        \
+  hipLaunchKernelGGL((k_fold<S_, TPI_, 28, QP_, false, true>), dim3(grid_for(ngroups * TPI_)), dim3(256), 0, st, X, \
+                     xstride, count, C_, n0, P, pstride, ngroups, nullptr, sin, pgs)
+  if (S2 == 48) {
+    DDSHE_NARROW(48, 16, false, consts);
+  } else if (S2 == 80) {
+    if (ngroups >= 32768)
+      DDSHE_NARROW(80, 4, false, consts);
+    else if (ngroups >= 16384)
+      DDSHE_NARROW(80, 8, false, consts);
+    else
+      DDSHE_NARROW(80, 16, false, consts);
+  } else {
+    const int tpi = ngroups >= kTail8MinGroups ? 8 : ngroups <= kTail32MaxGroups ? 32 : 16;
+    if (qp_mod) {
+      if (tpi == 8) DDSHE_NARROW(160, 8, true, qp_mod);
+      else if (tpi == 32) DDSHE_NARROW(160, 32, true, qp_mod);
+      else DDSHE_NARROW(160, 16, true, qp_mod);
+    } else {
+      if (tpi == 8) DDSHE_NARROW(160, 8, false, consts);
+      else if (tpi == 32) DDSHE_NARROW(160, 32, false, consts);
+      else DDSHE_NARROW(160, 16, false, consts);
+    }
+  }
+#undef DDSHE_NARROW
+  return hipGetLastError();
+}
+
 hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
                             const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups,
-                            hipStream_t st) {
+                            hipStream_t st, size_t pgs) {
   if (ngroups == 0 || ngroups > count) return hipErrorInvalidValue;
   if (const int t80 = tail80_tpi(S, ngroups)) {  // S = 80 has no QP modulus (tail_qp)
     if (t80 == 4)
       hipLaunchKernelGGL((k_fold<80, 4, 28>), dim3(grid_for(ngroups * 4)), dim3(256), 0, st, X, xstride, count, consts,
-                         n0, P, pstride, ngroups);
+                         n0, P, pstride, ngroups, nullptr, 80, pgs);
     else
       hipLaunchKernelGGL((k_fold<80, 8, 28>), dim3(grid_for(ngroups * 8)), dim3(256), 0, st, X, xstride, count, consts,
-                         n0, P, pstride, ngroups);
+                         n0, P, pstride, ngroups, nullptr, 80, pgs);
     return hipGetLastError();
   }
   if (use_tail8(S, ngroups)) {
     if (qp_mod)
       hipLaunchKernelGGL((k_fold<160, 8, 28, true>), dim3(grid_for(ngroups * 8)), dim3(256), 0, st, X, xstride, count,
-                         qp_mod, n0, P, pstride, ngroups);
+                         qp_mod, n0, P, pstride, ngroups, nullptr, 160, pgs);
     else
       hipLaunchKernelGGL((k_fold<160, 8, 28>), dim3(grid_for(ngroups * 8)), dim3(256), 0, st, X, xstride, count,
-                         consts, n0, P, pstride, ngroups);
+                         consts, n0, P, pstride, ngroups, nullptr, 160, pgs);
     return hipGetLastError();
   }
   if (use_tail32(S, ngroups)) {
     if (qp_mod)  // N~ = N·n0 in place of N (Mont QP): the quotient needs no multiply
       hipLaunchKernelGGL((k_fold<160, 32, 28, true>), dim3(grid_for(ngroups * 32)), dim3(256), 0, st, X, xstride,
-                         count, qp_mod, n0, P, pstride, ngroups);
+                         count, qp_mod, n0, P, pstride, ngroups, nullptr, 160, pgs);
     else
       hipLaunchKernelGGL((k_fold<160, 32, 28>), dim3(grid_for(ngroups * 32)), dim3(256), 0, st, X, xstride, count,
-                         consts, n0, P, pstride, ngroups);
+                         consts, n0, P, pstride, ngroups, nullptr, 160, pgs);
     return hipGetLastError();
   }
   if (qp_mod) {
     DDSHE_TAIL_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W, true>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st,
-                                            X, xstride, count, qp_mod, n0, P, pstride, ngroups));
+                                            X, xstride, count, qp_mod, n0, P, pstride, ngroups, nullptr, S, pgs));
   } else {
     DDSHE_TAIL_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X,
-                                            xstride, count, consts, n0, P, pstride, ngroups));
+                                            xstride, count, consts, n0, P, pstride, ngroups, nullptr, S, pgs));
   }
   return hipGetLastError();
 }

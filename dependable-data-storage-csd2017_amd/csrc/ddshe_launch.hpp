@@ -53,9 +53,13 @@ size_t fold1_min_rows(int S, int cus);
 hipError_t fold1_occupancy(int S, int* blocks_per_cu);
 // tree levels / finalize in the tail shape (S = tail limb count, consts of the tail shape)
 // qp_mod (nullable): N~ = N·n0 in tail limbs, used by the latency-bound levels when tail_qp(S)
+bool fold_narrow_shape(int S2);
+hipError_t launch_fold_narrow(int S2, const uint32_t* X, size_t xstride, size_t count, int sin, const uint32_t* consts,
+                              const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups,
+                              hipStream_t st, size_t pgs = 1);
 hipError_t launch_fold_tail(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
                             const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups,
-                            hipStream_t st);
+                            hipStream_t st, size_t pgs = 1);
 bool tail_qp(int S);
 // Reduction tree (ddshe_tree.hip): S limbs of W bits (Shape.TPI unused) for a main shape of up to
 // mod_bits bits; one launch reduces nleaves leaves (limb-major X, Sin limbs of Win bits, stride xstride;
@@ -65,7 +69,7 @@ bool tail_qp(int S);
 Shape tree_shape(size_t mod_bits);
 hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Win, size_t nleaves, const uint32_t* ids,
                        const uint32_t* consts, const uint32_t* Y, uint32_t* nodes, uint32_t* flags, uint32_t* out,
-                       int Sout, int Wout, hipStream_t st);
+                       int Sout, int Wout, hipStream_t st, size_t gstride = 1);
 // out[i] = A[i] * B[i] mod N in the tree shape (S limbs of W bits, row-major, operands < N, canonical
 // results): one workgroup per pair (k_pairs_sos). consts as launch_tree, R2 = R^2 mod N (R = 2^(W S)).
 hipError_t launch_pairs_sos(int S, const uint32_t* A, const uint32_t* B, size_t n, const uint32_t* consts,

@@ -525,7 +525,7 @@ hipError_t launch_pairs_sos(int S, const uint32_t* A, const uint32_t* B, size_t 
 
 hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Win, size_t nleaves, const uint32_t* ids,
                        const uint32_t* consts, const uint32_t* Y, uint32_t* nodes, uint32_t* flags, uint32_t* out,
-                       int Sout, int Wout, hipStream_t st) {
+                       int Sout, int Wout, hipStream_t st, size_t gstride) {
   static const int levels = tree_env("DDSHE_TREE_LEVELS", 1), fence = tree_env("DDSHE_TREE_FENCE", 1);
   static uint64_t* d_st = nullptr;
   static const bool stamping = getenv("DDSHE_TREE_STAMPS") && hipMalloc(&d_st, 2 * kStamps * 8) == hipSuccess;
@@ -535,7 +535,6 @@ hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Wi
   if (levels != 1 && fence == 1) return hipErrorInvalidValue;
   // level buffers for multi-launch trees live after the nodes: two ping-pong halves of nleaves rows
   uint32_t* lvl[2] = {nodes + (2 * nleaves + 2) * (size_t)S, nodes + (3 * nleaves + 2) * (size_t)S};
-  size_t gstride = 1;
   int flip = 0;
   for (;;) {
     const bool last = levels <= 0 || nleaves <= ((size_t)1 << levels);
