@@ -19,6 +19,7 @@
 // rides in bit 31 of its id (no random gather of valid[] in the last pass).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "ddshe_launch.hpp"
 
@@ -74,11 +75,19 @@ __global__ void __launch_bounds__(256) k_rs_prep(const int64_t* __restrict__ col
                                                  size_t n, int desc, uint64_t* __restrict__ part) {
   uint64_t lo = ~0ull, hi = 0;
   const size_t base = (size_t)blockIdx.x * 256 * kRsPrepRows + threadIdx.x;
-#pragma unroll 4
+  // all loads first (unconditional, index clamped: no load waits on a valid byte), then the min/max
+  int64_t raw[kRsPrepRows];
+  uint8_t hold[kRsPrepRows];
+#pragma unroll
   for (int k = 0; k < kRsPrepRows; ++k) {
-    const size_t i = base + (size_t)k * 256;
-    if (i < n && (!valid || valid[i])) {
-      const uint64_t key = rs_ukey((uint64_t)col[i], desc);
+    const size_t i = min(base + (size_t)k * 256, n - 1);
+    raw[k] = col[i];
+    hold[k] = valid ? valid[i] : 1;
+  }
+#pragma unroll
+  for (int k = 0; k < kRsPrepRows; ++k) {
+    if (base + (size_t)k * 256 < n && hold[k]) {
+      const uint64_t key = rs_ukey((uint64_t)raw[k], desc);
       lo = min(lo, key);
       hi = max(hi, key);
     }
@@ -112,9 +121,9 @@ __device__ __forceinline__ uint32_t rs_load_id(const uint32_t* __restrict__ ids,
   return (uint32_t)i | ((vbit && valid && !valid[i]) ? kRsLack : 0u);
 }
 
-__device__ __forceinline__ uint32_t rs_digit(uint64_t k, uint32_t id, const uint8_t* __restrict__ valid, int pass,
+__device__ __forceinline__ uint32_t rs_digit(uint64_t k, uint32_t id, const uint8_t* __restrict__ valid, int shift,
                                              bool last, int desc, bool vbit) {
-  uint32_t d = (uint32_t)(k >> (8 * pass)) & 0xFFu;
+  uint32_t d = (uint32_t)(k >> shift) & 0xFFu;
   if (last && valid) {
     const bool v = vbit ? (id & kRsLack) == 0 : valid[id] != 0;
     d = desc ? (v ? d : 256u) : (v ? d + 1u : 0u);
@@ -129,7 +138,7 @@ __device__ __forceinline__ size_t rs_row(size_t tile, int wid, int k, int lane) 
 
 __global__ void __launch_bounds__(kRsBlock) k_rs_hist(const uint64_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ ids,
-                                                      const uint8_t* __restrict__ valid, size_t n, int pass,
+                                                      const uint8_t* __restrict__ valid, size_t n, int shift,
                                                       bool last, int desc, bool vbit, uint64_t kmin,
                                                       uint32_t* __restrict__ hist, size_t nblocks) {
   __shared__ uint32_t cnt[kRsDigits];
@@ -150,7 +159,7 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_hist(const uint64_t* __restrict
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
     const size_t i = rs_row(blockIdx.x, wid, k, lane);
-    const uint32_t d = i < n ? rs_digit(key[k], id[k], valid, pass, last, desc, vbit) : kRsNone;
+    const uint32_t d = i < n ? rs_digit(key[k], id[k], valid, shift, last, desc, vbit) : kRsNone;
     // one LDS atomic per distinct digit of the wave (OPE columns repeat digits a lot; measured
     // faster than per-wave histograms with one atomic per row)
     uint64_t peers = ~0ull;
@@ -216,12 +225,13 @@ __global__ void __launch_bounds__(256) k_rs_scan_digits(uint32_t* __restrict__ h
 // (runs average kRsTile/256 = 16 rows), instead of 64 different buckets per store.
 __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ ids,
-                                                         const uint8_t* __restrict__ valid, size_t n, int pass,
+                                                         const uint8_t* __restrict__ valid, size_t n, int shift,
                                                          int desc, bool vbit, bool last, uint64_t kmin,
                                                          const uint32_t* __restrict__ hist,
                                                          const uint32_t* __restrict__ dtot, size_t nblocks,
                                                          uint64_t* __restrict__ keys_out,
-                                                         uint32_t* __restrict__ ids_out) {
+                                                         uint32_t* __restrict__ ids_out,
+                                                         uint32_t* __restrict__ ids_copy) {
   __shared__ uint32_t cnt[kRsWaves][kRsDigits];
   __shared__ uint32_t dbase[kRsDigits + 1];   // global start of digit d, then of this tile's run of d
   __shared__ uint32_t lstart[kRsDigits + 1];  // tile-local start of digit d
@@ -266,7 +276,7 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
     const size_t i = rs_row(blockIdx.x, wid, k, lane);
-    dr[k] = i < n ? rs_digit(key[k], id[k], valid, pass, last, desc, vbit) : kRsNone;
+    dr[k] = i < n ? rs_digit(key[k], id[k], valid, shift, last, desc, vbit) : kRsNone;
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
@@ -317,14 +327,291 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
     const uint32_t dst = dbase[d] + (q - lstart[d]);
     if (keys_out) keys_out[dst] = skey[q];
     ids_out[dst] = sid[q];
+    if (ids_copy) ids_copy[dst] = sid[q];  // MSD split: side copy the in-bucket sort reads
+  }
+}
+
+// ---- MSD split + in-bucket sort (OPE columns whose key span needs > 3 LSD passes) ----------------
+// Two stable LSD passes over the TOP 16 bits of the span group the rows by those bits (65,536
+// buckets), each bucket in input order. Each bucket with two distinct keys is then put in its final
+// order, one wave per bucket (k_msd_local):
+//   * stable partition by distinct key: round r writes, in input order, the rows whose key is the
+//     r-th smallest of the bucket (ballot compaction) and finds the next smallest; a bucket of one key
+//     is a single copy round. OPE columns repeat values (the generator's plaintexts are < 10^4), so
+//     their buckets hold a few distinct keys however many rows they have.
+//   * when a bucket needs more rounds (2 for <= 512 rows, 16 above): a bitonic network over the packed
+//     value (rest of the key << pos bits | position in the bucket), unique, so the unstable network
+//     yields the stable order: one wave in registers up to 512 rows (<= 8 per lane), one 1024-thread
+//     workgroup up to 8192 rows (k_msd_big, 8 per thread, partners in other waves through LDS);
+//   * a bucket of > 8192 rows with > 16 distinct keys raises a flag and the host redoes the sort with
+//     the LSD passes (never seen on OPE data: it needs > 16 distinct keys among > 8192 rows whose
+//     keys agree on the top 16 bits of the span).
+// The last top pass writes each id to its final place if its bucket holds one key (OPE columns:
+// most buckets), plus a side copy (src) the in-bucket step reads, so nothing is sorted in place.
+// Bucket bounds come from one pass over the sorted keys (k_msd_bounds: the first and the last row of
+// every non-empty bucket and whether it holds two distinct keys); only those buckets are touched.
+// Per row: 2 LSD passes (+ 4 B for the side copy) + 8 B of bounds read, and for rows of multi-key
+// buckets (8 B key + 4 B id read, 4 B id written) per partition round or sort, against
+// ceil(bits(span) / 8) LSD passes (7 for a 2^54 span).
+constexpr int kMsdBits = 16;
+constexpr uint32_t kMsdBuckets = 1u << kMsdBits;
+constexpr uint32_t kMsdWaveMax = 512;
+constexpr uint32_t kMsdBlockMax = 8192;
+constexpr int kMsdBigBlocks = 512;  // grid of the block path (grid-stride over the big buckets)
+enum { kMsdCtlBig = 0, kMsdCtlOverflow = 1 };
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Ascending bitonic sort of G*E values, element e = t*E + r held by thread t in v[r]. Partners at
+// distance j < E are in the same thread, E <= j < 64E in the same wave (lane xor j/E), j >= 64E in
+// another wave: exchanged through xch (r-major, G*E slots; only when G > 64).
+template <int E, int LOGP, int G>
+__device__ __forceinline__ void bitonic(uint64_t (&v)[E], int t, uint64_t* xch) {
+#pragma unroll
+  for (int kk = 1; kk <= LOGP; ++kk) {
+#pragma unroll
+    for (int jj = kk - 1; jj >= 0; --jj) {
+      const int k = 1 << kk, j = 1 << jj;
+      if (j < E) {
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          if ((r & j) == 0) {
+            const bool up = ((t * E + r) & k) == 0;
+            const uint64_t a = v[r], b = v[r | j];
+            const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+            v[r] = up ? lo : hi;
+            v[r | j] = up ? hi : lo;
+          }
+        }
+      } else {
+        uint64_t p[E];
+        if (j < 64 * E) {
+#pragma unroll
+          for (int r = 0; r < E; ++r) p[r] = shfl_xor_u64(v[r], j / E);
+        } else {
+          __syncthreads();  // the previous exchange's reads are done
+#pragma unroll
+          for (int r = 0; r < E; ++r) xch[r * G + t] = v[r];
+          __syncthreads();
+#pragma unroll
+          for (int r = 0; r < E; ++r) p[r] = xch[r * G + (t ^ (j / E))];
+        }
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          const int e = t * E + r;
+          const bool take_min = ((e & j) == 0) == ((e & k) == 0);
+          const uint64_t a = v[r], b = p[r];
+          v[r] = take_min ? (a < b ? a : b) : (a < b ? b : a);
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t msd_bucket_of(uint64_t key, int s1) { return (uint32_t)(key >> s1); }
+
+// Holder range of the sorted rows: the last (validity) pass put the rows lacking the position in
+// bucket 256 (descending: at the end) or 0 (ascending: in front).
+__device__ __forceinline__ void msd_holders(const uint32_t* __restrict__ dtot, size_t n, int desc, bool has_valid,
+                                            size_t* h0, size_t* h1) {
+  *h0 = 0;
+  *h1 = n;
+  if (has_valid) {
+    if (desc) *h1 = n - dtot[256];
+    else *h0 = dtot[0];
+  }
+}
+
+// first[b] / end[b]: first row / one past the last row of non-empty bucket b (read only where multi[b]);
+// multi[b] = 1 when bucket b holds two distinct keys (preset to 0). Neighbouring keys come from the
+// adjacent lanes; 4 rows per thread (loads in flight together); block 0 also clears the control words.
+constexpr int kMsdBoundsRows = 4;
+__global__ void __launch_bounds__(256) k_msd_bounds(const uint64_t* __restrict__ keys, size_t n, int s1,
+                                                    const uint32_t* __restrict__ dtot, int desc, bool has_valid,
+                                                    uint32_t* __restrict__ first, uint32_t* __restrict__ end,
+                                                    uint32_t* __restrict__ multi, uint32_t* __restrict__ ctl) {
+  if (blockIdx.x == 0 && threadIdx.x < 8) ctl[threadIdx.x] = 0;
+  size_t h0, h1;
+  msd_holders(dtot, n, desc, has_valid, &h0, &h1);
+  const int lane = threadIdx.x & 63;
+  const size_t base = h0 + (size_t)blockIdx.x * 256 * kMsdBoundsRows + threadIdx.x;
+  uint64_t k[kMsdBoundsRows];
+#pragma unroll
+  for (int r = 0; r < kMsdBoundsRows; ++r) k[r] = keys[min(base + (size_t)r * 256, h1 - 1)];
+#pragma unroll
+  for (int r = 0; r < kMsdBoundsRows; ++r) {
+    const size_t i = base + (size_t)r * 256;
+    const bool in = i < h1;
+    uint64_t kp = (uint64_t)__shfl_up((long long)k[r], 1), kn = (uint64_t)__shfl_down((long long)k[r], 1);
+    if (!in) continue;
+    if (lane == 0 && i > h0) kp = keys[i - 1];
+    if (lane == 63 && i + 1 < h1) kn = keys[i + 1];
+    const uint32_t b = msd_bucket_of(k[r], s1);
+    const bool head = i == h0 || msd_bucket_of(kp, s1) != b;
+    if (head) first[b] = (uint32_t)i;
+    else if (kp != k[r]) multi[b] = 1u;
+    if (i == h1 - 1 || msd_bucket_of(kn, s1) != b) end[b] = (uint32_t)(i + 1);
+  }
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint64_t o = shfl_xor_u64(v, off);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// Stable partition of bucket [lo, lo + m) by distinct key, at most max_rounds rounds; returns whether
+// every row was written. Round: 8 chunks of 64 rows in flight, the rows whose key is cur compacted by
+// ballot, the next larger key found on the way. The first round takes cur = the bucket's first key
+// (a one-key bucket is then a single copy); a smaller key seen in it restarts from the smallest.
+__device__ __forceinline__ bool msd_wave_partition(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ src,
+                                                   uint32_t* __restrict__ ids, uint32_t lo, uint32_t m, int lane,
+                                                   int max_rounds) {
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint64_t cur = keys[lo];
+  uint32_t out = lo;
+  bool restarted = false;
+  for (int round = 0; round < max_rounds; ++round) {
+    uint64_t nxt = ~0ull, below = ~0ull;
+    for (uint32_t p0 = 0; p0 < m; p0 += 512) {
+      uint64_t k[8];
+      uint32_t id[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const uint32_t pos = min(p0 + (uint32_t)(r * 64 + lane), m - 1);
+        k[r] = keys[lo + pos];
+        id[r] = src[lo + pos];
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const bool in = p0 + (uint32_t)(r * 64) + lane < m;
+        const bool hit = in && k[r] == cur;
+        const uint64_t bal = __ballot(hit);
+        if (hit) ids[out + __popcll(bal & lt)] = id[r];
+        out += (uint32_t)__popcll(bal);
+        if (in && k[r] > cur && k[r] < nxt) nxt = k[r];
+        if (in && k[r] < below) below = k[r];
+      }
+    }
+    if (!restarted) {
+      restarted = true;
+      below = wave_min_u64(below);
+      if (below < cur) {  // the first key was not the smallest: start over from the smallest
+        cur = below;
+        out = lo;
+        continue;
+      }
+    }
+    if (out == lo + m) return true;
+    cur = wave_min_u64(nxt);
+  }
+  return false;
+}
+
+// one wave sorts a bucket of m <= 64E rows by bitonic network (input positions r*64 + lane: coalesced)
+template <int E, int LOGP>
+__device__ __forceinline__ void msd_wave_sort(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ src,
+                                              uint32_t* __restrict__ ids, uint32_t lo, uint32_t m, uint64_t rmask,
+                                              int lane) {
+  uint64_t v[E];
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const uint32_t pos = (uint32_t)r * 64 + lane;
+    v[r] = pos < m ? ((keys[lo + pos] & rmask) << 10) | pos : ~0ull;
+  }
+  bitonic<E, LOGP, 64>(v, lane, nullptr);
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const uint32_t e = (uint32_t)lane * E + r;
+    if (e < m) ids[lo + e] = src[lo + (uint32_t)(v[r] & 1023u)];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_msd_local(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ src,
+                                                   uint32_t* __restrict__ ids, const uint32_t* __restrict__ first,
+                                                   const uint32_t* __restrict__ end,
+                                                   const uint32_t* __restrict__ multi, int s1,
+                                                   uint32_t* __restrict__ ctl, uint32_t* __restrict__ big) {
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (!multi[b]) return;  // empty, or one key: the last pass already put its rows in their place
+  const uint32_t lo = first[b], m = end[b] - lo;
+  if (msd_wave_partition(keys, src, ids, lo, m, lane, m <= kMsdWaveMax ? 2 : 16)) return;
+  if (m > kMsdWaveMax) {
+    if (lane == 0) big[atomicAdd(&ctl[kMsdCtlBig], 1u)] = b;
+    return;
+  }
+  const uint64_t rmask = (1ull << s1) - 1ull;
+  if (m <= 64) msd_wave_sort<1, 6>(keys, src, ids, lo, m, rmask, lane);
+  else if (m <= 128) msd_wave_sort<2, 7>(keys, src, ids, lo, m, rmask, lane);
+  else if (m <= 256) msd_wave_sort<4, 8>(keys, src, ids, lo, m, rmask, lane);
+  else msd_wave_sort<8, 9>(keys, src, ids, lo, m, rmask, lane);
+}
+
+template <int E, int LOGP>
+__device__ __forceinline__ void msd_block_sort(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ src,
+                                               uint32_t* __restrict__ ids, uint32_t lo, uint32_t m, uint64_t rmask,
+                                               uint64_t* xch) {
+  const int t = threadIdx.x;
+  uint64_t v[E];
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const uint32_t pos = (uint32_t)r * 1024 + t;
+    v[r] = pos < m ? ((keys[lo + pos] & rmask) << 13) | pos : ~0ull;
+  }
+  bitonic<E, LOGP, 1024>(v, t, xch);
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const uint32_t e = (uint32_t)t * E + r;
+    if (e < m) ids[lo + e] = src[lo + (uint32_t)(v[r] & 8191u)];
+  }
+}
+
+// buckets of 513..8192 rows with more distinct keys than k_msd_local's partition rounds: one
+// workgroup each (grid-stride over the list); larger ones: overflow flag (host falls back to LSD)
+__global__ void __launch_bounds__(1024) k_msd_big(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ src,
+                                                  uint32_t* __restrict__ ids, const uint32_t* __restrict__ first,
+                                                  const uint32_t* __restrict__ end, int s1, uint32_t* __restrict__ ctl,
+                                                  const uint32_t* __restrict__ big) {
+  __shared__ uint64_t xch[kMsdBlockMax];
+  const uint32_t nbig = ctl[kMsdCtlBig];
+  const uint64_t rmask = (1ull << s1) - 1ull;
+  for (uint32_t q = blockIdx.x; q < nbig; q += gridDim.x) {
+    const uint32_t b = big[q];
+    const uint32_t lo = first[b], m = end[b] - lo;
+    if (m > kMsdBlockMax) {
+      if (threadIdx.x == 0) atomicOr(&ctl[kMsdCtlOverflow], 1u);
+      continue;
+    }
+    if (m <= 2048) msd_block_sort<2, 11>(keys, src, ids, lo, m, rmask, xch);
+    else if (m <= 4096) msd_block_sort<4, 12>(keys, src, ids, lo, m, rmask, xch);
+    else msd_block_sort<8, 13>(keys, src, ids, lo, m, rmask, xch);
+    __syncthreads();  // xch is free for the next bucket
   }
 }
 
 size_t rs_blocks(size_t n) { return (n + kRsTile - 1) / kRsTile; }
 size_t rs_scratch_bytes(size_t n) {
-  // keys x2 (8 B), ids x1 extra (4 B; the other id buffer is the caller's output), histogram, OR/AND
+  // keys x2 (8 B), ids x1 extra (4 B; the other id buffer is the caller's output), histogram, OR/AND,
+  // MSD bucket starts + control words + big-bucket list
   return 2 * n * 8 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 1024 +
-         16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows));
+         16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows)) + 768 + (4 * (size_t)kMsdBuckets + 8) * 4 +
+         n * 4;  // + the side copy of the grouped ids
+}
+
+// the MSD path pays off from 4 LSD passes on (a span of > 24 bits) and enough rows to fill the buckets
+static bool msd_enabled(size_t n, int sb) {
+  static const int mode = [] {
+    const char* s = getenv("DDSHE_ORDER_MSD");  // 0: LSD passes only (A/B)
+    return s ? atoi(s) : 1;
+  }();
+  return mode != 0 && n >= ((size_t)1 << 16) && sb > 24;
 }
 
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
@@ -339,6 +626,12 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   uint64_t* red = (uint64_t*)(((uintptr_t)(dtot + kRsDigits) + 15) & ~(uintptr_t)15);
   uint64_t* part = red + 2;
   const size_t pb = (n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows);
+  uint32_t* mfirst = (uint32_t*)(((uintptr_t)(part + 2 * pb) + 255) & ~(uintptr_t)255);
+  uint32_t* mmulti = mfirst + kMsdBuckets;
+  uint32_t* mend = mmulti + kMsdBuckets;
+  uint32_t* mctl = mend + kMsdBuckets;
+  uint32_t* mbig = mctl + 8;
+  uint32_t* msrc = (uint32_t*)(((uintptr_t)(mbig + kMsdBuckets) + 255) & ~(uintptr_t)255);
   hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
   hipLaunchKernelGGL(k_rs_red, dim3(1), dim3(1024), 0, st, part, pb, red);
   uint64_t hred[2];
@@ -348,31 +641,56 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   // the bytes of max - min (at least one pass when rows may lack the position: its last pass buckets them)
   const uint64_t kmin = hred[0] <= hred[1] ? hred[0] : 0ull;
   const uint64_t span = hred[0] <= hred[1] ? hred[1] - hred[0] : 0ull;
-  int passes[8], np = 0;
-  for (int p = 0; p < 8 && (span >> (8 * p)) != 0; ++p) passes[np++] = p;
-  if (np == 0 && valid) passes[np++] = 0;
+  const int sb = span ? 64 - __builtin_clzll(span) : 0;  // bits of the span
+  const bool vbit = valid && n <= (size_t)kRsLack;
+  // executed pass j writes ids to fin when (np-1-j) is even, so the last one lands there
+  auto run_passes = [&](const int* shifts, int np, bool keep_keys, uint32_t* fin, uint32_t* tmp,
+                        uint32_t* copy) -> const uint64_t* {
+    const uint32_t* ids_in = nullptr;  // identity before the first pass
+    const uint64_t* kin = (const uint64_t*)col;  // raw column before the first pass
+    uint64_t* kout = ka;
+    for (int j = 0; j < np; ++j) {
+      uint32_t* ids_out = ((np - 1 - j) % 2 == 0) ? fin : tmp;
+      const bool last = j == np - 1;
+      hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)nb), dim3(kRsBlock), 0, st, kin, ids_in, valid, n, shifts[j], last,
+                         desc, vbit, kmin, hist, nb);
+      hipLaunchKernelGGL(k_rs_scan_digits, dim3(kRsDigits), dim3(256), 0, st, hist, nb, dtot);
+      hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)nb), dim3(kRsBlock), 0, st, kin, ids_in, valid, n, shifts[j],
+                         desc, vbit, last, kmin, hist, dtot, nb, (last && !keep_keys) ? nullptr : kout, ids_out,
+                         last ? copy : nullptr);
+      kin = kout;
+      kout = kout == ka ? kb : ka;
+      ids_in = ids_out;
+    }
+    return kin;
+  };
+  if (msd_enabled(n, sb)) {
+    const int s1 = sb - kMsdBits;
+    const int shifts[2] = {s1, sb - 8};
+    // grouped ids -> out_ids (one-key buckets are final there) and the side copy msrc
+    const uint64_t* sorted = run_passes(shifts, 2, true, out_ids, ib, msrc);
+    if ((e = hipMemsetAsync(mmulti, 0, kMsdBuckets * 4, st)) != hipSuccess) return e;
+    const size_t nbd = (n + 256 * kMsdBoundsRows - 1) / (256 * kMsdBoundsRows);  // over <= n holder rows
+    hipLaunchKernelGGL(k_msd_bounds, dim3((unsigned)nbd), dim3(256), 0, st, sorted, n, s1, dtot, desc, valid != nullptr,
+                       mfirst, mend, mmulti, mctl);
+    hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / 4), dim3(256), 0, st, sorted, msrc, out_ids, mfirst, mend, mmulti,
+                       s1, mctl, mbig);
+    hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, sorted, msrc, out_ids, mfirst, mend, s1, mctl,
+                       mbig);
+    uint32_t hctl[2];
+    if ((e = hipMemcpyAsync(hctl, mctl, sizeof(hctl), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    if (!hctl[kMsdCtlOverflow]) return hipGetLastError();
+    // a bucket of > 8192 rows with > 16 distinct keys: redo the whole sort with the LSD passes
+  }
+  int shifts[8], np = 0;
+  for (int p = 0; p < 8 && (span >> (8 * p)) != 0; ++p) shifts[np++] = 8 * p;
+  if (np == 0 && valid) shifts[np++] = 0;
   if (np == 0) {
     hipLaunchKernelGGL(k_rs_iota, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out_ids, n);
     return hipGetLastError();
   }
-  // executed pass j writes ids to out_ids when (np-1-j) is even, so the last one lands there
-  const uint32_t* ids_in = nullptr;  // identity before the first pass
-  const uint64_t* kin = (const uint64_t*)col;  // raw column before the first pass
-  uint64_t* kout = ka;
-  for (int j = 0; j < np; ++j) {
-    const int pass = passes[j];
-    uint32_t* ids_out = ((np - 1 - j) % 2 == 0) ? out_ids : ib;
-    const bool last = j == np - 1;
-    const bool vbit = valid && n <= (size_t)kRsLack;
-    hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)nb), dim3(kRsBlock), 0, st, kin, ids_in, valid, n, pass, last, desc,
-                       vbit, kmin, hist, nb);
-    hipLaunchKernelGGL(k_rs_scan_digits, dim3(kRsDigits), dim3(256), 0, st, hist, nb, dtot);
-    hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)nb), dim3(kRsBlock), 0, st, kin, ids_in, valid, n, pass, desc,
-                       vbit, last, kmin, hist, dtot, nb, last ? nullptr : kout, ids_out);
-    kin = kout;
-    kout = kout == ka ? kb : ka;
-    ids_in = ids_out;
-  }
+  run_passes(shifts, np, false, out_ids, ib, nullptr);
   return hipGetLastError();
 }
 

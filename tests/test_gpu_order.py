@@ -119,3 +119,32 @@ def test_order_sl_non_holders_32_rows(eng):
         assert got == homo.order(route, keyed, 0), route
         lack = [k for k, r in keyed if len(r) == 0]
         assert [k for k in got if k in set(lack)] == lack  # non-holders keep their input order
+
+
+@pytest.mark.parametrize("kind", ["uniform_2p40", "ope_map_ties", "block_buckets", "overflow_bucket"])
+def test_order_msd_buckets(eng, kind):
+    """Spans of > 24 bits over >= 65,536 rows take the MSD split: two stable passes over the top 16
+    bits of the span, then each of the 65,536 buckets sorted by the rest of its keys (one wave up to
+    1024 rows, one workgroup up to 8192, all-equal buckets left as they are); a bucket of more rows
+    with distinct keys makes the engine redo the sort with the LSD passes. Every path against numpy."""
+    rng = np.random.default_rng(23)
+    n = 400_009
+    if kind == "uniform_2p40":
+        col = rng.integers(-(1 << 39), 1 << 39, size=n, dtype=np.int64)
+    elif kind == "ope_map_ties":  # the bench's generator: 10^4 distinct values, ~40 rows each here
+        ope_map = np.cumsum(rng.integers(1, 1 << 40, size=10001, dtype=np.int64)) - (1 << 52)
+        col = ope_map[rng.integers(1, 10001, size=n)]
+    else:
+        # span 2^40 -> buckets of 2^24 key values; a few buckets crowded with distinct keys
+        col = rng.integers(0, 1 << 40, size=n, dtype=np.int64)
+        sizes = [1025, 1500, 3000, 4097, 6000, 8192] if kind == "block_buckets" else [300, 20_000]
+        at = 0
+        for j, sz in enumerate(sizes):
+            bucket = (j * 9973 + 77) % (1 << 16)
+            rows = rng.choice(n, size=sz, replace=False) if j else np.arange(at, at + sz)
+            col[rows] = (bucket << 24) + rng.integers(0, 1 << 24, size=sz)
+            col[rows[: sz // 7]] = (bucket << 24) + 5  # ties inside the crowded bucket
+    valid = (rng.random(n) > 0.05).astype(np.uint8)
+    for desc in (True, False):
+        assert np.array_equal(eng.ope_order(col, valid, desc), expected(col, valid, desc)), (kind, desc)
+    assert np.array_equal(eng.ope_order(col, None, True), expected(col, np.ones(n, np.uint8), True)), kind
