@@ -219,13 +219,16 @@ size_t tree_direct_rows() {
   }();
   return n;
 }
-// DDSHE_TREE_SWITCH (leaves, default 1024; A/B at 10M rows: tail 0.232 -> 0.226 ms against 512): wider levels run as tail-shape lane-group launches (many
+// DDSHE_TREE_SWITCH (leaves, default 4096): wider levels run as tail-shape lane-group launches (many
 // products per launch: throughput), the last log2(switch) levels as tree launches (one workgroup per
-// product: latency)
+// product: latency; the widest of them on 256-thread workgroups, ddshe_tree.hip). Round 3 A/B
+// (tools/tree_sweep.sh, profiles/r03_tree_plan_sweep.txt): with the 256-thread wide levels and
+// in-kernel hand-offs, 1024 -> 4096 takes a 10k-row fold of the 1024-bit key 0.092 -> 0.088 ms and
+// of the 2048-bit key 0.141 -> 0.129 ms; 10M-row folds within noise.
 size_t tree_switch_leaves() {
   static const size_t n = [] {
     const char* e = getenv("DDSHE_TREE_SWITCH");
-    return e ? (size_t)atoll(e) : (size_t)1024;
+    return e ? (size_t)atoll(e) : (size_t)4096;
   }();
   return n;
 }

@@ -433,8 +433,7 @@ constexpr int kMsdBoundsRows = 4;
 __global__ void __launch_bounds__(256) k_msd_bounds(const uint64_t* __restrict__ keys, size_t n, int s1,
                                                     const uint32_t* __restrict__ dtot, int desc, bool has_valid,
                                                     uint32_t* __restrict__ first, uint32_t* __restrict__ end,
-                                                    uint32_t* __restrict__ multi, uint32_t* __restrict__ ctl) {
-  if (blockIdx.x == 0 && threadIdx.x < 8) ctl[threadIdx.x] = 0;
+                                                    uint32_t* __restrict__ multi) {
   size_t h0, h1;
   msd_holders(dtot, n, desc, has_valid, &h0, &h1);
   const int lane = threadIdx.x & 63;
@@ -538,20 +537,23 @@ __global__ void __launch_bounds__(256) k_msd_local(const uint64_t* __restrict__ 
                                                    const uint32_t* __restrict__ end,
                                                    const uint32_t* __restrict__ multi, int s1,
                                                    uint32_t* __restrict__ ctl, uint32_t* __restrict__ big) {
-  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (!multi[b]) return;  // empty, or one key: the last pass already put its rows in their place
-  const uint32_t lo = first[b], m = end[b] - lo;
-  if (msd_wave_partition(keys, src, ids, lo, m, lane, m <= kMsdWaveMax ? 2 : 16)) return;
-  if (m > kMsdWaveMax) {
-    if (lane == 0) big[atomicAdd(&ctl[kMsdCtlBig], 1u)] = b;
-    return;
+  {  // one wave per bucket (a grid-stride loop over the buckets measured 34 -> 56 us: the multi-key
+     // buckets' rounds serialise within a wave)
+    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (!multi[b]) return;  // empty, or one key: the last pass already put its rows in their place
+    const uint32_t lo = first[b], m = end[b] - lo;
+    if (msd_wave_partition(keys, src, ids, lo, m, lane, m <= kMsdWaveMax ? 2 : 16)) return;
+    if (m > kMsdWaveMax) {
+      if (lane == 0) big[atomicAdd(&ctl[kMsdCtlBig], 1u)] = b;
+      return;
+    }
+    const uint64_t rmask = (1ull << s1) - 1ull;
+    if (m <= 64) msd_wave_sort<1, 6>(keys, src, ids, lo, m, rmask, lane);
+    else if (m <= 128) msd_wave_sort<2, 7>(keys, src, ids, lo, m, rmask, lane);
+    else if (m <= 256) msd_wave_sort<4, 8>(keys, src, ids, lo, m, rmask, lane);
+    else msd_wave_sort<8, 9>(keys, src, ids, lo, m, rmask, lane);
   }
-  const uint64_t rmask = (1ull << s1) - 1ull;
-  if (m <= 64) msd_wave_sort<1, 6>(keys, src, ids, lo, m, rmask, lane);
-  else if (m <= 128) msd_wave_sort<2, 7>(keys, src, ids, lo, m, rmask, lane);
-  else if (m <= 256) msd_wave_sort<4, 8>(keys, src, ids, lo, m, rmask, lane);
-  else msd_wave_sort<8, 9>(keys, src, ids, lo, m, rmask, lane);
 }
 
 template <int E, int LOGP>
@@ -627,9 +629,9 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   uint64_t* part = red + 2;
   const size_t pb = (n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows);
   uint32_t* mfirst = (uint32_t*)(((uintptr_t)(part + 2 * pb) + 255) & ~(uintptr_t)255);
-  uint32_t* mmulti = mfirst + kMsdBuckets;
-  uint32_t* mend = mmulti + kMsdBuckets;
-  uint32_t* mctl = mend + kMsdBuckets;
+  uint32_t* mend = mfirst + kMsdBuckets;
+  uint32_t* mmulti = mend + kMsdBuckets;
+  uint32_t* mctl = mmulti + kMsdBuckets;  // right after the multi flags: one memset clears both
   uint32_t* mbig = mctl + 8;
   uint32_t* msrc = (uint32_t*)(((uintptr_t)(mbig + kMsdBuckets) + 255) & ~(uintptr_t)255);
   hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
@@ -669,10 +671,10 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     const int shifts[2] = {s1, sb - 8};
     // grouped ids -> out_ids (one-key buckets are final there) and the side copy msrc
     const uint64_t* sorted = run_passes(shifts, 2, true, out_ids, ib, msrc);
-    if ((e = hipMemsetAsync(mmulti, 0, kMsdBuckets * 4, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(mmulti, 0, (kMsdBuckets + 8) * 4, st)) != hipSuccess) return e;  // flags + control
     const size_t nbd = (n + 256 * kMsdBoundsRows - 1) / (256 * kMsdBoundsRows);  // over <= n holder rows
     hipLaunchKernelGGL(k_msd_bounds, dim3((unsigned)nbd), dim3(256), 0, st, sorted, n, s1, dtot, desc, valid != nullptr,
-                       mfirst, mend, mmulti, mctl);
+                       mfirst, mend, mmulti);
     hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / 4), dim3(256), 0, st, sorted, msrc, out_ids, mfirst, mend, mmulti,
                        s1, mctl, mbig);
     hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, sorted, msrc, out_ids, mfirst, mend, s1, mctl,

@@ -256,17 +256,19 @@ __device__ __forceinline__ size_t node_row(int h, size_t i) { return (i << h) + 
 // At the root: finalize (Y != nullptr): out = canonical result, S limbs of W bits;
 //   else out = canonical partial, Sout limbs of Wout bits, consecutive.
 // fence_mode 0: every wave releases / acquires at agent scope around a hand-off; 1: wave 0 only.
-template <int S, int W>
-__global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restrict__ X, size_t xstride, size_t gstride,
+template <int S, int W, int NT>
+__global__ void __launch_bounds__(NT) k_tree(const uint32_t* __restrict__ X, size_t xstride, size_t gstride,
                                                        int Sin, int Win, size_t nleaves,
                                                        const uint32_t* __restrict__ ids,
                                                        const uint32_t* __restrict__ consts,
                                                        const uint32_t* __restrict__ Y, uint32_t* __restrict__ nodes,
                                                        uint32_t* __restrict__ flags, uint32_t* __restrict__ out, int Sout,
                                                        int Wout, int max_levels, uint32_t* __restrict__ lvl_out,
-                                                       int fence_mode, uint64_t* __restrict__ stamps) {
+                                                       int fence_mode, uint64_t* __restrict__ stamps,
+                                                       uint32_t* __restrict__ clear, size_t nclear) {
   using O = Sos<S, W>;
-  constexpr int NT = kTreeThreads;
+  // the next launch's hand-off counters, zeroed here instead of by a separate memset launch
+  for (size_t j = (size_t)blockIdx.x * NT + threadIdx.x; j < nclear; j += (size_t)gridDim.x * NT) clear[j] = 0u;
   // y operands (b, N, n') zero-padded around y[0] (Sos::conv); x operands (a, d) zero past S
   __shared__ __attribute__((aligned(16))) uint32_t sa[O::XL], sd[O::XL], byp[O::YTOT], nyp[O::YTOT], npyp[O::YTOT];
   __shared__ uint32_t stmp[S + 64], stmp2[S + 64];
@@ -290,15 +292,18 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
   const int tid = threadIdx.x;
   const size_t b = blockIdx.x;
   const bool pair = 2 * b + 1 < nleaves;
-  // the leaves' words first (Sin <= S + 64 < kTreeThreads: one per thread), so their global loads are in
-  // flight together with the constants' below: one memory round trip instead of two
-  uint32_t lw0 = 0, lw1 = 0;
+  // the leaves' words first (Sin <= S + 64), so their global loads are in flight together with the
+  // constants' below: one memory round trip instead of two
+  constexpr int LW = (S + 64 + NT - 1) / NT;  // leaf words per thread
+  uint32_t lw0[LW], lw1[LW];
   {
     const size_t r0 = ids ? (size_t)ids[2 * b] : 2 * b;
     const size_t r1 = pair ? (ids ? (size_t)ids[2 * b + 1] : 2 * b + 1) : r0;
-    if (tid < Sin) {
-      lw0 = X[(size_t)tid * xstride + r0 * gstride];
-      if (pair) lw1 = X[(size_t)tid * xstride + r1 * gstride];
+#pragma unroll
+    for (int q = 0; q < LW; ++q) {
+      const int j = tid + q * NT;
+      lw0[q] = j < Sin ? X[(size_t)j * xstride + r0 * gstride] : 0u;
+      lw1[q] = (pair && j < Sin) ? X[(size_t)j * xstride + r1 * gstride] : 0u;
     }
   }
   for (int j = tid; j < O::YTOT; j += NT) {
@@ -315,18 +320,22 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
   for (int j = tid; j < 4 * S; j += NT) sT[j] = 0;  // both column buffers (Sos::monpro)
   for (int j = tid; j < S; j += NT) sM[j] = 0;
   {  // both leaves at once
-    if (tid < Sin) {
-      stmp[tid] = lw0;
-      stmp2[tid] = lw1;
+#pragma unroll
+    for (int q = 0; q < LW; ++q) {
+      const int j = tid + q * NT;
+      if (j < Sin) {
+        stmp[j] = lw0[q];
+        stmp2[j] = lw1[q];
+      }
     }
     __syncthreads();
     if (Sin == S && Win == W) {  // a previous launch's nodes: redundant limbs (< 2^W + 3), kept as they are
-      for (int j = tid; j < S; j += kTreeThreads) {
+      for (int j = tid; j < S; j += NT) {
         sa[j] = stmp[j];
         if (pair) sb[j] = stmp2[j];
       }
     } else {  // rows / first-level partials: normalised limbs of another radix
-      for (int j = tid; j < S; j += kTreeThreads) {
+      for (int j = tid; j < S; j += NT) {
         sa[j] = repack_limb(stmp, Sin, Win, W, j);
         if (pair) sb[j] = repack_limb(stmp2, Sin, Win, W, j);
       }
@@ -340,7 +349,7 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
   size_t i = b;
   while (((size_t)1 << h) < nleaves) {
     if (max_levels > 0 && h >= max_levels) {  // hand the node to the next launch
-      for (int j = tid; j < S; j += kTreeThreads) lvl_out[i * S + j] = sa[j];
+      for (int j = tid; j < S; j += NT) lvl_out[i * S + j] = sa[j];
       if (stamped) {
         sp.mark();
         if (threadIdx.x == 0) s_stamps[1] = __builtin_amdgcn_s_memrealtime() | ((uint64_t)sp.k << 56);
@@ -358,11 +367,11 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
         // release = s_waitcnt), and the sibling reads them with agent-scope atomic loads (sc1: not
         // served from a stale line of its own XCD's L2). tools/microbench/xcd_flag.hip: ~0.6 us per
         // hop this way against ~20 us with agent-scope release/acquire (L2 writeback + invalidate).
-        for (int j = tid; j < S; j += kTreeThreads)
+        for (int j = tid; j < S; j += NT)
           __hip_atomic_store(mine + j, sa[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
       } else {
-        for (int j = tid; j < S; j += kTreeThreads) mine[j] = sa[j];
+        for (int j = tid; j < S; j += NT) mine[j] = sa[j];
       }
       if (fence_mode == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // every wave: its stores
       __syncthreads();
@@ -380,10 +389,10 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
       if (fence_mode == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every wave: the sibling's stores
       const uint32_t* other = nodes + node_row(h, sib) * S;
       if (fence_mode == 2) {
-        for (int j = tid; j < S; j += kTreeThreads)
+        for (int j = tid; j < S; j += NT)
           sb[j] = __hip_atomic_load(const_cast<uint32_t*>(other) + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
-        for (int j = tid; j < S; j += kTreeThreads) sb[j] = __builtin_nontemporal_load(other + j);
+        for (int j = tid; j < S; j += NT) sb[j] = __builtin_nontemporal_load(other + j);
       }
       __syncthreads();
       O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM, par, sp);
@@ -393,7 +402,7 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
   }
   // root
   if (Y) {
-    for (int j = tid; j < S; j += kTreeThreads) sb[j] = Y[j];
+    for (int j = tid; j < S; j += NT) sb[j] = Y[j];
     __syncthreads();
     sp.mark();
     O::template monpro<NT>(sa, sb, ny, npy, sT, sd, sM, par, sp);
@@ -402,9 +411,9 @@ __global__ void __launch_bounds__(kTreeThreads) k_tree(const uint32_t* __restric
   __syncthreads();
   sp.mark();
   if (Y) {
-    for (int j = tid; j < S; j += kTreeThreads) out[j] = sa[j];
+    for (int j = tid; j < S; j += NT) out[j] = sa[j];
   } else {
-    for (int j = tid; j < Sout; j += kTreeThreads) out[j] = repack_limb(sa, S, W, Wout, j);
+    for (int j = tid; j < Sout; j += NT) out[j] = repack_limb(sa, S, W, Wout, j);
   }
   if (stamped) {
     if (threadIdx.x == 0) s_stamps[1] = __builtin_amdgcn_s_memrealtime() | ((uint64_t)sp.k << 56);
@@ -483,12 +492,19 @@ Shape tree_shape(size_t mod_bits) {
   return Shape{0, 0, 0};
 }
 
-// DDSHE_TREE_LEVELS (default 1; 0 = one launch walks to the root through in-kernel hand-offs, whose
-// agent-scope L2 writeback/invalidate fences measured far slower than a launch per level): levels per launch;
-// DDSHE_TREE_FENCE (default 1; with LEVELS != 1 only 0 or 2 are accepted): hand-off fence style (k_tree);
-// 2 = no cache maintenance (sc1 write-through
-// node stores and loads, relaxed flag): bit-exact on the GPU suite, and with it 2-5 levels per launch are
-// within run-to-run noise of one level per launch (10M-row tail 0.24-0.25 ms, 10k-row fold 0.12-0.13 ms)
+// Launch plan of a tree over n leaves:
+//   * wide levels (more than DDSHE_TREE_WIDE blocks, default 256 = one per CU): one level per launch on
+//     256-thread workgroups (k_tree<S, W, 256>): 8 products resident per CU instead of 1-2, each product
+//     slower than on 1024 threads but the level finishes in fewer rounds;
+//   * the rest on 1024-thread workgroups, DDSHE_TREE_LEVELS levels per launch (0 = to the root).
+//     With in-kernel hand-offs (LEVELS != 1) the node words are handed over in the form MI355X_MICROARCH.md
+//     (§ inter-workgroup visibility, "Valid forms", first table row) lists as measured valid: every node
+//     word stored sc1 (relaxed agent-scope atomic store), every storing wave's s_waitcnt vmcnt(0), a
+//     workgroup barrier, ONE lane's agent-scope atomic add on the parent's counter, the block whose add
+//     returned 1 continues and its waves load the sibling with sc1 loads after a barrier; hipMalloc'd
+//     memory; ONE workgroup per CU, enforced by the launch's dynamic LDS (> half of the CU's 160 KiB).
+//     DDSHE_TREE_FENCE selects the hand-off style: 2 = that form, 0 = agent-scope release/acquire by
+//     every wave (L2 writeback + L1 invalidate per hop), 1 = one level per launch only.
 static int tree_env(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
@@ -523,10 +539,14 @@ hipError_t launch_pairs_sos(int S, const uint32_t* A, const uint32_t* B, size_t 
   return hipGetLastError();
 }
 
+constexpr int kTreeWideThreads = 256;
+constexpr size_t kOneWgPerCuLds = 96 * 1024;  // dynamic LDS of a hand-off launch: one workgroup per CU
+
 hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Win, size_t nleaves, const uint32_t* ids,
                        const uint32_t* consts, const uint32_t* Y, uint32_t* nodes, uint32_t* flags, uint32_t* out,
                        int Sout, int Wout, hipStream_t st, size_t gstride) {
-  static const int levels = tree_env("DDSHE_TREE_LEVELS", 1), fence = tree_env("DDSHE_TREE_FENCE", 1);
+  static const int levels = tree_env("DDSHE_TREE_LEVELS", 0), fence = tree_env("DDSHE_TREE_FENCE", 2);
+  static const size_t wide = (size_t)tree_env("DDSHE_TREE_WIDE", 256);
   static uint64_t* d_st = nullptr;
   static const bool stamping = getenv("DDSHE_TREE_STAMPS") && hipMalloc(&d_st, 2 * kStamps * 8) == hipSuccess;
   if (nleaves == 0 || Sin > S + 64) return hipErrorInvalidValue;
@@ -536,23 +556,47 @@ hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Wi
   // level buffers for multi-launch trees live after the nodes: two ping-pong halves of nleaves rows
   uint32_t* lvl[2] = {nodes + (2 * nleaves + 2) * (size_t)S, nodes + (3 * nleaves + 2) * (size_t)S};
   int flip = 0;
+  bool flags_clear = false;  // a previous wide launch zeroed this launch's counters
   for (;;) {
-    const bool last = levels <= 0 || nleaves <= ((size_t)1 << levels);
     const size_t blocks = (nleaves + 1) / 2;
-    if (nleaves > 2 && (last ? levels != 1 : levels > 1)) {  // hand-offs happen in this launch
+    const bool wide_level = blocks > wide;  // 256-thread workgroups, one level
+    const int lv = wide_level ? 1 : levels;
+    const bool last = lv <= 0 || nleaves <= ((size_t)1 << lv);
+    const bool handoff = nleaves > 2 && (last ? lv != 1 : lv > 1);  // hand-offs happen in this launch
+    if (handoff && !flags_clear) {
       hipError_t e = hipMemsetAsync(flags, 0, (2 * nleaves + 2) * 4, st);
       if (e != hipSuccess) return e;
     }
-    DDSHE_TREE_SWITCH(S, hipLaunchKernelGGL((k_tree<S, W>), dim3((unsigned)blocks), dim3(kTreeThreads), 0, st, X,
-                                            xstride, gstride, Sin, Win, nleaves, ids, consts, Y, nodes, flags, out,
-                                            Sout, Wout, last ? 0 : levels, lvl[flip], fence,
-                                            stamping ? d_st : nullptr));
+    flags_clear = false;
+    if (wide_level) {
+      // the next launch: its leaves and whether it hands off in-kernel (then this one zeroes its counters)
+      const size_t nn = (nleaves + 1) >> 1, nb = (nn + 1) / 2;
+      const int nlv = nb > wide ? 1 : levels;
+      const bool nlast = nlv <= 0 || nn <= ((size_t)1 << nlv);
+      const size_t nclear = (nn > 2 && (nlast ? nlv != 1 : nlv > 1)) ? 2 * nn + 2 : 0;
+      flags_clear = nclear != 0;
+      DDSHE_TREE_SWITCH(S, hipLaunchKernelGGL((k_tree<S, W, kTreeWideThreads>), dim3((unsigned)blocks),
+                                              dim3(kTreeWideThreads), 0, st, X, xstride, gstride, Sin, Win, nleaves,
+                                              ids, consts, Y, nodes, flags, out, Sout, Wout, last ? 0 : 1, lvl[flip],
+                                              fence, stamping ? d_st : nullptr, flags, nclear));
+    } else {
+      const size_t dyn = handoff ? kOneWgPerCuLds : 0;
+      DDSHE_TREE_SWITCH(S, {
+        static const hipError_t attr = hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&k_tree<S, W, kTreeThreads>), hipFuncAttributeMaxDynamicSharedMemorySize,
+            (int)kOneWgPerCuLds);
+        (void)attr;
+        hipLaunchKernelGGL((k_tree<S, W, kTreeThreads>), dim3((unsigned)blocks), dim3(kTreeThreads), dyn, st, X,
+                           xstride, gstride, Sin, Win, nleaves, ids, consts, Y, nodes, flags, out, Sout, Wout,
+                           last ? 0 : lv, lvl[flip], fence, stamping ? d_st : nullptr, nullptr, (size_t)0);
+      });
+    }
     hipError_t e = hipGetLastError();
     if (stamping && e == hipSuccess) dump_stamps(d_st, S, nleaves, blocks, st);
     if (e != hipSuccess || last) return e;
     X = lvl[flip];
     flip ^= 1;
-    nleaves = (nleaves + ((size_t)1 << levels) - 1) >> levels;
+    nleaves = (nleaves + ((size_t)1 << lv) - 1) >> lv;
     xstride = 1;
     gstride = S;
     Sin = S;
