@@ -268,9 +268,17 @@ namespace host {
 // Coalescing queue of the pairwise routes for one modulus: a caller queues its pair; whoever finds
 // a batch slot free becomes a leader and runs one k_pairs launch over everything queued so far (group
 // commit: no added wait when calls arrive one at a time, one launch per burst under load). Up to
-// kPairInflight batches run at once, each on its own stream, so one batch's host round trip overlaps
+// pair_inflight() batches run at once, each on its own stream, so one batch's host round trip overlaps
 // the next; a finished leader wakes exactly the callers it served and the oldest waiter (no herd).
-constexpr int kPairInflight = 2;
+// DDSHE_PAIR_INFLIGHT overrides it for A/B runs
+inline int pair_inflight() {
+  static const int n = [] {
+    const char* e = getenv("DDSHE_PAIR_INFLIGHT");
+    const int v = e ? atoi(e) : 2;
+    return v < 1 ? 1 : v;
+  }();
+  return n;
+}
 struct PairReq {
   bn::Limbs a, b;  // magnitudes, already < N
   bn::Limbs r;     // a*b mod N

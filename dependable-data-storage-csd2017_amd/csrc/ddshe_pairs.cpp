@@ -5,13 +5,14 @@
 // one Montgomery product; the proxy runs routes concurrently on its pool (DDSRestServer.scala:21), so
 // concurrent requests under one modulus share a queue and the first caller to find it idle runs ONE
 // k_pairs launch over every pair queued so far (the others sleep on the queue's condition variable
-// and wake with their result). A lone request pays no batching wait. Up to kPairInflight batches of
+// and wake with their result). A lone request pays no batching wait. Up to pair_inflight() batches of
 // one modulus run at once (own streams): while one waits for its GPU round trip the next gathers and
 // launches. A burst of up to kTailPairs
 // pairs runs in the latency shape straight from the parsed limbs (one pinned H2D, one k_pairs launch,
 // one D2H, one synchronisation); larger ones take the batched dds_modmul_pairs path. A queue lives
 // while it has work: the last caller out of an idle queue drops it, so moduli sent once by clients
 // leave nothing behind.
+#include <stdlib.h>
 #include <string.h>
 
 #include <chrono>
@@ -85,6 +86,17 @@ void run_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& ba
   }
 }
 
+// DDSHE_PAIR_SPIN_US (default 100): how long a caller in another leader's batch yields before it sleeps
+// (64 native callers, tools/native/pairs_sweep.sh: 400 us -> p99 9-19 ms, 100 us -> p99 0.8-1.0 ms at
+// the same 1.2-1.5e5 pairs/s: yielding threads crowd out the leaders on a 16-core host share)
+int pair_spin_us() {
+  static const int us = [] {
+    const char* e = getenv("DDSHE_PAIR_SPIN_US");
+    return e ? atoi(e) : 100;
+  }();
+  return us;
+}
+
 int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req) {
   std::shared_ptr<PairQueue> q;
   {
@@ -99,7 +111,7 @@ int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req) {
     if (req->taken) {
       // in another leader's batch: spin briefly without the lock (a batch takes tens of µs), then sleep
       lk.unlock();
-      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(400);
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(pair_spin_us());
       while (!req->done.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < until)
         std::this_thread::yield();
       lk.lock();
@@ -109,7 +121,7 @@ int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req) {
       req->sleeping = false;
       continue;
     }
-    if (q->inflight >= kPairInflight) {
+    if (q->inflight >= pair_inflight()) {
       req->sleeping = true;
       req->cv.wait(lk);
       req->sleeping = false;
