@@ -71,11 +71,11 @@ __device__ __forceinline__ void rs_minmax_block(uint64_t lo, uint64_t hi, uint64
   }
 }
 
-__global__ void __launch_bounds__(256) k_rs_prep(const int64_t* __restrict__ col, const uint8_t* __restrict__ valid,
-                                                 size_t n, int desc, uint64_t* __restrict__ part) {
+// the same over rows one at a time (a column not 16-byte aligned, or valid bytes at an odd address)
+__global__ void __launch_bounds__(256) k_rs_prep_rows(const int64_t* __restrict__ col, const uint8_t* __restrict__ valid,
+                                                      size_t n, int desc, uint64_t* __restrict__ part) {
   uint64_t lo = ~0ull, hi = 0;
   const size_t base = (size_t)blockIdx.x * 256 * kRsPrepRows + threadIdx.x;
-  // all loads first (unconditional, index clamped: no load waits on a valid byte), then the min/max
   int64_t raw[kRsPrepRows];
   uint8_t hold[kRsPrepRows];
 #pragma unroll
@@ -91,6 +91,46 @@ __global__ void __launch_bounds__(256) k_rs_prep(const int64_t* __restrict__ col
       lo = min(lo, key);
       hi = max(hi, key);
     }
+  }
+  rs_minmax_block(lo, hi, part + 2 * blockIdx.x);
+}
+
+__global__ void __launch_bounds__(256) k_rs_prep(const int64_t* __restrict__ col, const uint8_t* __restrict__ valid,
+                                                 size_t n, int desc, uint64_t* __restrict__ part) {
+  uint64_t lo = ~0ull, hi = 0;
+  // rows in pairs: a wave instruction reads 64 consecutive 16-byte key pairs (and their 2 valid bytes);
+  // all loads first (unconditional, index clamped: no load waits on a valid byte), then the min/max
+  constexpr int P = kRsPrepRows / 2;
+  const size_t base = (size_t)blockIdx.x * 256 * kRsPrepRows;
+  const size_t npair = n / 2;  // whole pairs; an odd last row is read on its own
+  ulonglong2 kv[P];
+  uint16_t hv[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const size_t q = min(base / 2 + (size_t)k * 256 + threadIdx.x, npair ? npair - 1 : 0);
+    kv[k] = npair ? reinterpret_cast<const ulonglong2*>(col)[q] : make_ulonglong2(0, 0);
+    hv[k] = (valid && npair) ? reinterpret_cast<const uint16_t*>(valid)[q] : (uint16_t)0x0101;
+  }
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const size_t q = base / 2 + (size_t)k * 256 + threadIdx.x;
+    if (q < npair) {
+      if (hv[k] & 0xFFu) {
+        const uint64_t key = rs_ukey(kv[k].x, desc);
+        lo = min(lo, key);
+        hi = max(hi, key);
+      }
+      if (hv[k] >> 8) {
+        const uint64_t key = rs_ukey(kv[k].y, desc);
+        lo = min(lo, key);
+        hi = max(hi, key);
+      }
+    }
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0 && (!valid || valid[n - 1])) {  // odd last row
+    const uint64_t key = rs_ukey((uint64_t)col[n - 1], desc);
+    lo = min(lo, key);
+    hi = max(hi, key);
   }
   rs_minmax_block(lo, hi, part + 2 * blockIdx.x);
 }
@@ -634,7 +674,10 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   uint32_t* mctl = mmulti + kMsdBuckets;  // right after the multi flags: one memset clears both
   uint32_t* mbig = mctl + 8;
   uint32_t* msrc = (uint32_t*)(((uintptr_t)(mbig + kMsdBuckets) + 255) & ~(uintptr_t)255);
-  hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
+  if (((uintptr_t)col & 15) == 0 && ((uintptr_t)valid & 1) == 0)
+    hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
+  else
+    hipLaunchKernelGGL(k_rs_prep_rows, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
   hipLaunchKernelGGL(k_rs_red, dim3(1), dim3(1024), 0, st, part, pb, red);
   uint64_t hred[2];
   hipError_t e = hipMemcpyAsync(hred, red, sizeof(hred), hipMemcpyDeviceToHost, st);

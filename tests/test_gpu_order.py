@@ -148,3 +148,24 @@ def test_order_msd_buckets(eng, kind):
     for desc in (True, False):
         assert np.array_equal(eng.ope_order(col, valid, desc), expected(col, valid, desc)), (kind, desc)
     assert np.array_equal(eng.ope_order(col, None, True), expected(col, np.ones(n, np.uint8), True)), kind
+
+
+@pytest.mark.parametrize("offset", [0, 1])
+def test_order_device_pointers(eng, offset):
+    """dds_ope_order_device on caller-owned device buffers: the min/max prep reads 16-byte key pairs
+    when the column is 16-byte aligned (and the valid bytes 2-byte aligned) and single rows otherwise
+    (a column starting at an odd row of an allocation)."""
+    import torch
+    rng = np.random.default_rng(31 + offset)
+    n = 300_001
+    col = rng.integers(-(1 << 45), 1 << 45, size=n + 1, dtype=np.int64)
+    valid = (rng.random(n + 1) > 0.07).astype(np.uint8)
+    d_col = torch.from_numpy(col).to("cuda")
+    d_valid = torch.from_numpy(valid).to("cuda")
+    d_out = torch.empty(n, dtype=torch.int32, device="cuda")
+    for desc in (True, False):
+        eng.ope_order_device(d_col.data_ptr() + 8 * offset, d_valid.data_ptr() + offset, n, desc, d_out.data_ptr())
+        torch.cuda.synchronize()
+        got = d_out.cpu().numpy().view(np.uint32)
+        want = expected(col[offset:offset + n], valid[offset:offset + n], desc)
+        assert np.array_equal(got, want), (offset, desc)
