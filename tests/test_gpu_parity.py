@@ -367,3 +367,24 @@ def test_gpu_egress_pairs_and_column_read(eng, bits):
     assert col.read(0, len(rows)) == [x % N for x in rows]
     assert col.read(7, 5) == [x % N for x in rows[7:12]]
     col.close()
+
+
+@pytest.mark.parametrize("key_name", ["paillier1024_seed1", "paillier2048_committed"])
+def test_tree_handoff_repeated_folds(eng, keys, key_name):
+    """The tree's last levels run in ONE launch with in-kernel hand-offs (sc1 node words, the last
+    arriver continues). Repeated folds over every tree shape of the launch plan (256-thread wide
+    levels, then the hand-off launch from <= 256 blocks; odd leaf counts leave unpaired nodes) must
+    all agree and decrypt to the sum of the plaintexts: a stale sibling read would break either."""
+    import ddshe
+    k = keys[key_name]
+    rows = 70_001
+    col = eng.column(k["nsquare"], rows)
+    col.fill_paillier_synth(k["n"], k["g"], seed=9, row0=0, count=rows, pool=128)
+    ms = ddshe.synth_plaintexts(9, 0, rows).astype(np.int64)
+    for count in (3, 257, 513, 1025, 2049, 4097, 8193, 20_000, 70_001):
+        want = int(ms[:count].sum()) % k["n"]
+        first = col.fold(0, count)
+        assert homo.paillier_decrypt(first, k) == want, count
+        for _ in range(12):
+            assert col.fold(0, count) == first, count
+    col.close()
