@@ -532,11 +532,21 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
   HIP_TRY(w->rflags.ensure(count));
   HIP_TRY(w->flags.ensure(16));
   HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, st));
+  if (!w->cstream) {
+    HIP_TRY(hipStreamCreateWithFlags(&w->cstream, hipStreamNonBlocking));
+    for (auto& e : w->ev_copy) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  hipStream_t cs = w->cstream;
+  // rows per chunk: a request of fewer than 2 x 2^18 rows still splits into two chunks (>= 4096 rows
+  // each), so the second chunk's host and H2D copies overlap the first one's parse (config 1: 10k
+  // rows, 6.2 MB of chars). Not more: a small chunk's parse is latency-bound (~46 us whatever its
+  // size), and four chunks measured slower (0.43 -> 0.49 ms) than one.
+  const size_t crows = std::min(kDecChunkRows, std::max<size_t>(4096, (count + 1) / 2));
   bool used[2] = {false, false};
   int slot = 0;
   std::vector<size_t> lens;
   for (size_t b = 0; b < count;) {
-    if (used[slot]) HIP_TRY(hipEventSynchronize(w->ev_dec[slot]));
+    if (used[slot]) HIP_TRY(hipEventSynchronize(w->ev_copy[slot]));  // the H2D out of this host slot is done
     HIP_TRY(w->hch[slot].ensure(kDecChunkBytes + 64));
     HIP_TRY(w->hoff[slot].ensure((kDecChunkRows + 1) * 8));
     char* dst = (char*)w->hch[slot].p + 16;
@@ -545,7 +555,7 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
     o[0] = 0;
     if (!src.strs) {  // Arrow-style rows: one bulk copy of the chunk's chars, offsets rebased
       const uint64_t base = src.offs[b];
-      size_t lo = b, hi = std::min(count, b + kDecChunkRows);  // largest e in [b, hi] with chars <= chunk
+      size_t lo = b, hi = std::min(count, b + crows);  // largest e in [b, hi] with chars <= chunk
       while (lo < hi) {
         const size_t mid = lo + (hi - lo + 1) / 2;
         if (src.offs[mid] - base <= kDecChunkBytes - 64) lo = mid;
@@ -558,10 +568,10 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
         for (size_t i = b; i <= e; ++i) o[i - b] = src.offs[i] - base;
       }
     }
-    if (src.strs && count - b >= 4096) {
+    if (src.strs && std::min(count - b, crows) >= 1024) {
       // NUL-terminated rows (JNA String[]): lengths and copies spread over the host pool; the
       // chunk cut and the offsets are one sequential pass over the lengths
-      const size_t hi = std::min(count, b + kDecChunkRows);
+      const size_t hi = std::min(count, b + crows);
       lens.resize(hi - b);
       CopyPool::get().parallel_for(hi - b, 1024, [&](size_t x, size_t y) {
         for (size_t i = x; i < y; ++i) lens[i] = strlen(src.strs[b + i]);
@@ -578,7 +588,7 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
           memcpy(dst + o[i], o[i + 1] - o[i] == lens[i] ? src.strs[b + i] : "0", o[i + 1] - o[i]);
       });
     }
-    while (e < count && e - b < kDecChunkRows) {
+    while (e < count && e - b < crows) {
       size_t n = src.len(e);
       const bool longrow = n > kDecChunkBytes - 64;
       if (longrow) n = 1;
@@ -590,10 +600,17 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
     }
     const size_t nrows = e - b, bytes = (16 + pos + 16 + 3) & ~(size_t)3;
     memset(dst + pos, 0, bytes - 16 - pos);
+    // the device slot is free once the parse of its previous chunk has run (a growing buffer is
+    // reallocated only after that parse, host-side)
+    if (used[slot] && (w->dch[slot].cap < bytes || w->doff[slot].cap < (nrows + 1) * 8))
+      HIP_TRY(hipEventSynchronize(w->ev_dec[slot]));
     HIP_TRY(w->dch[slot].ensure(bytes));
     HIP_TRY(w->doff[slot].ensure((nrows + 1) * 8));
-    HIP_TRY(hipMemcpyAsync(w->dch[slot].p, w->hch[slot].p, bytes, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(w->doff[slot].p, o, (nrows + 1) * 8, hipMemcpyHostToDevice, st));
+    if (used[slot]) HIP_TRY(hipStreamWaitEvent(cs, w->ev_dec[slot], 0));
+    HIP_TRY(hipMemcpyAsync(w->dch[slot].p, w->hch[slot].p, bytes, hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipMemcpyAsync(w->doff[slot].p, o, (nrows + 1) * 8, hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipEventRecord(w->ev_copy[slot], cs));
+    HIP_TRY(hipStreamWaitEvent(st, w->ev_copy[slot], 0));
     HIP_TRY(launch_dec_parse(mc.S, w->dch[slot].as<uint32_t>(), w->doff[slot].as<uint64_t>(), 0, nrows, mc.dtab,
                              mc.jfit, mc.jpad, mc.d, X + b, stride, w->rflags.as<uint8_t>() + b,
                              w->flags.as<uint32_t>(), st));

@@ -255,10 +255,21 @@ hipError_t launch_dec_parse(int S, const uint32_t* chars4, const uint64_t* offs,
                             size_t stride, uint8_t* rowflags, uint32_t* flags, hipStream_t st) {
   if (count == 0) return hipSuccess;
   const int ldsw = ((jfit > S ? jfit : S) + 3) & ~3;
+  // A batch too small to fill the chip (config 1: 10k rows at 2 lanes each is 0.3 waves per SIMD) is
+  // latency-bound: per-lane work is ~K^2 / (2 TPI) MACs, so such batches take a wider lane group
+  // where the shape divides (S = 40, 76, 112); the output layout (limb r * L + l) is the same.
+  constexpr size_t kDecLatencyLanes = 131072;
   DDSHE_SWITCH(S, {
-    const size_t lds = (size_t)(256 / TPI) * ldsw * 4;
-    hipLaunchKernelGGL((k_dec_parse<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), lds, st, chars4, offs,
-                       obase, count, tab, jfit, jpad, ldsw, consts, X, stride, rowflags, flags);
+    constexpr int TL = (S % (4 * TPI) == 0 && 4 * TPI <= 16) ? 4 * TPI : (S % (2 * TPI) == 0 && 2 * TPI <= 16) ? 2 * TPI : TPI;
+    if (TL != TPI && count * TPI < kDecLatencyLanes) {
+      const size_t lds = (size_t)(256 / TL) * ldsw * 4;
+      hipLaunchKernelGGL((k_dec_parse<S, TL, W>), dim3(grid_for(count * TL)), dim3(256), lds, st, chars4, offs,
+                         obase, count, tab, jfit, jpad, ldsw, consts, X, stride, rowflags, flags);
+    } else {
+      const size_t lds = (size_t)(256 / TPI) * ldsw * 4;
+      hipLaunchKernelGGL((k_dec_parse<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), lds, st, chars4, offs,
+                         obase, count, tab, jfit, jpad, ldsw, consts, X, stride, rowflags, flags);
+    }
   });
   return hipGetLastError();
 }

@@ -97,7 +97,13 @@ struct Worker {
   HostBuf hbig;    // large read-backs (Search ids / match masks, Order permutations) before the caller's copy
   DevBuf dch[2], doff[2], rflags;
   hipEvent_t ev_dec[2] = {};
+  // decimal ingest: H2D copies on their own stream (chunk s + 1 copies while chunk s parses)
+  hipStream_t cstream = nullptr;
+  hipEvent_t ev_copy[2] = {};
   ~Worker() {
+    for (auto e : ev_copy)
+      if (e) (void)hipEventDestroy(e);
+    if (cstream) (void)hipStreamDestroy(cstream);
     for (auto e : ev)
       if (e) (void)hipEventDestroy(e);
     for (auto e : ev_dec)
