@@ -68,12 +68,13 @@ __device__ __forceinline__ uint32_t grp_or(uint32_t x, int r) {
   return o;
 }
 
-// tab: Pt[l * jpad + j] = limb l of 10^(8j) (j < jfit, zero up to jpad), then jst[i] (i < L): a
-// multiple of 4 <= the first j whose power reaches limb TPI*i. ldsw: LDS words per group.
+// tab: Pt[l * jpad + j] = limb l of 10^(8j) (j < jfit, zero up to jpad), then jst[i] (i < L of the shape's
+// own TPI): a multiple of 4 <= the first j whose power reaches limb TPI*i. A launch with a wider lane
+// group (TL = jstep * TPI lanes) reads jst[i * jstep] for its limb TL*i. ldsw: LDS words per group.
 template <int S, int TPI, int W>
 __global__ void __launch_bounds__(256) k_dec_parse(const uint32_t* __restrict__ chars4, const uint64_t* __restrict__ offs,
                                                    uint64_t obase, size_t count, const uint32_t* __restrict__ tab,
-                                                   int jfit, int jpad, int ldsw,
+                                                   int jfit, int jpad, int ldsw, int jstep,
                                                    const uint32_t* __restrict__ consts, uint32_t* __restrict__ X,
                                                    size_t stride, uint8_t* __restrict__ rowflags,
                                                    uint32_t* __restrict__ flags) {
@@ -135,20 +136,38 @@ __global__ void __launch_bounds__(256) k_dec_parse(const uint32_t* __restrict__ 
 #pragma unroll
   for (int i = 0; i < L; ++i) acc[i] = 0;
   if (live && !(fl & kDecFormat)) {
+    // QL limbs per pass: one LDS read of 4 words feeds QL table rows (independent loads in flight
+    // instead of one dependent L2 round trip per 4 words of one limb). A pass starts at its lowest
+    // limb's first non-zero word; the higher limbs' table entries below their own start are zero.
+    constexpr int QL = 4;
     const uint32_t* jst = tab + (size_t)S * jpad;
+    const uint4* wb = reinterpret_cast<const uint4*>(buf);
 #pragma unroll
-    for (int i = 0; i < L; ++i) {
-      const uint4* pl = reinterpret_cast<const uint4*>(tab + (size_t)(g.r + TPI * i) * jpad);
-      const uint4* wb = reinterpret_cast<const uint4*>(buf);
-      uint64_t s = 0;
-      for (int j4 = (int)jst[i] >> 2; j4 < (kw >> 2); ++j4) {
-        const uint4 w = wb[j4], pv = pl[j4];
-        s += (uint64_t)w.x * pv.x;
-        s += (uint64_t)w.y * pv.y;
-        s += (uint64_t)w.z * pv.z;
-        s += (uint64_t)w.w * pv.w;
+    for (int i0 = 0; i0 < L; i0 += QL) {
+      const uint4* pl[QL];
+      uint64_t s[QL];
+#pragma unroll
+      for (int q = 0; q < QL; ++q) {
+        pl[q] = reinterpret_cast<const uint4*>(tab + (size_t)(g.r + TPI * (i0 + q < L ? i0 + q : i0)) * jpad);
+        s[q] = 0;
       }
-      acc[i] = s;
+#pragma unroll 2
+      for (int j4 = (int)jst[i0 * jstep] >> 2; j4 < (kw >> 2); ++j4) {
+        const uint4 w = wb[j4];
+#pragma unroll
+        for (int q = 0; q < QL; ++q) {
+          if (i0 + q < L) {
+            const uint4 pv = pl[q][j4];
+            s[q] += (uint64_t)w.x * pv.x;
+            s[q] += (uint64_t)w.y * pv.y;
+            s[q] += (uint64_t)w.z * pv.z;
+            s[q] += (uint64_t)w.w * pv.w;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < QL; ++q)
+        if (i0 + q < L) acc[i0 + q] = s[q];
     }
   }
 
@@ -264,11 +283,11 @@ hipError_t launch_dec_parse(int S, const uint32_t* chars4, const uint64_t* offs,
     if (TL != TPI && count * TPI < kDecLatencyLanes) {
       const size_t lds = (size_t)(256 / TL) * ldsw * 4;
       hipLaunchKernelGGL((k_dec_parse<S, TL, W>), dim3(grid_for(count * TL)), dim3(256), lds, st, chars4, offs,
-                         obase, count, tab, jfit, jpad, ldsw, consts, X, stride, rowflags, flags);
+                         obase, count, tab, jfit, jpad, ldsw, TL / TPI, consts, X, stride, rowflags, flags);
     } else {
       const size_t lds = (size_t)(256 / TPI) * ldsw * 4;
       hipLaunchKernelGGL((k_dec_parse<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), lds, st, chars4, offs,
-                         obase, count, tab, jfit, jpad, ldsw, consts, X, stride, rowflags, flags);
+                         obase, count, tab, jfit, jpad, ldsw, 1, consts, X, stride, rowflags, flags);
     }
   });
   return hipGetLastError();
