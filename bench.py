@@ -315,7 +315,7 @@ class SumWorkload(_Workload):
         roof = self.fold_roofline(S_32)
         roof["kernel"] = "k_fold<148,4,28> (first fold level over the rows)"
         # HBM bytes per launch from the committed rocprofv3 PMC passes of this kernel (10M rows, each read once)
-        traffic = pmc_traffic("sum", ("k_fold<148, 4, 28, true, false>",), largest=True)
+        traffic = pmc_traffic("sum", ("k_fold<148, 4, 28, true, false, false>",), largest=True)
         if traffic is not None:
             traffic *= self.mine / 1e7
         roof.update(traffic=traffic, traffic_unit=f"HBM bytes per launch (PMC, profiles/{PMC_FILE})")
@@ -670,6 +670,8 @@ def pmc_traffic(workload, kernels, per_step=False, largest=False):
     tot = 0.0
     for k in kernels:
         d = ks.get(f"{workload}:{k}")
+        if d is None:  # a template that gained trailing parameters since the name was written here
+            d = next((v for n, v in ks.items() if n.startswith(f"{workload}:{k[:-1]},")), None)
         if d is None:
             return None
         if largest and "hbm_bytes_max_dispatch" in d:
