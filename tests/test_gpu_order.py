@@ -169,3 +169,25 @@ def test_order_device_pointers(eng, offset):
         got = d_out.cpu().numpy().view(np.uint32)
         want = expected(col[offset:offset + n], valid[offset:offset + n], desc)
         assert np.array_equal(got, want), (offset, desc)
+
+
+def test_resident_opecol_order_msd_with_dead_rows(eng):
+    """The resident OPE column's order (dds_opecol_order: OrderLS / OrderSL over the live rows) at a
+    size and span that take the MSD split, with removed sets (dead rows) dropped after the sort."""
+    import ddshe
+    rng = np.random.default_rng(41)
+    n = 150_001
+    col = rng.integers(-(1 << 50), 1 << 50, size=n, dtype=np.int64)
+    col[rng.choice(n, size=n // 3, replace=False)] = 12345  # a crowded key (one-key bucket)
+    oc = ddshe.OpeColumn(eng, n)
+    oc.append(col)
+    dead = rng.choice(n, size=n // 10, replace=False)
+    oc.set_live(dead, 0)
+    live = np.ones(n, dtype=bool)
+    live[dead] = False
+    idx = np.arange(n)[live]
+    for desc in (True, False):
+        key = ~col[idx] if desc else col[idx]
+        want = idx[np.argsort(key, kind="stable")]
+        assert np.array_equal(oc.order(desc), want.astype(np.uint32)), desc
+    oc.close()
