@@ -970,14 +970,14 @@ class OrderWorkload(_Workload):
                 print("VERIFY FAILED", file=sys.stderr)
         step_s = elapsed / a.steps
         alg = 13 * self.mine  # read key + valid byte, write one row id
-        roof = {"bound": "hbm", "kernel": "k_rs_prep + 2 LSD passes over the top 16 bits of the key span (k_rs_hist/"
-                "k_rs_scan_digits/k_rs_scatter) + k_msd_bounds + k_msd_local/k_msd_big (in-bucket order of the "
+        roof = {"bound": "hbm", "kernel": "k_rs_prep + 2 LSD passes over the top 16 bits of the key span (k_rs_hist/k_rs_scan_tiles/"
+                "k_rs_scan_chunks/k_rs_scatter) + k_msd_bounds + k_msd_local/k_msd_big (in-bucket order of the "
                 "buckets holding two distinct keys)",
                 "achieved": alg / step_s / 1e9, "peak": 8000.0, "unit": "GB/s", "frac": alg / step_s / 1e9 / 8000.0,
                 "algorithmic_bytes": alg,
-                # prep 9 + 2 passes x (hist 8 + scatter 24) + 4 (ids + side copy in the last pass) + bounds 8
-                "issued_bytes_est": self.mine * (9 + 2 * 32 + 8 + 8),
-                "traffic": pmc_traffic("order", ("k_rs_prep", "k_rs_red", "k_rs_hist", "k_rs_scan_digits", "k_rs_scatter",
+                # prep 9 + 2 passes x (hist 8 + scatter 24) + bounds 8 (+ the multi-key buckets' rounds)
+                "issued_bytes_est": self.mine * (9 + 2 * 32 + 8),
+                "traffic": pmc_traffic("order", ("k_rs_prep", "k_rs_red", "k_rs_hist", "k_rs_scan_tiles", "k_rs_scan_chunks", "k_rs_scatter",
                                                  "k_msd_bounds", "k_msd_local", "k_msd_big"), per_step=True),
                 "traffic_unit": "HBM bytes per OrderLS call (PMC, profiles/" + PMC_FILE + ")"}
         roof["issued_GBps"] = roof["issued_bytes_est"] / step_s / 1e9  # what the MSD-split design moves

@@ -9,8 +9,8 @@
 // Keys are offset by the smallest key of a holder (k_rs_prep / k_rs_red: min and max over the rows that
 // hold the position), so only the bytes of (max - min) are sorted: ceil(bits(max - min) / 8) passes
 // (an OPE column spanning 2^54 values needs 7, not 8). Per 8-bit digit pass (the last executed one
-// has 257 buckets: the validity of the row moves it to the end / front): k_rs_hist (per-tile digit counts, digit-major) -> k_rs_scan_digits (per-digit
-// scan over tiles, one block per digit, coalesced 1024-count chunks; the scatter blocks scan the 257
+// has 257 buckets: the validity of the row moves it to the end / front): k_rs_hist (per-tile digit counts, tile-major) -> k_rs_scan_tiles +
+// k_rs_scan_chunks (per-digit scan over tiles in chunks of 64 tiles; the scatter blocks scan the 257
 // digit totals themselves) -> k_rs_scatter (stable rank inside the tile: each wave walks a contiguous
 // quarter of the tile, peers with equal digits are found with 9 ballots, per-wave digit counters in
 // LDS; the ranked rows are staged in LDS in tile-local digit order and written out by consecutive
@@ -211,53 +211,53 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_hist(const uint64_t* __restrict
     if (d != kRsNone && (peers & lt) == 0) atomicAdd(&cnt[d], (uint32_t)__popcll(peers));
   }
   __syncthreads();
-  for (int d = threadIdx.x; d < kRsDigits; d += kRsBlock) hist[(size_t)d * nblocks + blockIdx.x] = cnt[d];
+  for (int d = threadIdx.x; d < kRsDigits; d += kRsBlock) hist[(size_t)blockIdx.x * kRsDigits + d] = cnt[d];  // 1 KiB, coalesced
 }
 
-// per digit d (one block each): exclusive scan of the tile counts hist[d][0..nblocks) in place,
-// digit total -> dtot[d]. Chunks of 1024 counts: thread t owns counts 4t..4t+3 of a chunk (a wave's
-// loads cover 1 KiB contiguous); up to kScanRegChunks chunks are loaded before any is scanned.
-constexpr int kScanRegChunks = 8;
-__global__ void __launch_bounds__(256) k_rs_scan_digits(uint32_t* __restrict__ hist, size_t nblocks,
-                                                        uint32_t* __restrict__ dtot) {
-  __shared__ uint32_t wtot[4];
-  uint32_t* h = hist + (size_t)blockIdx.x * nblocks;
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  uint32_t carry = 0;
-  for (size_t c0 = 0; c0 < nblocks; c0 += (size_t)1024 * kScanRegChunks) {
-    uint32_t v[kScanRegChunks][4];
+// Tile counts are tile-major (hist[tile][digit]: each histogram block writes 1 KiB in one go; the
+// digit-major layout cost one 32-byte sector per 4-byte count, 8x the bytes, PMC round 2). The
+// exclusive scan over tiles per digit then runs in two steps:
+//   k_rs_scan_tiles: one block per chunk of kScanTiles tiles, one thread per digit: the chunk's
+//     counts of that digit (coalesced rows across the digit threads) are replaced in place by their
+//     exclusive prefix within the chunk, and the chunk total goes to ctot[chunk][digit];
+//   k_rs_scan_chunks: one block, one thread per digit: exclusive prefix of the chunk totals in place,
+//     digit total -> dtot[digit].
+// A tile's offset for digit d is then dbase[d] + ctot[chunk][d] + hist[tile][d] (k_rs_scatter).
+constexpr int kScanTiles = 64;
+constexpr int kScanThreads = 320;  // >= kRsDigits
+__global__ void __launch_bounds__(kScanThreads) k_rs_scan_tiles(uint32_t* __restrict__ hist, size_t nblocks,
+                                                                uint32_t* __restrict__ ctot) {
+  const int d = threadIdx.x;
+  if (d >= kRsDigits) return;
+  const size_t t0 = (size_t)blockIdx.x * kScanTiles;
+  uint32_t v[kScanTiles];
 #pragma unroll
-    for (int c = 0; c < kScanRegChunks; ++c)
+  for (int r = 0; r < kScanTiles; ++r) v[r] = t0 + r < nblocks ? hist[(t0 + r) * kRsDigits + d] : 0u;
+  uint32_t run = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const size_t b = c0 + (size_t)c * 1024 + 4 * tid + j;
-        v[c][j] = b < nblocks ? h[b] : 0u;
-      }
+  for (int r = 0; r < kScanTiles; ++r) {
+    if (t0 + r < nblocks) hist[(t0 + r) * kRsDigits + d] = run;
+    run += v[r];
+  }
+  ctot[(size_t)blockIdx.x * kRsDigits + d] = run;
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_rs_scan_chunks(uint32_t* __restrict__ ctot, size_t nchunks,
+                                                                 uint32_t* __restrict__ dtot) {
+  const int d = threadIdx.x;
+  if (d >= kRsDigits) return;
+  uint32_t run = 0;
+  for (size_t c0 = 0; c0 < nchunks; c0 += 16) {
+    uint32_t v[16];
 #pragma unroll
-    for (int c = 0; c < kScanRegChunks; ++c) {
-      if (c0 + (size_t)c * 1024 >= nblocks) break;  // block-uniform
-      const uint32_t s = v[c][0] + v[c][1] + v[c][2] + v[c][3];
-      uint32_t inc = s;
-      for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)inc, off);
-        if (lane >= off) inc += y;
-      }
-      if (lane == 63) wtot[wid] = inc;
-      __syncthreads();
-      uint32_t run = carry + inc - s;
-      for (int w = 0; w < wid; ++w) run += wtot[w];
-      const uint32_t ctot = wtot[0] + wtot[1] + wtot[2] + wtot[3];
-      __syncthreads();
+    for (int q = 0; q < 16; ++q) v[q] = c0 + q < nchunks ? ctot[(c0 + q) * kRsDigits + d] : 0u;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const size_t b = c0 + (size_t)c * 1024 + 4 * tid + j;
-        if (b < nblocks) h[b] = run;
-        run += v[c][j];
-      }
-      carry += ctot;
+    for (int q = 0; q < 16; ++q) {
+      if (c0 + q < nchunks) ctot[(c0 + q) * kRsDigits + d] = run;
+      run += v[q];
     }
   }
-  if (tid == 0) dtot[blockIdx.x] = carry;
+  dtot[d] = run;
 }
 
 // The ranked rows are first placed in tile-local digit order in LDS, then written out by
@@ -268,10 +268,10 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
                                                          const uint8_t* __restrict__ valid, size_t n, int shift,
                                                          int desc, bool vbit, bool last, uint64_t kmin,
                                                          const uint32_t* __restrict__ hist,
+                                                         const uint32_t* __restrict__ ctot,
                                                          const uint32_t* __restrict__ dtot, size_t nblocks,
                                                          uint64_t* __restrict__ keys_out,
-                                                         uint32_t* __restrict__ ids_out,
-                                                         uint32_t* __restrict__ ids_copy) {
+                                                         uint32_t* __restrict__ ids_out) {
   __shared__ uint32_t cnt[kRsWaves][kRsDigits];
   __shared__ uint32_t dbase[kRsDigits + 1];   // global start of digit d, then of this tile's run of d
   __shared__ uint32_t lstart[kRsDigits + 1];  // tile-local start of digit d
@@ -347,7 +347,7 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
       cnt[w][d] = run;
       run += c;
     }
-    dbase[d] += hist[(size_t)d * nblocks + blockIdx.x];
+    dbase[d] += ctot[(size_t)(blockIdx.x / kScanTiles) * kRsDigits + d] + hist[(size_t)blockIdx.x * kRsDigits + d];
   }
   __syncthreads();
 #pragma unroll
@@ -367,7 +367,6 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
     const uint32_t dst = dbase[d] + (q - lstart[d]);
     if (keys_out) keys_out[dst] = skey[q];
     ids_out[dst] = sid[q];
-    if (ids_copy) ids_copy[dst] = sid[q];  // MSD split: side copy the in-bucket sort reads
   }
 }
 
@@ -387,11 +386,12 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
 //     the LSD passes (never seen on OPE data: it needs > 16 distinct keys among > 8192 rows whose
 //     keys agree on the top 16 bits of the span).
 // The last top pass writes each id to its final place if its bucket holds one key (OPE columns:
-// most buckets), plus a side copy (src) the in-bucket step reads, so nothing is sorted in place.
+// most buckets); a multi-key bucket's wave first copies its ids to the first pass's (now free) id
+// buffer and reads them from there, so nothing is sorted in place.
 // Bucket bounds come from one pass over the sorted keys (k_msd_bounds: the first and the last row of
 // every non-empty bucket and whether it holds two distinct keys); only those buckets are touched.
-// Per row: 2 LSD passes (+ 4 B for the side copy) + 8 B of bounds read, and for rows of multi-key
-// buckets (8 B key + 4 B id read, 4 B id written) per partition round or sort, against
+// Per row: 2 LSD passes + 8 B of bounds read, and for rows of multi-key buckets a 4 B id copy plus
+// (8 B key + 4 B id read, 4 B id written) per partition round or sort, against
 // ceil(bits(span) / 8) LSD passes (7 for a 2^54 span).
 constexpr int kMsdBits = 16;
 constexpr uint32_t kMsdBuckets = 1u << kMsdBits;
@@ -572,7 +572,7 @@ __device__ __forceinline__ void msd_wave_sort(const uint64_t* __restrict__ keys,
   }
 }
 
-__global__ void __launch_bounds__(256) k_msd_local(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ src,
+__global__ void __launch_bounds__(256) k_msd_local(const uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
                                                    uint32_t* __restrict__ ids, const uint32_t* __restrict__ first,
                                                    const uint32_t* __restrict__ end,
                                                    const uint32_t* __restrict__ multi, int s1,
@@ -583,6 +583,9 @@ __global__ void __launch_bounds__(256) k_msd_local(const uint64_t* __restrict__ 
     const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (!multi[b]) return;  // empty, or one key: the last pass already put its rows in their place
     const uint32_t lo = first[b], m = end[b] - lo;
+    // this bucket's grouped ids to the side buffer (free after the last pass), read from there below
+    for (uint32_t p = lane; p < m; p += 64) src[lo + p] = ids[lo + p];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's copies land before its lanes read them
     if (msd_wave_partition(keys, src, ids, lo, m, lane, m <= kMsdWaveMax ? 2 : 16)) return;
     if (m > kMsdWaveMax) {
       if (lane == 0) big[atomicAdd(&ctl[kMsdCtlBig], 1u)] = b;
@@ -643,8 +646,8 @@ size_t rs_scratch_bytes(size_t n) {
   // keys x2 (8 B), ids x1 extra (4 B; the other id buffer is the caller's output), histogram, OR/AND,
   // MSD bucket starts + control words + big-bucket list
   return 2 * n * 8 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 1024 +
-         16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows)) + 768 + (4 * (size_t)kMsdBuckets + 8) * 4 +
-         n * 4;  // + the side copy of the grouped ids
+         (size_t)kRsDigits * ((rs_blocks(n) + kScanTiles - 1) / kScanTiles) * 4 + 256 +
+         16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows)) + 768 + (4 * (size_t)kMsdBuckets + 8) * 4;
 }
 
 // the MSD path pays off from 4 LSD passes on (a span of > 24 bits) and enough rows to fill the buckets
@@ -665,7 +668,9 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   uint32_t* ib = (uint32_t*)(kb + n);
   uint32_t* hist = (uint32_t*)(((uintptr_t)(ib + n) + 255) & ~(uintptr_t)255);
   uint32_t* dtot = hist + (size_t)kRsDigits * nb;
-  uint64_t* red = (uint64_t*)(((uintptr_t)(dtot + kRsDigits) + 15) & ~(uintptr_t)15);
+  const size_t nch = (nb + kScanTiles - 1) / kScanTiles;
+  uint32_t* ctot = (uint32_t*)(((uintptr_t)(dtot + kRsDigits) + 255) & ~(uintptr_t)255);
+  uint64_t* red = (uint64_t*)(((uintptr_t)(ctot + (size_t)kRsDigits * nch) + 15) & ~(uintptr_t)15);
   uint64_t* part = red + 2;
   const size_t pb = (n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows);
   uint32_t* mfirst = (uint32_t*)(((uintptr_t)(part + 2 * pb) + 255) & ~(uintptr_t)255);
@@ -673,7 +678,6 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   uint32_t* mmulti = mend + kMsdBuckets;
   uint32_t* mctl = mmulti + kMsdBuckets;  // right after the multi flags: one memset clears both
   uint32_t* mbig = mctl + 8;
-  uint32_t* msrc = (uint32_t*)(((uintptr_t)(mbig + kMsdBuckets) + 255) & ~(uintptr_t)255);
   if (((uintptr_t)col & 15) == 0 && ((uintptr_t)valid & 1) == 0)
     hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
   else
@@ -689,8 +693,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   const int sb = span ? 64 - __builtin_clzll(span) : 0;  // bits of the span
   const bool vbit = valid && n <= (size_t)kRsLack;
   // executed pass j writes ids to fin when (np-1-j) is even, so the last one lands there
-  auto run_passes = [&](const int* shifts, int np, bool keep_keys, uint32_t* fin, uint32_t* tmp,
-                        uint32_t* copy) -> const uint64_t* {
+  auto run_passes = [&](const int* shifts, int np, bool keep_keys, uint32_t* fin, uint32_t* tmp) -> const uint64_t* {
     const uint32_t* ids_in = nullptr;  // identity before the first pass
     const uint64_t* kin = (const uint64_t*)col;  // raw column before the first pass
     uint64_t* kout = ka;
@@ -699,10 +702,10 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
       const bool last = j == np - 1;
       hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)nb), dim3(kRsBlock), 0, st, kin, ids_in, valid, n, shifts[j], last,
                          desc, vbit, kmin, hist, nb);
-      hipLaunchKernelGGL(k_rs_scan_digits, dim3(kRsDigits), dim3(256), 0, st, hist, nb, dtot);
+      hipLaunchKernelGGL(k_rs_scan_tiles, dim3((unsigned)nch), dim3(kScanThreads), 0, st, hist, nb, ctot);
+      hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nch, dtot);
       hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)nb), dim3(kRsBlock), 0, st, kin, ids_in, valid, n, shifts[j],
-                         desc, vbit, last, kmin, hist, dtot, nb, (last && !keep_keys) ? nullptr : kout, ids_out,
-                         last ? copy : nullptr);
+                         desc, vbit, last, kmin, hist, ctot, dtot, nb, (last && !keep_keys) ? nullptr : kout, ids_out);
       kin = kout;
       kout = kout == ka ? kb : ka;
       ids_in = ids_out;
@@ -712,15 +715,16 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   if (msd_enabled(n, sb)) {
     const int s1 = sb - kMsdBits;
     const int shifts[2] = {s1, sb - 8};
-    // grouped ids -> out_ids (one-key buckets are final there) and the side copy msrc
-    const uint64_t* sorted = run_passes(shifts, 2, true, out_ids, ib, msrc);
+    // grouped ids -> out_ids (one-key buckets are final there); ib (the first pass's ids) is then free
+    // and serves as the side copy of the multi-key buckets (k_msd_local)
+    const uint64_t* sorted = run_passes(shifts, 2, true, out_ids, ib);
     if ((e = hipMemsetAsync(mmulti, 0, (kMsdBuckets + 8) * 4, st)) != hipSuccess) return e;  // flags + control
     const size_t nbd = (n + 256 * kMsdBoundsRows - 1) / (256 * kMsdBoundsRows);  // over <= n holder rows
     hipLaunchKernelGGL(k_msd_bounds, dim3((unsigned)nbd), dim3(256), 0, st, sorted, n, s1, dtot, desc, valid != nullptr,
                        mfirst, mend, mmulti);
-    hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / 4), dim3(256), 0, st, sorted, msrc, out_ids, mfirst, mend, mmulti,
+    hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / 4), dim3(256), 0, st, sorted, ib, out_ids, mfirst, mend, mmulti,
                        s1, mctl, mbig);
-    hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, sorted, msrc, out_ids, mfirst, mend, s1, mctl,
+    hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, sorted, ib, out_ids, mfirst, mend, s1, mctl,
                        mbig);
     uint32_t hctl[2];
     if ((e = hipMemcpyAsync(hctl, mctl, sizeof(hctl), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
@@ -735,7 +739,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     hipLaunchKernelGGL(k_rs_iota, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out_ids, n);
     return hipGetLastError();
   }
-  run_passes(shifts, np, false, out_ids, ib, nullptr);
+  run_passes(shifts, np, false, out_ids, ib);
   return hipGetLastError();
 }
 
