@@ -506,9 +506,10 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 }
 
 // Stable partition of bucket [lo, lo + m) by distinct key, at most max_rounds rounds; returns whether
-// every row was written. Round: 8 chunks of 64 rows in flight, the rows whose key is cur compacted by
+// every row was written. Round: kPartRows chunks of 64 rows in flight, the rows whose key is cur compacted by
 // ballot, the next larger key found on the way. The first round takes cur = the bucket's first key
 // (a one-key bucket is then a single copy); a smaller key seen in it restarts from the smallest.
+constexpr int kPartRows = 16;  // rows per lane in flight (8: the same kernel time within noise)
 __device__ __forceinline__ bool msd_wave_partition(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ src,
                                                    uint32_t* __restrict__ ids, uint32_t lo, uint32_t m, int lane,
                                                    int max_rounds) {
@@ -518,17 +519,17 @@ __device__ __forceinline__ bool msd_wave_partition(const uint64_t* __restrict__ 
   bool restarted = false;
   for (int round = 0; round < max_rounds; ++round) {
     uint64_t nxt = ~0ull, below = ~0ull;
-    for (uint32_t p0 = 0; p0 < m; p0 += 512) {
-      uint64_t k[8];
-      uint32_t id[8];
+    for (uint32_t p0 = 0; p0 < m; p0 += 64 * kPartRows) {
+      uint64_t k[kPartRows];
+      uint32_t id[kPartRows];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
+      for (int r = 0; r < kPartRows; ++r) {
         const uint32_t pos = min(p0 + (uint32_t)(r * 64 + lane), m - 1);
         k[r] = keys[lo + pos];
         id[r] = src[lo + pos];
       }
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
+      for (int r = 0; r < kPartRows; ++r) {
         const bool in = p0 + (uint32_t)(r * 64) + lane < m;
         const bool hit = in && k[r] == cur;
         const uint64_t bal = __ballot(hit);
@@ -584,7 +585,19 @@ __global__ void __launch_bounds__(256) k_msd_local(const uint64_t* __restrict__ 
     if (!multi[b]) return;  // empty, or one key: the last pass already put its rows in their place
     const uint32_t lo = first[b], m = end[b] - lo;
     // this bucket's grouped ids to the side buffer (free after the last pass), read from there below
-    for (uint32_t p = lane; p < m; p += 64) src[lo + p] = ids[lo + p];
+    for (uint32_t p0 = 0; p0 < m; p0 += 512) {  // 8 loads in flight per lane, then their stores
+      uint32_t v[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const uint32_t p = p0 + (uint32_t)(r * 64 + lane);
+        v[r] = p < m ? ids[lo + p] : 0u;
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const uint32_t p = p0 + (uint32_t)(r * 64 + lane);
+        if (p < m) src[lo + p] = v[r];
+      }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's copies land before its lanes read them
     if (msd_wave_partition(keys, src, ids, lo, m, lane, m <= kMsdWaveMax ? 2 : 16)) return;
     if (m > kMsdWaveMax) {

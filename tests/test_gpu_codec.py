@@ -160,3 +160,29 @@ def test_sum_all_dec_string_rows_parallel_chunks(eng, keys):
     for x in xs:
         want = want * x % N
     assert eng.sum_all_dec(rows, str(N)) == str(want)
+
+
+def test_sum_all_dec_two_chunks(eng, keys):
+    """dds_sum_all_dec splits a request of fewer than 2^19 rows into two chunks (the second one's
+    copies overlap the first one's parse, 4 lanes per row for these small batches): the fold over
+    12,001 rows equals the oracle's, and a malformed row or a negative / >= 2N row in the second chunk
+    is handled as in the first (NumberFormatException names the row; BigInteger.mod semantics)."""
+    from oracle import homo
+    N = keys["paillier1024_seed1"]["nsquare"]
+    rng = np.random.default_rng(12)
+    n = 12_001
+    xs = [int(rng.integers(1, 2**62)) * int(rng.integers(1, 2**62)) % N for _ in range(n)]
+    xs[8000] = -xs[8000]            # negative row in the second chunk
+    xs[9000] = xs[9000] + 3 * N     # row >= 2N in the second chunk
+    xs[11] = N - 1
+    rows = [str(x) for x in xs]
+    want = 1
+    for x in xs:
+        want = want * (x % N) % N
+    assert int(eng.sum_all_dec(rows, str(N))) == want == homo.modmul_fold([x % N for x in xs], N)
+    bad = list(rows)
+    bad[9500] = "12x4"
+    with pytest.raises(ddshe.DDSError) as ei:
+        eng.sum_all_dec(bad, str(N))
+    assert ei.value.status == ddshe.DDS_E_FORMAT
+    assert "9500" in str(ei.value)
