@@ -356,8 +356,9 @@ int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const 
   }
   const int S3 = mc.S3;
   const int64_t E = lt.E - mc.wS3() * ((int64_t)lt.n - 1);  // n-1 tree products, R3^-1 each
-  // nodes (2n + 2 rows) + two level buffers (n rows each, multi-launch trees) + flags (2n + 2 words)
-  HIP_TRY(w->tree.ensure(((4 * lt.n + 2) * (size_t)S3 + 2 * lt.n + 2) * 4));
+  // nodes (2n + 2 rows) + two level buffers (n rows each, multi-launch trees) + flags (2n + 4 words: the
+  // final launch may count Y as one more leaf)
+  HIP_TRY(w->tree.ensure(((4 * lt.n + 2) * (size_t)S3 + 2 * lt.n + 4) * 4));
   uint32_t* nodes = w->tree.as<uint32_t>();
   uint32_t* tflags = nodes + (4 * lt.n + 2) * (size_t)S3;
   HIP_TRY(w->out.ensure((size_t)std::max(S2, S3) * 4));

@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(NT) k_tree(const uint32_t* __restrict__ X, siz
                                                        uint32_t* __restrict__ flags, uint32_t* __restrict__ out, int Sout,
                                                        int Wout, int max_levels, uint32_t* __restrict__ lvl_out,
                                                        int fence_mode, uint64_t* __restrict__ stamps,
-                                                       uint32_t* __restrict__ clear, size_t nclear) {
+                                                       uint32_t* __restrict__ clear, size_t nclear, int yleaf) {
   using O = Sos<S, W>;
   // the next launch's hand-off counters, zeroed here instead of by a separate memset launch
   for (size_t j = (size_t)blockIdx.x * NT + threadIdx.x; j < nclear; j += (size_t)gridDim.x * NT) clear[j] = 0u;
@@ -292,18 +292,23 @@ __global__ void __launch_bounds__(NT) k_tree(const uint32_t* __restrict__ X, siz
   const int tid = threadIdx.x;
   const size_t b = blockIdx.x;
   const bool pair = 2 * b + 1 < nleaves;
+  // yleaf: the last leaf (index nleaves - 1) is Y, in this radix (the finalising factor enters as a
+  // leaf instead of as a product after the root: same product count, one product less in sequence)
+  const size_t nx = nleaves - (yleaf ? 1 : 0);  // leaves from X
+  const bool y0 = yleaf && 2 * b == nx, y1 = yleaf && 2 * b + 1 == nx;
+  const int n0 = y0 ? S : Sin, n1 = y1 ? S : Sin;  // words of each leaf
   // the leaves' words first (Sin <= S + 64), so their global loads are in flight together with the
   // constants' below: one memory round trip instead of two
   constexpr int LW = (S + 64 + NT - 1) / NT;  // leaf words per thread
   uint32_t lw0[LW], lw1[LW];
   {
-    const size_t r0 = ids ? (size_t)ids[2 * b] : 2 * b;
-    const size_t r1 = pair ? (ids ? (size_t)ids[2 * b + 1] : 2 * b + 1) : r0;
+    const size_t r0 = y0 ? 0 : (ids ? (size_t)ids[2 * b] : 2 * b);
+    const size_t r1 = (pair && !y1) ? (ids ? (size_t)ids[2 * b + 1] : 2 * b + 1) : r0;
 #pragma unroll
     for (int q = 0; q < LW; ++q) {
       const int j = tid + q * NT;
-      lw0[q] = j < Sin ? X[(size_t)j * xstride + r0 * gstride] : 0u;
-      lw1[q] = (pair && j < Sin) ? X[(size_t)j * xstride + r1 * gstride] : 0u;
+      lw0[q] = j < n0 ? (y0 ? Y[j] : X[(size_t)j * xstride + r0 * gstride]) : 0u;
+      lw1[q] = (pair && j < n1) ? (y1 ? Y[j] : X[(size_t)j * xstride + r1 * gstride]) : 0u;
     }
   }
   for (int j = tid; j < O::YTOT; j += NT) {
@@ -323,22 +328,16 @@ __global__ void __launch_bounds__(NT) k_tree(const uint32_t* __restrict__ X, siz
 #pragma unroll
     for (int q = 0; q < LW; ++q) {
       const int j = tid + q * NT;
-      if (j < Sin) {
-        stmp[j] = lw0[q];
-        stmp2[j] = lw1[q];
-      }
+      if (j < n0) stmp[j] = lw0[q];
+      if (j < n1) stmp2[j] = lw1[q];
     }
     __syncthreads();
-    if (Sin == S && Win == W) {  // a previous launch's nodes: redundant limbs (< 2^W + 3), kept as they are
-      for (int j = tid; j < S; j += NT) {
-        sa[j] = stmp[j];
-        if (pair) sb[j] = stmp2[j];
-      }
-    } else {  // rows / first-level partials: normalised limbs of another radix
-      for (int j = tid; j < S; j += NT) {
-        sa[j] = repack_limb(stmp, Sin, Win, W, j);
-        if (pair) sb[j] = repack_limb(stmp2, Sin, Win, W, j);
-      }
+    // a previous launch's nodes (and Y) are in this radix: redundant limbs (< 2^W + 3), kept as they
+    // are; rows / first-level partials are normalised limbs of another radix
+    const bool same = Sin == S && Win == W;
+    for (int j = tid; j < S; j += NT) {
+      sa[j] = (same || y0) ? stmp[j] : repack_limb(stmp, Sin, Win, W, j);
+      if (pair) sb[j] = (same || y1) ? stmp2[j] : repack_limb(stmp2, Sin, Win, W, j);
     }
     __syncthreads();
   }
@@ -401,7 +400,7 @@ __global__ void __launch_bounds__(NT) k_tree(const uint32_t* __restrict__ X, siz
     ++h;
   }
   // root
-  if (Y) {
+  if (Y && !yleaf) {
     for (int j = tid; j < S; j += NT) sb[j] = Y[j];
     __syncthreads();
     sp.mark();
@@ -562,9 +561,13 @@ hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Wi
     const bool wide_level = blocks > wide;  // 256-thread workgroups, one level
     const int lv = wide_level ? 1 : levels;
     const bool last = lv <= 0 || nleaves <= ((size_t)1 << lv);
-    const bool handoff = nleaves > 2 && (last ? lv != 1 : lv > 1);  // hand-offs happen in this launch
+    // the launch that walks to the root with in-kernel hand-offs takes Y as one more leaf (not for
+    // <= 2 leaves: the extra leaf would add the hand-off and its counter reset to a one-product tree)
+    const int yleaf = (last && Y && lv != 1 && nleaves > 2) ? 1 : 0;
+    const size_t nl = nleaves + yleaf;
+    const bool handoff = nl > 2 && (last ? lv != 1 : lv > 1);  // hand-offs happen in this launch
     if (handoff && !flags_clear) {
-      hipError_t e = hipMemsetAsync(flags, 0, (2 * nleaves + 2) * 4, st);
+      hipError_t e = hipMemsetAsync(flags, 0, (2 * nl + 2) * 4, st);
       if (e != hipSuccess) return e;
     }
     flags_clear = false;
@@ -573,12 +576,13 @@ hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Wi
       const size_t nn = (nleaves + 1) >> 1, nb = (nn + 1) / 2;
       const int nlv = nb > wide ? 1 : levels;
       const bool nlast = nlv <= 0 || nn <= ((size_t)1 << nlv);
-      const size_t nclear = (nn > 2 && (nlast ? nlv != 1 : nlv > 1)) ? 2 * nn + 2 : 0;
+      const size_t nnl = nn + ((nlast && Y && nlv != 1 && nn > 2) ? 1 : 0);  // its leaves, Y included
+      const size_t nclear = (nnl > 2 && (nlast ? nlv != 1 : nlv > 1)) ? 2 * nnl + 2 : 0;
       flags_clear = nclear != 0;
       DDSHE_TREE_SWITCH(S, hipLaunchKernelGGL((k_tree<S, W, kTreeWideThreads>), dim3((unsigned)blocks),
                                               dim3(kTreeWideThreads), 0, st, X, xstride, gstride, Sin, Win, nleaves,
                                               ids, consts, Y, nodes, flags, out, Sout, Wout, last ? 0 : 1, lvl[flip],
-                                              fence, stamping ? d_st : nullptr, flags, nclear));
+                                              fence, stamping ? d_st : nullptr, flags, nclear, 0));
     } else {
       const size_t dyn = handoff ? kOneWgPerCuLds : 0;
       DDSHE_TREE_SWITCH(S, {
@@ -586,9 +590,9 @@ hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Wi
             reinterpret_cast<const void*>(&k_tree<S, W, kTreeThreads>), hipFuncAttributeMaxDynamicSharedMemorySize,
             (int)kOneWgPerCuLds);
         (void)attr;
-        hipLaunchKernelGGL((k_tree<S, W, kTreeThreads>), dim3((unsigned)blocks), dim3(kTreeThreads), dyn, st, X,
-                           xstride, gstride, Sin, Win, nleaves, ids, consts, Y, nodes, flags, out, Sout, Wout,
-                           last ? 0 : lv, lvl[flip], fence, stamping ? d_st : nullptr, nullptr, (size_t)0);
+        hipLaunchKernelGGL((k_tree<S, W, kTreeThreads>), dim3((unsigned)((nl + 1) / 2)), dim3(kTreeThreads), dyn, st,
+                           X, xstride, gstride, Sin, Win, nl, ids, consts, Y, nodes, flags, out, Sout, Wout,
+                           last ? 0 : lv, lvl[flip], fence, stamping ? d_st : nullptr, nullptr, (size_t)0, yleaf);
       });
     }
     hipError_t e = hipGetLastError();
