@@ -176,6 +176,12 @@ class NotFound(DDSError):
     """DDS_E_EMPTY: the reference route answers HTTP 404."""
 
 
+def _be_int(buf, n: int) -> int:
+    """Big-endian integer from the first n bytes of a ctypes buffer (one memcpy; slicing a ctypes array
+    builds a Python list of ints first)."""
+    return int.from_bytes(C.string_at(C.addressof(buf), n), "big")
+
+
 def _check(rc: int, where: str):
     if rc == DDS_E_EMPTY:
         raise NotFound(rc, where)
@@ -287,7 +293,7 @@ class Engine:
         out = (C.c_uint8 * max(width, mb))()
         olen = C.c_size_t()
         _check(fn(self._h, int_to_be(modulus, mb), mb, buf, width, len(ops), out, len(out), C.byref(olen)), fn.__name__)
-        return int.from_bytes(bytes(out[: olen.value]), "big")
+        return _be_int(out, olen.value)
 
     def fold_buffer(self, modulus: int, buf: np.ndarray) -> int:
         """dds_modmul_fold over a host buffer of fixed-width big-endian rows (uint8 [count, width]):
@@ -299,7 +305,7 @@ class Engine:
         olen = C.c_size_t()
         _check(_lib.dds_modmul_fold(self._h, int_to_be(modulus, mb), mb, buf.ctypes.data, width, count, out, len(out),
                                     C.byref(olen)), "dds_modmul_fold")
-        return int.from_bytes(bytes(out[: olen.value]), "big")
+        return _be_int(out, olen.value)
 
     def modmul_fold(self, modulus: int, ops, width=None) -> int:
         return self._fold(_lib.dds_modmul_fold, modulus, ops, width)
@@ -330,7 +336,7 @@ class Engine:
         olen = C.c_size_t()
         _check(_lib.dds_bigint_sum(self._h, ints_to_be(ops, width), width, len(ops), out, len(out), C.byref(olen)),
                "dds_bigint_sum")
-        return int.from_bytes(bytes(out[: olen.value]), "big")
+        return _be_int(out, olen.value)
 
     def bigint_product(self, ops) -> int:
         """Unbounded product (MultAll without pubkey, DDSRestServer.scala:520)."""
@@ -340,7 +346,7 @@ class Engine:
         olen = C.c_size_t()
         _check(_lib.dds_bigint_product(self._h, ints_to_be(ops, width), width, len(ops), out, len(out),
                                        C.byref(olen)), "dds_bigint_product")
-        return int.from_bytes(bytes(out[: olen.value]), "big")
+        return _be_int(out, olen.value)
 
     # ---- decimal route entry points ----
     def _dec(self, fn, values, modulus: str | None) -> str:
@@ -467,7 +473,7 @@ class Engine:
         _check(_lib.dds_combine_partials_device(self._h, int_to_be(modulus, mb), mb, C.c_void_p(d_partials),
                                                 rows.ctypes.data_as(_u64p), len(rows), out, mb, C.byref(olen)),
                "dds_combine_partials_device")
-        return int.from_bytes(bytes(out[: olen.value]), "big")
+        return _be_int(out, olen.value)
 
     def combine_partials(self, modulus: int, partials: np.ndarray, rows) -> int:
         partials = np.ascontiguousarray(partials, dtype=np.uint32)
@@ -479,7 +485,7 @@ class Engine:
                                          partials.ctypes.data_as(C.POINTER(C.c_uint32)),
                                          rows.ctypes.data_as(C.POINTER(C.c_uint64)), len(rows), out, mb,
                                          C.byref(olen)), "dds_combine_partials")
-        return int.from_bytes(bytes(out[: olen.value]), "big")
+        return _be_int(out, olen.value)
 
 
 class Column(_Mutable):
@@ -549,7 +555,7 @@ class Column(_Mutable):
         out = (C.c_uint8 * (self.mb + 4096))()  # a one-row fold returns the operand, which may be wider
         olen = C.c_size_t()
         _check(_lib.dds_col_fold(self._h, first, count, out, len(out), C.byref(olen)), "dds_col_fold")
-        return int.from_bytes(bytes(out[: olen.value]), "big")
+        return _be_int(out, olen.value)
 
     def fold_rows(self, row_ids) -> int:
         """dds_col_fold_rows: SumAll/MultAll over the rows row_ids (a one-row fold returns the operand
@@ -559,7 +565,7 @@ class Column(_Mutable):
         olen = C.c_size_t()
         _check(_lib.dds_col_fold_rows(self._h, ids.ctypes.data_as(_u64p), len(ids), out, len(out), C.byref(olen)),
                "dds_col_fold_rows")
-        return int.from_bytes(bytes(out[: olen.value]), "big")
+        return _be_int(out, olen.value)
 
     def fold_dec(self, row_ids=None, count: int | None = None) -> str:
         """dds_col_fold_dec: the route's decimal reply over row_ids (or rows [0, count))."""
@@ -794,7 +800,7 @@ class MColumn(_Mutable):
         out = (C.c_uint8 * (self.mb + 4096))()
         olen = C.c_size_t()
         _check(_lib.dds_mcol_fold(self._h, out, len(out), C.byref(olen)), "dds_mcol_fold")
-        return int.from_bytes(bytes(out[: olen.value]), "big")
+        return _be_int(out, olen.value)
 
     def fold_rows(self, row_ids) -> int:
         ids = np.ascontiguousarray(row_ids, dtype=np.uint64)
@@ -802,7 +808,7 @@ class MColumn(_Mutable):
         olen = C.c_size_t()
         _check(_lib.dds_mcol_fold_rows(self._h, ids.ctypes.data_as(_u64p), len(ids), out, len(out), C.byref(olen)),
                "dds_mcol_fold_rows")
-        return int.from_bytes(bytes(out[: olen.value]), "big")
+        return _be_int(out, olen.value)
 
     def fold_dec(self, row_ids=None) -> str:
         ids = None if row_ids is None else np.ascontiguousarray(row_ids, dtype=np.uint64)
