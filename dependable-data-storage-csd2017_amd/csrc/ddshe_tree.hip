@@ -494,7 +494,8 @@ Shape tree_shape(size_t mod_bits) {
 // Launch plan of a tree over n leaves:
 //   * wide levels (more than DDSHE_TREE_WIDE blocks, default 256 = one per CU): one level per launch on
 //     256-thread workgroups (k_tree<S, W, 256>): 8 products resident per CU instead of 1-2, each product
-//     slower than on 1024 threads but the level finishes in fewer rounds;
+//     slower than on 1024 threads but the level finishes in fewer rounds (512-thread workgroups for the
+//     levels of <= 1024 blocks measured the same, tools/tree_sweep.sh);
 //   * the rest on 1024-thread workgroups, DDSHE_TREE_LEVELS levels per launch (0 = to the root).
 //     With in-kernel hand-offs (LEVELS != 1) the node words are handed over in the form MI355X_MICROARCH.md
 //     (§ inter-workgroup visibility, "Valid forms", first table row) lists as measured valid: every node

@@ -1,12 +1,7 @@
 #!/bin/bash
 # tail sweeps (tools/tree_ab.py, each variant in its own process): launch plan of the reduction tree
 cd /root/repo
-for v in "DDSHE_TREE_LEVELS=1 DDSHE_TREE_FENCE=1 DDSHE_TREE_SWITCH=1024 DDSHE_TREE_WIDE=100000" \
-         "DDSHE_TREE_LEVELS=0 DDSHE_TREE_FENCE=2 DDSHE_TREE_SWITCH=8192 DDSHE_TREE_WIDE=256" \
-         "DDSHE_TREE_LEVELS=0 DDSHE_TREE_FENCE=2 DDSHE_TREE_SWITCH=8192 DDSHE_TREE_WIDE=512" \
-         "DDSHE_TREE_LEVELS=0 DDSHE_TREE_FENCE=2 DDSHE_TREE_SWITCH=8192 DDSHE_TREE_WIDE=160" \
-         "DDSHE_TREE_LEVELS=0 DDSHE_TREE_FENCE=2 DDSHE_TREE_SWITCH=16384 DDSHE_TREE_WIDE=256" \
-         "DDSHE_TREE_LEVELS=0 DDSHE_TREE_FENCE=2 DDSHE_TREE_SWITCH=4096 DDSHE_TREE_WIDE=256"; do
+for v in "DDSHE_TREE_MID=0" "DDSHE_TREE_MID=256" "DDSHE_TREE_MID=0" "DDSHE_TREE_MID=256" "DDSHE_TREE_MID=128"; do
   echo "== $v"
   env $v timeout -k 5 120 python -u tools/tree_ab.py || exit 1
 done
