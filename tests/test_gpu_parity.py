@@ -388,3 +388,19 @@ def test_tree_handoff_repeated_folds(eng, keys, key_name):
         for _ in range(12):
             assert col.fold(0, count) == first, count
     col.close()
+
+
+def test_config2_full_size_fold(eng, keys):
+    """BASELINE.json config 2 at its full size inside the test suite (not only in bench.py): 10M
+    synthetic Paillier ciphertexts under the committed 2048-bit key, resident on the GPU (5.9 GB), one
+    SumAll fold; Dec(fold) == sum of the plaintexts, and a 300-row prefix fold equals the oracle's."""
+    import ddshe
+    k = keys["paillier2048_committed"]
+    count = 10_000_000
+    col = eng.column(k["nsquare"], count)
+    col.fill_paillier_synth(k["n"], k["g"], seed=1, row0=0, count=count, pool=1024)
+    ms = ddshe.synth_plaintexts(1, 0, count)
+    assert homo.paillier_decrypt(col.fold(), k) == int(ms.astype(np.int64).sum()) % k["n"]
+    sample = col.read(0, 300)
+    assert col.fold(0, 300) == homo.modmul_fold(sample, k["nsquare"])
+    col.close()
