@@ -2282,10 +2282,23 @@ struct dds_strtab {
   uint8_t* chars = nullptr;
   uint64_t *elem_off = nullptr, *row_off = nullptr;
   uint32_t* fp = nullptr;  // per-element 32-bit fingerprint
+  // SearchEq's position-major indexes (k_str_posfp), built on the first query at a position; the
+  // kPosIdx most recent positions are kept
+  struct PosIdx {
+    uint64_t position = 0;
+    uint32_t* fp = nullptr;
+    uint64_t* present = nullptr;
+  };
+  static constexpr size_t kPosIdx = 8;
+  std::vector<PosIdx> pos;  // most recent last
   std::mutex mu;
   ~dds_strtab() {
     for (void* p : {(void*)chars, (void*)elem_off, (void*)row_off, (void*)fp})
       if (p) (void)hipFree(p);
+    for (auto& x : pos) {
+      if (x.fp) (void)hipFree(x.fp);
+      if (x.present) (void)hipFree(x.present);
+    }
   }
 };
 
@@ -2359,9 +2372,35 @@ int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values
   if (!nb.empty()) HIP_TRY(hipMemcpyAsync(w->in2.p, nb.data(), nb.size(), hipMemcpyHostToDevice, wl.st));
   record_time(ctx, w, wl.st, true, 2);
   uint32_t* flags = w->x.as<uint32_t>();
-  if (mode == 0) {
-    HIP_TRY(launch_str_eq(t->row_off + row0, nrows, t->elem_off, t->chars, t->fp, w->in2.as<uint8_t>(), nd, position,
-                          negate, flags, wl.st));
+  if (mode == 0) {  // SearchEq / NEq: over the position-major index of `position` (built on first use)
+    dds_strtab::PosIdx* px = nullptr;
+    for (auto it = t->pos.begin(); it != t->pos.end(); ++it)
+      if (it->position == position) {
+        const dds_strtab::PosIdx x = *it;  // most recent last
+        t->pos.erase(it);
+        t->pos.push_back(x);
+        px = &t->pos.back();
+        break;
+      }
+    if (!px) {
+      if (t->pos.size() >= dds_strtab::kPosIdx) {  // evict the least recent (its last query has synchronised)
+        (void)hipFree(t->pos.front().fp);
+        (void)hipFree(t->pos.front().present);
+        t->pos.erase(t->pos.begin());
+      }
+      dds_strtab::PosIdx x;
+      x.position = position;
+      if (hipMalloc(&x.fp, std::max<size_t>(t->nrows, 1) * 4) != hipSuccess) return fail(DDS_E_NOMEM, "position index");
+      if (hipMalloc(&x.present, ((t->nrows + 63) / 64 + 1) * 8) != hipSuccess) {
+        (void)hipFree(x.fp);
+        return fail(DDS_E_NOMEM, "position index");
+      }
+      t->pos.push_back(x);
+      px = &t->pos.back();
+      HIP_TRY(launch_str_posfp(t->row_off, t->nrows, t->fp, position, px->fp, px->present, wl.st));
+    }
+    HIP_TRY(launch_str_eq_pos(px->fp, px->present, row0, nrows, t->row_off, t->elem_off, t->chars,
+                              w->in2.as<uint8_t>(), nd, position, negate, flags, wl.st));
   } else {
     uint64_t e_first = 0, e_last = 0;  // element range of rows [row0, row0 + nrows)
     HIP_TRY(hipMemcpy(&e_first, t->row_off + row0, 8, hipMemcpyDeviceToHost));

@@ -164,6 +164,13 @@ hipError_t launch_str_eq(const uint64_t* row_off, size_t nrows, const uint64_t* 
                          int negate, uint32_t* flags, hipStream_t st);
 // SearchEntry/OR/AND/IsElement: flags[row] |= bit j for every element equal to needle j (flags zeroed
 // by the launcher); elements [e_first, e_first + nelems), rows [0, nrows) of row_off
+// SearchEq's position-major index and the query over it (ddshe_strscan.hip)
+hipError_t launch_str_posfp(const uint64_t* row_off, size_t nrows, const uint32_t* fp, uint64_t position,
+                            uint32_t* posfp, uint64_t* present, hipStream_t st);
+hipError_t launch_str_eq_pos(const uint32_t* posfp, const uint64_t* present, size_t row0, size_t nrows,
+                             const uint64_t* row_off, const uint64_t* elem_off, const uint8_t* chars,
+                             const uint8_t* nchars, const StrNeedles& nd, uint64_t position, int negate,
+                             uint32_t* flags, hipStream_t st);
 hipError_t launch_str_any(const uint32_t* fp, uint64_t e_first, size_t nelems, const uint64_t* row_off, size_t nrows,
                           const uint64_t* elem_off, const uint8_t* chars, const uint8_t* nchars, const StrNeedles& nd,
                           uint32_t* flags, hipStream_t st);

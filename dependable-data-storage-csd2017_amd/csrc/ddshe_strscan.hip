@@ -58,6 +58,39 @@ __global__ void k_str_eq(const uint64_t* __restrict__ row_off, size_t nrows, con
   flags[r] = f;
 }
 
+// SearchEq's position-major index (built on the first query at a position, kept with the table):
+// posfp[r] = fingerprint of row r's element `position`, present bit r = the row passes the route's
+// strict guard (length - 1 > position, DDSRestServer.scala:615). A query then reads 4 B per row,
+// coalesced, instead of gathering one 4-byte fingerprint per 32-byte sector (plus 8 B of row
+// offsets); only fingerprint hits touch the row offsets and the bytes.
+__global__ void k_str_posfp(const uint64_t* __restrict__ row_off, size_t nrows, const uint32_t* __restrict__ fp,
+                            uint64_t position, uint32_t* __restrict__ posfp, uint64_t* __restrict__ present) {
+  const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool pres = false;
+  if (r < nrows) {
+    const uint64_t e0 = row_off[r], e1 = row_off[r + 1];
+    pres = e1 - e0 > position + 1;
+    posfp[r] = pres ? fp[e0 + position] : 0u;
+  }
+  const uint64_t m = __ballot(pres);
+  if ((threadIdx.x & 63) == 0 && r < nrows) present[r >> 6] = m;  // r: the wave's first row, a multiple of 64
+}
+
+__global__ void k_str_eq_pos(const uint32_t* __restrict__ posfp, const uint64_t* __restrict__ present, size_t row0,
+                             size_t nrows, const uint64_t* __restrict__ row_off, const uint64_t* __restrict__ elem_off,
+                             const uint8_t* __restrict__ chars, const uint8_t* __restrict__ nchars, StrNeedles nd,
+                             uint64_t position, int negate, uint32_t* __restrict__ flags) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrows) return;
+  const size_t r = row0 + i;
+  uint32_t f = 0;
+  if ((present[r >> 6] >> (r & 63)) & 1ull) {
+    const bool eq = posfp[r] == (uint32_t)(nd.h[0] >> 32) && str_hit(row_off[r] + position, 0, elem_off, chars, nchars, nd);
+    f = eq != (negate != 0);
+  }
+  flags[i] = f;
+}
+
 // row holding element e: last r with row_off[r] <= e (row_off ascending, rows may be empty)
 __device__ __forceinline__ size_t row_of(const uint64_t* __restrict__ row_off, size_t nrows, uint64_t e) {
   size_t lo = 0, hi = nrows;  // invariant: row_off[lo] <= e < row_off[hi]
@@ -115,6 +148,24 @@ hipError_t launch_str_eq(const uint64_t* row_off, size_t nrows, const uint64_t* 
   if (nrows == 0) return hipSuccess;
   hipLaunchKernelGGL(k_str_eq, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, st, row_off, nrows, elem_off,
                      chars, fp, nchars, nd, position, negate, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_str_posfp(const uint64_t* row_off, size_t nrows, const uint32_t* fp, uint64_t position,
+                            uint32_t* posfp, uint64_t* present, hipStream_t st) {
+  if (nrows == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_str_posfp, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, st, row_off, nrows, fp, position,
+                     posfp, present);
+  return hipGetLastError();
+}
+
+hipError_t launch_str_eq_pos(const uint32_t* posfp, const uint64_t* present, size_t row0, size_t nrows,
+                             const uint64_t* row_off, const uint64_t* elem_off, const uint8_t* chars,
+                             const uint8_t* nchars, const StrNeedles& nd, uint64_t position, int negate,
+                             uint32_t* flags, hipStream_t st) {
+  if (nrows == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_str_eq_pos, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, st, posfp, present, row0,
+                     nrows, row_off, elem_off, chars, nchars, nd, position, negate, flags);
   return hipGetLastError();
 }
 

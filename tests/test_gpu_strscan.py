@@ -80,3 +80,21 @@ def test_search_large_table(eng):
     want_eq = np.array([i for i, r in enumerate(rows) if len(r) - 1 > 0 and r[0] == target], dtype=np.uint32)
     assert np.array_equal(tab.search_eq(0, target), want_eq)
     tab.close()
+
+
+def test_search_eq_position_index_resident(eng):
+    """SearchEq / NEq on a resident table read a position-major fingerprint index built on the first
+    query at each position (at most 8 kept): 11 positions queried twice (evictions and rebuilds),
+    rows shorter than the position (the strict guard length - 1 > position) never match."""
+    rng = random.Random(21)
+    words = [format(rng.getrandbits(40), "x") for _ in range(6)] + ["", "7"]
+    rows = [[rng.choice(words) for _ in range(rng.randrange(0, 13))] for _ in range(20_003)]
+    tab = eng.strtab(rows)
+    for rep in range(2):
+        for position in range(11):
+            value = words[(position + rep) % len(words)]
+            for negate in (False, True):
+                want = np.array([i for i, r in enumerate(rows)
+                                 if len(r) - 1 > position and (r[position] == value) != negate], dtype=np.uint32)
+                assert np.array_equal(tab.search_eq(position, value, negate), want), (rep, position, negate)
+    tab.close()
