@@ -2399,8 +2399,10 @@ int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values
       px = &t->pos.back();
       HIP_TRY(launch_str_posfp(t->row_off, t->nrows, t->fp, position, px->fp, px->present, wl.st));
     }
-    HIP_TRY(launch_str_eq_pos(px->fp, px->present, row0, nrows, t->row_off, t->elem_off, t->chars,
-                              w->in2.as<uint8_t>(), nd, position, negate, flags, wl.st));
+    uint32_t* dst = device_out ? out_rows : w->out.as<uint32_t>();
+    HIP_TRY(launch_str_eq_compact(px->fp, px->present, row0, nrows, t->row_off, t->elem_off, t->chars,
+                                  w->in2.as<uint8_t>(), nd, position, negate, w->misc.p, w->flags.as<uint64_t>(), dst,
+                                  wl.st));
   } else {
     uint64_t e_first = 0, e_last = 0;  // element range of rows [row0, row0 + nrows)
     HIP_TRY(hipMemcpy(&e_first, t->row_off + row0, 8, hipMemcpyDeviceToHost));
@@ -2413,8 +2415,10 @@ int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values
                            w->in2.as<uint8_t>(), nd, flags, wl.st));
   }
   uint32_t* dst = device_out ? out_rows : w->out.as<uint32_t>();
-  const uint32_t req = mode == 2 ? (1u << nvalues) - 1u : 0u;
-  HIP_TRY(launch_flag_compact(flags, nrows, req, w->misc.p, w->flags.as<uint64_t>(), dst, wl.st));
+  if (mode != 0) {  // SearchEq compacted above, straight from its position index
+    const uint32_t req = mode == 2 ? (1u << nvalues) - 1u : 0u;
+    HIP_TRY(launch_flag_compact(flags, nrows, req, w->misc.p, w->flags.as<uint64_t>(), dst, wl.st));
+  }
   record_time(ctx, w, wl.st, false, 2);
   uint64_t total = 0;
   HIP_TRY(read_sync(w, wl.st, w->flags.p, &total, 8));

@@ -685,6 +685,59 @@ __global__ void __launch_bounds__(kOpeBlock) k_flag_count(const uint32_t* __rest
   ope_store_mask(m, masks, counts, blockIdx.x);
 }
 
+// SearchEq/NEq front end (ddshe_strscan.hip's position index): same tile layout and masks as
+// k_ope_count; row r = row0 + i matches iff its present bit is set (length - 1 > position) and its
+// fingerprint equals the needle's (bytes verified on a hit), xor negate. Reads 4 B + 1 bit per row and
+// writes no per-row flags.
+__global__ void __launch_bounds__(kOpeBlock) k_str_eq_count(const uint32_t* __restrict__ posfp,
+                                                            const uint64_t* __restrict__ present, size_t row0, size_t n,
+                                                            const uint64_t* __restrict__ row_off,
+                                                            const uint64_t* __restrict__ elem_off,
+                                                            const uint8_t* __restrict__ chars,
+                                                            const uint8_t* __restrict__ nchars, StrNeedles nd,
+                                                            uint64_t position, int negate,
+                                                            uint32_t* __restrict__ masks,
+                                                            uint32_t* __restrict__ counts) {
+  const size_t t0 = (size_t)blockIdx.x * kOpeTile + 4 * (size_t)threadIdx.x;
+  const uint32_t want = (uint32_t)(nd.h[0] >> 32);
+  uint32_t f[kOpeItems];
+  uint32_t pb[kOpeGroups];
+  const bool vec = (row0 % 4 == 0) && t0 + (kOpeGroups - 1) * 4 * kOpeBlock + 3 < n;
+#pragma unroll
+  for (int k = 0; k < kOpeGroups; ++k) {
+    const size_t i = t0 + (size_t)k * 4 * kOpeBlock;
+    if (vec) {
+      const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(posfp + row0 + i));
+      f[4 * k] = x.x;
+      f[4 * k + 1] = x.y;
+      f[4 * k + 2] = x.z;
+      f[4 * k + 3] = x.w;
+      const size_t r = row0 + i;  // 4 rows inside one present word (r % 4 == 0)
+      pb[k] = (uint32_t)(present[r >> 6] >> (r & 63)) & 0xFu;
+    } else {
+      uint32_t b = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t r = row0 + min(i + j, n - 1);
+        f[4 * k + j] = posfp[r];
+        b |= (i + j < n ? (uint32_t)(present[r >> 6] >> (r & 63)) & 1u : 0u) << j;
+      }
+      pb[k] = b;
+    }
+  }
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < kOpeGroups; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!((pb[k] >> j) & 1u)) continue;
+      const size_t r = row0 + t0 + (size_t)k * 4 * kOpeBlock + j;
+      const bool eq = f[4 * k + j] == want && str_hit(row_off[r] + position, 0, elem_off, chars, nchars, nd);
+      if (eq != (negate != 0)) m |= 1u << (4 * k + j);
+    }
+  ope_store_mask(m, masks, counts, blockIdx.x);
+}
+
 // Byte-mask compaction front end (live rows of a resident column, dds_col_set_live): same tile layout
 // and masks as k_ope_count, predicate (b[r] & vmask) != 0 on a byte per row. `bytes` may start at any
 // offset (a row range of the mask): 4-byte loads only when it is aligned.
@@ -1305,6 +1358,20 @@ hipError_t launch_flag_compact(const uint32_t* flags, size_t n, uint32_t req, vo
   uint32_t* counts = (uint32_t*)scratch;
   uint32_t* masks = counts + nb;
   hipLaunchKernelGGL(k_flag_count, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, flags, n, req, masks, counts);
+  hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, masks, counts, out, total);
+  return hipGetLastError();
+}
+
+hipError_t launch_str_eq_compact(const uint32_t* posfp, const uint64_t* present, size_t row0, size_t nrows,
+                                 const uint64_t* row_off, const uint64_t* elem_off, const uint8_t* chars,
+                                 const uint8_t* nchars, const StrNeedles& nd, uint64_t position, int negate,
+                                 void* scratch, uint64_t* total, uint32_t* out, hipStream_t st) {
+  const size_t nb = ope_blocks(nrows);
+  if (nb == 0) return hipSuccess;
+  uint32_t* counts = (uint32_t*)scratch;
+  uint32_t* masks = counts + nb;
+  hipLaunchKernelGGL(k_str_eq_count, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, posfp, present, row0, nrows, row_off,
+                     elem_off, chars, nchars, nd, position, negate, masks, counts);
   hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, masks, counts, out, total);
   return hipGetLastError();
 }

@@ -158,19 +158,32 @@ struct StrNeedles {  // up to 3 items (SearchEntryAND/OR triplets), bytes in a d
 };
 hipError_t launch_str_digest(const uint8_t* chars, const uint64_t* elem_off, size_t nelems, uint32_t* fp,
                              hipStream_t st);
-// SearchEq/NEq: flags[r] = contents(position) == needle 0 (xor negate), rows with length-1 > position
-hipError_t launch_str_eq(const uint64_t* row_off, size_t nrows, const uint64_t* elem_off, const uint8_t* chars,
-                         const uint32_t* fp, const uint8_t* nchars, const StrNeedles& nd, uint64_t position,
-                         int negate, uint32_t* flags, hipStream_t st);
-// SearchEntry/OR/AND/IsElement: flags[row] |= bit j for every element equal to needle j (flags zeroed
-// by the launcher); elements [e_first, e_first + nelems), rows [0, nrows) of row_off
-// SearchEq's position-major index and the query over it (ddshe_strscan.hip)
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
+__device__ __forceinline__ bool str_equal(const uint8_t* __restrict__ x, const uint8_t* __restrict__ y, uint64_t len) {
+  for (uint64_t i = 0; i < len; ++i)
+    if (x[i] != y[i]) return false;
+  return true;
+}
+// element e equals needle j (its fingerprint already matched): length, then bytes
+__device__ __forceinline__ bool str_hit(uint64_t e, int j, const uint64_t* __restrict__ elem_off,
+                                        const uint8_t* __restrict__ chars, const uint8_t* __restrict__ nchars,
+                                        const StrNeedles& nd) {
+  const uint64_t a = elem_off[e], b = elem_off[e + 1];
+  return b - a == nd.len[j] && str_equal(chars + a, nchars + nd.off[j], nd.len[j]);
+}
+#endif
+// SearchEq/NEq over a position index straight into the compaction masks (k_str_eq_count, the tile
+// layout of k_ope_count) + k_ope_scatter: ascending row ids (relative to row0) of the matching rows
+hipError_t launch_str_eq_compact(const uint32_t* posfp, const uint64_t* present, size_t row0, size_t nrows,
+                                 const uint64_t* row_off, const uint64_t* elem_off, const uint8_t* chars,
+                                 const uint8_t* nchars, const StrNeedles& nd, uint64_t position, int negate,
+                                 void* scratch, uint64_t* total, uint32_t* out, hipStream_t st);
+// SearchEq's position-major index (ddshe_strscan.hip): per row the fingerprint of element `position`
+// and a present bit (length - 1 > position); queried by launch_str_eq_compact
 hipError_t launch_str_posfp(const uint64_t* row_off, size_t nrows, const uint32_t* fp, uint64_t position,
                             uint32_t* posfp, uint64_t* present, hipStream_t st);
-hipError_t launch_str_eq_pos(const uint32_t* posfp, const uint64_t* present, size_t row0, size_t nrows,
-                             const uint64_t* row_off, const uint64_t* elem_off, const uint8_t* chars,
-                             const uint8_t* nchars, const StrNeedles& nd, uint64_t position, int negate,
-                             uint32_t* flags, hipStream_t st);
+// SearchEntry/OR/AND/IsElement: flags[row] |= bit j for every element equal to needle j (flags zeroed
+// by the launcher); elements [e_first, e_first + nelems), rows [0, nrows) of row_off
 hipError_t launch_str_any(const uint32_t* fp, uint64_t e_first, size_t nelems, const uint64_t* row_off, size_t nrows,
                           const uint64_t* elem_off, const uint8_t* chars, const uint8_t* nchars, const StrNeedles& nd,
                           uint32_t* flags, hipStream_t st);

@@ -12,8 +12,9 @@
 //   k_str_any: one thread per 4 consecutive elements (one 16-byte fingerprint load); a verified hit
 //              finds its row by binary search in row_off (hits are rare) and ORs the needle bit
 //              into the row's u32 flag;
-//   k_str_eq:  one thread per row (the element at `position` of each row);
-// then k_flag_count / k_ope_scatter compact the flagged rows into ascending row ids.
+//   SearchEq: the position index below (k_str_posfp) read by k_str_eq_count (ddshe_kernels.hip),
+//              which writes the compaction masks directly;
+// then k_flag_count (SearchEntry) / k_ope_scatter compact the flagged rows into ascending row ids.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -29,39 +30,10 @@ __global__ void k_str_digest(const uint8_t* __restrict__ chars, const uint64_t* 
   fp[e] = (uint32_t)(str_digest(chars + a, b - a) >> 32);
 }
 
-__device__ __forceinline__ bool str_equal(const uint8_t* __restrict__ x, const uint8_t* __restrict__ y, uint64_t len) {
-  for (uint64_t i = 0; i < len; ++i)
-    if (x[i] != y[i]) return false;
-  return true;
-}
-
-__device__ __forceinline__ bool str_hit(uint64_t e, int j, const uint64_t* __restrict__ elem_off,
-                                        const uint8_t* __restrict__ chars, const uint8_t* __restrict__ nchars,
-                                        const StrNeedles& nd) {
-  const uint64_t a = elem_off[e], b = elem_off[e + 1];
-  return b - a == nd.len[j] && str_equal(chars + a, nchars + nd.off[j], nd.len[j]);
-}
-
-__global__ void k_str_eq(const uint64_t* __restrict__ row_off, size_t nrows, const uint64_t* __restrict__ elem_off,
-                         const uint8_t* __restrict__ chars, const uint32_t* __restrict__ fp,
-                         const uint8_t* __restrict__ nchars, StrNeedles nd, uint64_t position, int negate,
-                         uint32_t* __restrict__ flags) {
-  const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nrows) return;
-  const uint64_t e0 = row_off[r], e1 = row_off[r + 1];
-  uint32_t f = 0;
-  if (e1 - e0 > position + 1) {
-    const uint64_t e = e0 + position;
-    const bool eq = fp[e] == (uint32_t)(nd.h[0] >> 32) && str_hit(e, 0, elem_off, chars, nchars, nd);
-    f = eq != (negate != 0);
-  }
-  flags[r] = f;
-}
-
 // SearchEq's position-major index (built on the first query at a position, kept with the table):
 // posfp[r] = fingerprint of row r's element `position`, present bit r = the row passes the route's
-// strict guard (length - 1 > position, DDSRestServer.scala:615). A query then reads 4 B per row,
-// coalesced, instead of gathering one 4-byte fingerprint per 32-byte sector (plus 8 B of row
+// strict guard (length - 1 > position, DDSRestServer.scala:615). A query (k_str_eq_count) reads 4 B per
+// row, coalesced, instead of gathering one 4-byte fingerprint per 32-byte sector (plus 8 B of row
 // offsets); only fingerprint hits touch the row offsets and the bytes.
 __global__ void k_str_posfp(const uint64_t* __restrict__ row_off, size_t nrows, const uint32_t* __restrict__ fp,
                             uint64_t position, uint32_t* __restrict__ posfp, uint64_t* __restrict__ present) {
@@ -74,21 +46,6 @@ __global__ void k_str_posfp(const uint64_t* __restrict__ row_off, size_t nrows, 
   }
   const uint64_t m = __ballot(pres);
   if ((threadIdx.x & 63) == 0 && r < nrows) present[r >> 6] = m;  // r: the wave's first row, a multiple of 64
-}
-
-__global__ void k_str_eq_pos(const uint32_t* __restrict__ posfp, const uint64_t* __restrict__ present, size_t row0,
-                             size_t nrows, const uint64_t* __restrict__ row_off, const uint64_t* __restrict__ elem_off,
-                             const uint8_t* __restrict__ chars, const uint8_t* __restrict__ nchars, StrNeedles nd,
-                             uint64_t position, int negate, uint32_t* __restrict__ flags) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nrows) return;
-  const size_t r = row0 + i;
-  uint32_t f = 0;
-  if ((present[r >> 6] >> (r & 63)) & 1ull) {
-    const bool eq = posfp[r] == (uint32_t)(nd.h[0] >> 32) && str_hit(row_off[r] + position, 0, elem_off, chars, nchars, nd);
-    f = eq != (negate != 0);
-  }
-  flags[i] = f;
 }
 
 // row holding element e: last r with row_off[r] <= e (row_off ascending, rows may be empty)
@@ -142,30 +99,11 @@ hipError_t launch_str_digest(const uint8_t* chars, const uint64_t* elem_off, siz
   return hipGetLastError();
 }
 
-hipError_t launch_str_eq(const uint64_t* row_off, size_t nrows, const uint64_t* elem_off, const uint8_t* chars,
-                         const uint32_t* fp, const uint8_t* nchars, const StrNeedles& nd, uint64_t position,
-                         int negate, uint32_t* flags, hipStream_t st) {
-  if (nrows == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_str_eq, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, st, row_off, nrows, elem_off,
-                     chars, fp, nchars, nd, position, negate, flags);
-  return hipGetLastError();
-}
-
 hipError_t launch_str_posfp(const uint64_t* row_off, size_t nrows, const uint32_t* fp, uint64_t position,
                             uint32_t* posfp, uint64_t* present, hipStream_t st) {
   if (nrows == 0) return hipSuccess;
   hipLaunchKernelGGL(k_str_posfp, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, st, row_off, nrows, fp, position,
                      posfp, present);
-  return hipGetLastError();
-}
-
-hipError_t launch_str_eq_pos(const uint32_t* posfp, const uint64_t* present, size_t row0, size_t nrows,
-                             const uint64_t* row_off, const uint64_t* elem_off, const uint8_t* chars,
-                             const uint8_t* nchars, const StrNeedles& nd, uint64_t position, int negate,
-                             uint32_t* flags, hipStream_t st) {
-  if (nrows == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_str_eq_pos, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, st, posfp, present, row0,
-                     nrows, row_off, elem_off, chars, nchars, nd, position, negate, flags);
   return hipGetLastError();
 }
 
