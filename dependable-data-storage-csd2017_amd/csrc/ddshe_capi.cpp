@@ -2412,12 +2412,13 @@ int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values
       e_last = t->nelems;
     }
     HIP_TRY(launch_str_any(t->fp, e_first, e_last - e_first, t->row_off + row0, nrows, t->elem_off, t->chars,
-                           w->in2.as<uint8_t>(), nd, flags, wl.st));
+                           w->in2.as<uint8_t>(), nd, reinterpret_cast<uint8_t*>(flags), wl.st));
   }
   uint32_t* dst = device_out ? out_rows : w->out.as<uint32_t>();
   if (mode != 0) {  // SearchEq compacted above, straight from its position index
-    const uint32_t req = mode == 2 ? (1u << nvalues) - 1u : 0u;
-    HIP_TRY(launch_flag_compact(flags, nrows, req, w->misc.p, w->flags.as<uint64_t>(), dst, wl.st));
+    const uint32_t req = mode == 2 ? (1u << nvalues) - 1u : 0u;  // AND: every needle's bit
+    HIP_TRY(launch_byte_compact(reinterpret_cast<const uint8_t*>(flags), nrows, 0xFFu, w->misc.p,
+                                w->flags.as<uint64_t>(), dst, wl.st, req));
   }
   record_time(ctx, w, wl.st, false, 2);
   uint64_t total = 0;

@@ -653,38 +653,6 @@ __global__ void __launch_bounds__(kOpeBlock) k_ope_count(const int64_t* __restri
   ope_store_mask(m, masks, counts, blockIdx.x);
 }
 
-// Row-flag compaction front end (deterministic-equality scans): same tile layout and masks as
-// k_ope_count, predicate on u32 row flags: req == 0 -> flag != 0, else (flag & req) == req.
-__global__ void __launch_bounds__(kOpeBlock) k_flag_count(const uint32_t* __restrict__ flags, size_t n, uint32_t req,
-                                                          uint32_t* __restrict__ masks,
-                                                          uint32_t* __restrict__ counts) {
-  const size_t t0 = (size_t)blockIdx.x * kOpeTile + 4 * (size_t)threadIdx.x;
-  uint32_t f[kOpeItems];
-  if (t0 + (kOpeGroups - 1) * 4 * kOpeBlock + 3 < n) {
-#pragma unroll
-    for (int k = 0; k < kOpeGroups; ++k) {
-      const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(flags + t0 + (size_t)k * 4 * kOpeBlock));
-      f[4 * k] = x.x;
-      f[4 * k + 1] = x.y;
-      f[4 * k + 2] = x.z;
-      f[4 * k + 3] = x.w;
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < kOpeGroups; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const size_t r = t0 + (size_t)k * 4 * kOpeBlock + j;
-        f[4 * k + j] = r < n ? flags[r] : 0u;
-      }
-  }
-  uint32_t m = 0;
-#pragma unroll
-  for (int i = 0; i < kOpeItems; ++i)
-    if (req ? (f[i] & req) == req : f[i] != 0) m |= 1u << i;
-  ope_store_mask(m, masks, counts, blockIdx.x);
-}
-
 // SearchEq/NEq front end (ddshe_strscan.hip's position index): same tile layout and masks as
 // k_ope_count; row r = row0 + i matches iff its present bit is set (length - 1 > position) and its
 // fingerprint equals the needle's (bytes verified on a hit), xor negate. Reads 4 B + 1 bit per row and
@@ -738,11 +706,12 @@ __global__ void __launch_bounds__(kOpeBlock) k_str_eq_count(const uint32_t* __re
   ope_store_mask(m, masks, counts, blockIdx.x);
 }
 
-// Byte-mask compaction front end (live rows of a resident column, dds_col_set_live): same tile layout
-// and masks as k_ope_count, predicate (b[r] & vmask) != 0 on a byte per row. `bytes` may start at any
+// Byte-mask compaction front end (live rows of a resident column, dds_col_set_live; the string scans'
+// needle bits): same tile layout and masks as k_ope_count, predicate (b[r] & vmask) != 0 and
+// (b[r] & vall) == vall on a byte per row. `bytes` may start at any
 // offset (a row range of the mask): 4-byte loads only when it is aligned.
 __global__ void __launch_bounds__(kOpeBlock) k_byte_count(const uint8_t* __restrict__ bytes, size_t n, uint32_t vmask,
-                                                          uint32_t* __restrict__ masks,
+                                                          uint32_t vall, uint32_t* __restrict__ masks,
                                                           uint32_t* __restrict__ counts) {
   const size_t t0 = (size_t)blockIdx.x * kOpeTile + 4 * (size_t)threadIdx.x;
   uint32_t v[kOpeGroups];
@@ -767,7 +736,7 @@ __global__ void __launch_bounds__(kOpeBlock) k_byte_count(const uint8_t* __restr
   for (int k = 0; k < kOpeGroups; ++k)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if ((v[k] >> (8 * j)) & vmask) m |= 1u << (4 * k + j);
+      if ((((v[k] >> (8 * j)) & vmask) != 0u) && (((v[k] >> (8 * j)) & vall) == vall)) m |= 1u << (4 * k + j);
   ope_store_mask(m, masks, counts, blockIdx.x);
 }
 
@@ -1351,17 +1320,6 @@ size_t ope_blocks(size_t n) { return (n + kOpeTile - 1) / kOpeTile; }
 
 size_t ope_scratch_bytes(size_t n) { return ope_blocks(n) * (4 + 4 * kOpeBlock) + 8; }
 
-hipError_t launch_flag_compact(const uint32_t* flags, size_t n, uint32_t req, void* scratch, uint64_t* total,
-                               uint32_t* out, hipStream_t st) {
-  const size_t nb = ope_blocks(n);
-  if (nb == 0) return hipSuccess;
-  uint32_t* counts = (uint32_t*)scratch;
-  uint32_t* masks = counts + nb;
-  hipLaunchKernelGGL(k_flag_count, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, flags, n, req, masks, counts);
-  hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, masks, counts, out, total);
-  return hipGetLastError();
-}
-
 hipError_t launch_str_eq_compact(const uint32_t* posfp, const uint64_t* present, size_t row0, size_t nrows,
                                  const uint64_t* row_off, const uint64_t* elem_off, const uint8_t* chars,
                                  const uint8_t* nchars, const StrNeedles& nd, uint64_t position, int negate,
@@ -1377,12 +1335,12 @@ hipError_t launch_str_eq_compact(const uint32_t* posfp, const uint64_t* present,
 }
 
 hipError_t launch_byte_compact(const uint8_t* bytes, size_t n, uint32_t vmask, void* scratch, uint64_t* total,
-                               uint32_t* out, hipStream_t st) {
+                               uint32_t* out, hipStream_t st, uint32_t vall) {
   const size_t nb = ope_blocks(n);
   if (nb == 0) return hipSuccess;
   uint32_t* counts = (uint32_t*)scratch;
   uint32_t* masks = counts + nb;
-  hipLaunchKernelGGL(k_byte_count, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, bytes, n, vmask, masks, counts);
+  hipLaunchKernelGGL(k_byte_count, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, bytes, n, vmask, vall, masks, counts);
   hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, masks, counts, out, total);
   return hipGetLastError();
 }

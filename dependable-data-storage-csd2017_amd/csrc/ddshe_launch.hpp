@@ -110,9 +110,6 @@ hipError_t launch_synth_rows(int S, const uint32_t* T, size_t tstride, uint32_t 
                              uint32_t shards = 1, uint32_t shard = 0);  // row mapping of a sharded column
 size_t ope_blocks(size_t n);
 size_t ope_scratch_bytes(size_t n);  // per-tile match counts + per-thread match masks
-// rows with flags[r] != 0 (req == 0) or (flags[r] & req) == req -> ascending ids; scratch as above
-hipError_t launch_flag_compact(const uint32_t* flags, size_t n, uint32_t req, void* scratch, uint64_t* total,
-                               uint32_t* out, hipStream_t st);
 // rows i with (valid[i] & vmask) != 0 and (valid[i] & vbad) == 0 (valid == nullptr: every row) and
 // col[i] <op> bound -> ascending ids in out, count in *total (device)
 hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
@@ -125,7 +122,8 @@ hipError_t launch_ope_mask(const int64_t* col, const uint8_t* valid, size_t n, i
 uint32_t* ope_mask_words(void* scratch, size_t n);
 // rows i with (bytes[i] & vmask) != 0 -> ascending ids in out, count in *total (device); scratch as above
 hipError_t launch_byte_compact(const uint8_t* bytes, size_t n, uint32_t vmask, void* scratch, uint64_t* total,
-                               uint32_t* out, hipStream_t st);
+                               uint32_t* out, hipStream_t st,
+                               uint32_t vall = 0);
 // resident-row mutations (ddshe_mutate.hip): rows ids[i] of dst (S limbs, stride dstride) <- column i of
 // src (stride sstride); dst[ids[i]] <- vals[i] for bytes / u64; keep[p] = !dead[perm[p]]; dst[i] = src[idx[i]]
 hipError_t launch_scatter_rows(const uint32_t* src, size_t sstride, const uint32_t* ids, size_t n, int S, uint32_t* dst,
@@ -182,11 +180,11 @@ hipError_t launch_str_eq_compact(const uint32_t* posfp, const uint64_t* present,
 // and a present bit (length - 1 > position); queried by launch_str_eq_compact
 hipError_t launch_str_posfp(const uint64_t* row_off, size_t nrows, const uint32_t* fp, uint64_t position,
                             uint32_t* posfp, uint64_t* present, hipStream_t st);
-// SearchEntry/OR/AND/IsElement: flags[row] |= bit j for every element equal to needle j (flags zeroed
-// by the launcher); elements [e_first, e_first + nelems), rows [0, nrows) of row_off
+// SearchEntry/OR/AND/IsElement: flag byte of row |= bit j for every element equal to needle j (flags
+// zeroed by the launcher, 4-byte aligned); elements [e_first, e_first + nelems), rows [0, nrows) of row_off
 hipError_t launch_str_any(const uint32_t* fp, uint64_t e_first, size_t nelems, const uint64_t* row_off, size_t nrows,
                           const uint64_t* elem_off, const uint8_t* chars, const uint8_t* nchars, const StrNeedles& nd,
-                          uint32_t* flags, hipStream_t st);
+                          uint8_t* flags, hipStream_t st);
 hipError_t launch_plain_sum(const uint32_t* X, size_t stride, size_t count, int S, size_t nthreads, uint64_t* part,
                             uint64_t* out, hipStream_t st);
 // unbounded product tree level: rows (2p, 2p+1) of A[count][len] (radix 2^16 in u32)

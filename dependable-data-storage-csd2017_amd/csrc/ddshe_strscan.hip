@@ -9,12 +9,12 @@
 // resident 32-bit fingerprint per element (k_str_digest: top half of str_digest). A scan streams
 // 4 B of fingerprint per element it must look at; bytes are compared only on a fingerprint hit
 // (about nelems * needles / 2^32 false hits per scan), so results stay exact.
-//   k_str_any: one thread per 4 consecutive elements (one 16-byte fingerprint load); a verified hit
-//              finds its row by binary search in row_off (hits are rare) and ORs the needle bit
-//              into the row's u32 flag;
+//   k_str_any: four 16-byte fingerprint loads per thread (block-interleaved quads); a verified
+//              hit finds its row by binary search in row_off (hits are rare) and ORs the needle bit
+//              into the row's flag byte;
 //   SearchEq: the position index below (k_str_posfp) read by k_str_eq_count (ddshe_kernels.hip),
 //              which writes the compaction masks directly;
-// then k_flag_count (SearchEntry) / k_ope_scatter compact the flagged rows into ascending row ids.
+// then k_byte_count (SearchEntry) / k_ope_scatter compact the flagged rows into ascending row ids.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -59,36 +59,52 @@ __device__ __forceinline__ size_t row_of(const uint64_t* __restrict__ row_off, s
   return lo;
 }
 
-__global__ void k_str_any(const uint32_t* __restrict__ fp, uint64_t e_first, size_t nelems,
-                          const uint64_t* __restrict__ row_off, size_t nrows, const uint64_t* __restrict__ elem_off,
-                          const uint8_t* __restrict__ chars, const uint8_t* __restrict__ nchars, StrNeedles nd,
-                          uint32_t* __restrict__ flags) {
-  const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // element quad
-  const uint64_t e0 = e_first + 4 * q;
-  if (4 * q >= nelems) return;
-  uint32_t f[4];
-  if (4 * q + 3 < nelems && e0 % 4 == 0) {
-    const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(fp + e0));
-    f[0] = x.x;
-    f[1] = x.y;
-    f[2] = x.z;
-    f[3] = x.w;
-  } else {
-    for (int i = 0; i < 4; ++i) f[i] = 4 * q + i < nelems ? fp[e0 + i] : 0u;
+// one thread per kStrQuads element quads, block-interleaved (quad b*256*kStrQuads + k*256 + tid: each
+// 16-byte load instruction of a wave covers 1 KiB contiguous; all kStrQuads loads in flight together);
+// a verified hit ORs the needle bit into its row's flag byte (a 32-bit atomic on the byte's word:
+// hits are rare)
+constexpr int kStrQuads = 4;
+__global__ void __launch_bounds__(256) k_str_any(const uint32_t* __restrict__ fp, uint64_t e_first, size_t nelems,
+                                                 const uint64_t* __restrict__ row_off, size_t nrows,
+                                                 const uint64_t* __restrict__ elem_off, const uint8_t* __restrict__ chars,
+                                                 const uint8_t* __restrict__ nchars, StrNeedles nd,
+                                                 uint8_t* __restrict__ flags) {
+  const size_t qb = (size_t)blockIdx.x * 256 * kStrQuads + threadIdx.x;  // quad of k = 0
+  uint32_t f[4 * kStrQuads];
+#pragma unroll
+  for (int k = 0; k < kStrQuads; ++k) {
+    const size_t q = qb + (size_t)k * 256;
+    const uint64_t e0 = e_first + 4 * q;
+    if (e_first % 4 == 0 && 4 * q + 3 < nelems) {
+      const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(fp + e0));
+      f[4 * k] = x.x;
+      f[4 * k + 1] = x.y;
+      f[4 * k + 2] = x.z;
+      f[4 * k + 3] = x.w;
+    } else {
+      for (int i = 0; i < 4; ++i) f[4 * k + i] = 4 * q + i < nelems ? fp[e0 + i] : 0u;
+    }
   }
   const uint32_t h0 = (uint32_t)(nd.h[0] >> 32), h1 = (uint32_t)(nd.h[1] >> 32), h2 = (uint32_t)(nd.h[2] >> 32);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (4 * q + i >= nelems) break;
-    const bool c0 = f[i] == h0, c1 = nd.n > 1 && f[i] == h1, c2 = nd.n > 2 && f[i] == h2;
-    if (!(c0 | c1 | c2)) continue;  // the common case: no fingerprint hit
-    const uint64_t e = e0 + i;
-    uint32_t bits = 0;
-    if (c0 && str_hit(e, 0, elem_off, chars, nchars, nd)) bits |= 1u;
-    if (c1 && str_hit(e, 1, elem_off, chars, nchars, nd)) bits |= 2u;
-    if (c2 && str_hit(e, 2, elem_off, chars, nchars, nd)) bits |= 4u;
-    if (bits) atomicOr(&flags[row_of(row_off, nrows, e)], bits);
-  }
+  for (int k = 0; k < kStrQuads; ++k)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const size_t ei = 4 * (qb + (size_t)k * 256) + i;  // element index relative to e_first
+      if (ei >= nelems) continue;
+      const uint32_t v = f[4 * k + i];
+      const bool c0 = v == h0, c1 = nd.n > 1 && v == h1, c2 = nd.n > 2 && v == h2;
+      if (!(c0 | c1 | c2)) continue;  // the common case: no fingerprint hit
+      const uint64_t e = e_first + ei;
+      uint32_t bits = 0;
+      if (c0 && str_hit(e, 0, elem_off, chars, nchars, nd)) bits |= 1u;
+      if (c1 && str_hit(e, 1, elem_off, chars, nchars, nd)) bits |= 2u;
+      if (c2 && str_hit(e, 2, elem_off, chars, nchars, nd)) bits |= 4u;
+      if (bits) {
+        const size_t r = row_of(row_off, nrows, e);
+        atomicOr(reinterpret_cast<uint32_t*>(flags + (r & ~(size_t)3)), bits << (8 * (r & 3)));
+      }
+    }
 }
 
 hipError_t launch_str_digest(const uint8_t* chars, const uint64_t* elem_off, size_t nelems, uint32_t* fp,
@@ -109,12 +125,12 @@ hipError_t launch_str_posfp(const uint64_t* row_off, size_t nrows, const uint32_
 
 hipError_t launch_str_any(const uint32_t* fp, uint64_t e_first, size_t nelems, const uint64_t* row_off, size_t nrows,
                           const uint64_t* elem_off, const uint8_t* chars, const uint8_t* nchars, const StrNeedles& nd,
-                          uint32_t* flags, hipStream_t st) {
+                          uint8_t* flags, hipStream_t st) {
   if (nrows == 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(flags, 0, nrows * 4, st);
+  hipError_t e = hipMemsetAsync(flags, 0, (nrows + 3) & ~(size_t)3, st);  // whole words (the atomics' unit)
   if (e != hipSuccess || nelems == 0) return e;
-  const size_t quads = (nelems + 3) / 4;
-  hipLaunchKernelGGL(k_str_any, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, st, fp, e_first, nelems, row_off,
+  const size_t quads = (nelems + 3) / 4, per_block = (size_t)256 * kStrQuads;
+  hipLaunchKernelGGL(k_str_any, dim3((unsigned)((quads + per_block - 1) / per_block)), dim3(256), 0, st, fp, e_first, nelems, row_off,
                      nrows, elem_off, chars, nchars, nd, flags);
   return hipGetLastError();
 }
