@@ -1003,6 +1003,9 @@ int col_write_commit(dds_col* col, RowWrite& plan) {
   if (m == 0) return DDS_OK;
   Worker* w = plan.wl->w;
   hipStream_t st = plan.wl->st;
+  // a multi-device write prepares every shard before committing any, so the current device is the last
+  // prepared shard's: the worker's buffers must be (re)allocated on this column's device
+  if (hipSetDevice(col->ctx->device) != hipSuccess) return fail(DDS_E_HIP, "hipSetDevice");
   HIP_TRY(w->ids.ensure(m * 4));
   HIP_TRY(hipMemcpyAsync(w->ids.p, plan.ids32.data(), m * 4, hipMemcpyHostToDevice, st));
   HIP_TRY(launch_scatter_rows(w->x2.as<uint32_t>(), plan.ss, w->ids.as<uint32_t>(), m, col->mc->S, col->d, col->stride,

@@ -199,7 +199,9 @@ int split_ids(dds_mcol* c, const uint64_t* ids, size_t n, std::vector<std::vecto
 }
 
 // dds_mcol_write_rows[_dec]: every shard's new rows are prepared (ingested, validated) before any is
-// committed, so an error leaves the whole column unchanged
+// committed, so a validation error (range, format, row id) leaves the whole column unchanged. A HIP
+// error during a commit (scatter / sync) can leave earlier shards committed: the column is then in an
+// undefined state and the caller must treat DDS_E_HIP from here as fatal to it.
 int mcol_write(dds_mcol* c, const uint64_t* ids, size_t n, const uint8_t* ops, size_t width, const char* chars,
                const uint64_t* offsets) {
   std::unique_lock<std::shared_mutex> lk(c->mu);

@@ -23,6 +23,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "ddshe_launch.hpp"
 
@@ -542,17 +546,44 @@ hipError_t launch_pairs_sos(int S, const uint32_t* A, const uint32_t* B, size_t 
 constexpr int kTreeWideThreads = 256;
 constexpr size_t kOneWgPerCuLds = 96 * 1024;  // dynamic LDS of a hand-off launch: one workgroup per CU
 
+// A hand-off launch asks for kOneWgPerCuLds of dynamic LDS on top of the kernel's static LDS (about
+// 150 KiB in all at S = 694). Checked once per (device, kernel): a device whose workgroups cannot have
+// that much (less than gfx950's 160 KiB per CU) runs the tree one level per launch instead of failing.
+static bool handoff_fits(const void* fn) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, bool> known;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = known.find({dev, fn});
+  if (it != known.end()) return it->second;
+  int lim = 0;
+  for (hipDeviceAttribute_t a : {hipDeviceAttributeMaxSharedMemoryPerBlock, hipDeviceAttributeSharedMemPerBlockOptin,
+                                 hipDeviceAttributeMaxSharedMemoryPerMultiprocessor}) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, a, dev) == hipSuccess) lim = std::max(lim, v);
+  }
+  hipFuncAttributes fa;
+  bool ok = hipFuncGetAttributes(&fa, fn) == hipSuccess && fa.sharedSizeBytes + kOneWgPerCuLds <= (size_t)lim &&
+            hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kOneWgPerCuLds) == hipSuccess;
+  (void)hipGetLastError();
+  known[{dev, fn}] = ok;
+  return ok;
+}
+
 hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Win, size_t nleaves, const uint32_t* ids,
                        const uint32_t* consts, const uint32_t* Y, uint32_t* nodes, uint32_t* flags, uint32_t* out,
                        int Sout, int Wout, hipStream_t st, size_t gstride) {
-  static const int levels = tree_env("DDSHE_TREE_LEVELS", 0), fence = tree_env("DDSHE_TREE_FENCE", 2);
+  static const int levels_env = tree_env("DDSHE_TREE_LEVELS", 0), fence = tree_env("DDSHE_TREE_FENCE", 2);
   static const size_t wide = (size_t)tree_env("DDSHE_TREE_WIDE", 256);
   static uint64_t* d_st = nullptr;
   static const bool stamping = getenv("DDSHE_TREE_STAMPS") && hipMalloc(&d_st, 2 * kStamps * 8) == hipSuccess;
   if (nleaves == 0 || Sin > S + 64) return hipErrorInvalidValue;
   // in-kernel hand-offs with wave-0-only fences rely on cache side effects the memory model does not
   // promise: only the every-wave (0) and sc1 write-through (2) styles may hand off in-kernel
-  if (levels != 1 && fence == 1) return hipErrorInvalidValue;
+  if (levels_env != 1 && fence == 1) return hipErrorInvalidValue;
+  int levels = levels_env;
+  if (levels != 1) DDSHE_TREE_SWITCH(S, if (!handoff_fits(reinterpret_cast<const void*>(&k_tree<S, W, kTreeThreads>))) levels = 1);
   // level buffers for multi-launch trees live after the nodes: two ping-pong halves of nleaves rows
   uint32_t* lvl[2] = {nodes + (2 * nleaves + 2) * (size_t)S, nodes + (3 * nleaves + 2) * (size_t)S};
   int flip = 0;
@@ -587,10 +618,6 @@ hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Wi
     } else {
       const size_t dyn = handoff ? kOneWgPerCuLds : 0;
       DDSHE_TREE_SWITCH(S, {
-        static const hipError_t attr = hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&k_tree<S, W, kTreeThreads>), hipFuncAttributeMaxDynamicSharedMemorySize,
-            (int)kOneWgPerCuLds);
-        (void)attr;
         hipLaunchKernelGGL((k_tree<S, W, kTreeThreads>), dim3((unsigned)((nl + 1) / 2)), dim3(kTreeThreads), dyn, st,
                            X, xstride, gstride, Sin, Win, nl, ids, consts, Y, nodes, flags, out, Sout, Wout,
                            last ? 0 : lv, lvl[flip], fence, stamping ? d_st : nullptr, nullptr, (size_t)0, yleaf);

@@ -41,7 +41,7 @@ typedef enum dds_status {
   DDS_E_EMPTY = 1,       /* no operand qualified: reference answers 404      */
   DDS_E_RANGE = 2,       /* operand does not fit the modulus' limb width      */
   DDS_E_HIP = 3,         /* HIP runtime / kernel failure                      */
-  DDS_E_ARG = 4,         /* bad argument (NULL, zero width, even modulus, ...)*/
+  DDS_E_ARG = 4,         /* bad argument (NULL, zero width, row id, ...)      */
   DDS_E_NOMEM = 5,       /* device or host allocation failed                  */
   DDS_E_UNSUPPORTED = 6, /* modulus larger than the largest kernel instance   */
   DDS_E_BUFSIZE = 7,     /* output buffer too small (required size returned)  */
@@ -218,7 +218,9 @@ int dds_mcol_fold_rows(dds_mcol* col, const uint64_t* row_ids, size_t n, uint8_t
                        size_t* out_len);
 int dds_mcol_fold_dec(dds_mcol* col, const uint64_t* row_ids, size_t n, char* out, size_t out_cap, size_t* out_len);
 /* dds_col_write_rows[_dec] / dds_col_set_live / dds_col_live_count on a sharded column (global row ids;
- * a failed write leaves every shard unchanged; folds above honour the live mask of every shard) */
+ * a write that fails validation (DDS_E_ARG / DDS_E_RANGE / DDS_E_FORMAT) leaves every shard unchanged;
+ * DDS_E_HIP from a write may leave some shards written and is fatal to the column; folds above honour
+ * the live mask of every shard) */
 int dds_mcol_write_rows(dds_mcol* col, const uint64_t* row_ids, size_t n, const uint8_t* operands_be, size_t width);
 int dds_mcol_write_rows_dec(dds_mcol* col, const uint64_t* row_ids, size_t n, const char* chars,
                             const uint64_t* offsets);
