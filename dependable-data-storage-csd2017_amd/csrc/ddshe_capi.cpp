@@ -179,6 +179,15 @@ size_t max_cached_moduli() {
   return n;
 }
 
+bool host_registered(dds_ctx* ctx, const void* p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(ctx->regmu);
+  const uintptr_t b = (uintptr_t)p;
+  auto it = ctx->host_regs.upper_bound(b);
+  if (it == ctx->host_regs.begin()) return false;
+  --it;
+  return b + bytes <= it->first + it->second;
+}
+
 void record_time(dds_ctx* ctx, Worker* w, hipStream_t st, bool begin, int slot) {
   if (!ctx->timing.load()) return;
   (void)hipEventRecord(w->ev[slot + (begin ? 0 : 1)], st);
@@ -1053,6 +1062,10 @@ int col_set_live(dds_col* col, const uint64_t* ids, size_t n, const uint8_t* liv
 }  // namespace ddshe
 
 // =============================================================================
+dds_ctx::~dds_ctx() {
+  for (auto& kv : host_regs) (void)hipHostUnregister(reinterpret_cast<void*>(kv.first));
+}
+
 extern "C" {
 
 const char* dds_strerror(int s) {
@@ -1105,6 +1118,35 @@ int dds_ctx_destroy(dds_ctx* ctx) {
   (void)hipDeviceSynchronize();
   delete ctx;
   return DDS_OK;
+}
+
+int dds_host_register(dds_ctx* ctx, void* ptr, size_t bytes) {
+  if (!ctx || !ptr || !bytes) return fail(DDS_E_ARG, "bad arguments");
+  std::lock_guard<std::mutex> lk(ctx->regmu);
+  const uintptr_t b = (uintptr_t)ptr;
+  auto it = ctx->host_regs.upper_bound(b);
+  if (it != ctx->host_regs.begin()) {
+    auto pv = std::prev(it);
+    if (pv->first == b && pv->second == bytes) return DDS_OK;  // already registered
+    if (pv->first + pv->second > b) return fail(DDS_E_ARG, "overlaps a registered buffer");
+  }
+  if (it != ctx->host_regs.end() && it->first < b + bytes) return fail(DDS_E_ARG, "overlaps a registered buffer");
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  ctx->host_regs[b] = bytes;
+  return DDS_OK;
+}
+
+int dds_host_unregister(dds_ctx* ctx, void* ptr) {
+  if (!ctx || !ptr) return fail(DDS_E_ARG, "bad arguments");
+  std::lock_guard<std::mutex> lk(ctx->regmu);
+  auto it = ctx->host_regs.find((uintptr_t)ptr);
+  if (it == ctx->host_regs.end()) return fail(DDS_E_ARG, "not a registered buffer");
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();  // no copy into it is still in flight
+  hipError_t e = hipHostUnregister(ptr);
+  ctx->host_regs.erase(it);
+  return e == hipSuccess ? DDS_OK : fail(DDS_E_HIP, "hipHostUnregister");
 }
 
 int dds_ctx_set_stream(dds_ctx* ctx, void* stream) {
@@ -2278,220 +2320,7 @@ int dds_ope_order(dds_ctx* ctx, const int64_t* col, const uint8_t* valid, size_t
   }
 }
 
-// ---- deterministic-equality scans (SearchEq/NEq, SearchEntry/OR/AND, IsElement) ----------
-struct dds_strtab {
-  dds_ctx* ctx = nullptr;
-  size_t nrows = 0, nelems = 0, nchars = 0;
-  uint8_t* chars = nullptr;
-  uint64_t *elem_off = nullptr, *row_off = nullptr;
-  uint32_t* fp = nullptr;  // per-element 32-bit fingerprint
-  // SearchEq's position-major indexes (k_str_posfp), built on the first query at a position; the
-  // kPosIdx most recent positions are kept
-  struct PosIdx {
-    uint64_t position = 0;
-    uint32_t* fp = nullptr;
-    uint64_t* present = nullptr;
-  };
-  static constexpr size_t kPosIdx = 8;
-  std::vector<PosIdx> pos;  // most recent last
-  std::mutex mu;
-  ~dds_strtab() {
-    for (void* p : {(void*)chars, (void*)elem_off, (void*)row_off, (void*)fp})
-      if (p) (void)hipFree(p);
-    for (auto& x : pos) {
-      if (x.fp) (void)hipFree(x.fp);
-      if (x.present) (void)hipFree(x.present);
-    }
-  }
-};
-
-int dds_strtab_create(dds_ctx* ctx, const char* chars, const uint64_t* elem_offsets, size_t nelems,
-                      const uint64_t* row_offsets, size_t nrows, dds_strtab** out) {
-  try {
-    if (!ctx || !out || !elem_offsets || !row_offsets || (elem_offsets[nelems] && !chars))
-      return fail(DDS_E_ARG, "bad arguments");
-    *out = nullptr;
-    if (elem_offsets[0] != 0 || row_offsets[0] != 0 || row_offsets[nrows] != nelems)
-      return fail(DDS_E_ARG, "offsets must start at 0 and cover every element");
-    for (size_t e = 0; e < nelems; ++e)
-      if (elem_offsets[e + 1] < elem_offsets[e]) return fail(DDS_E_ARG, "element offsets not monotone");
-    for (size_t r = 0; r < nrows; ++r)
-      if (row_offsets[r + 1] < row_offsets[r]) return fail(DDS_E_ARG, "row offsets not monotone");
-    std::unique_ptr<dds_strtab> t(new dds_strtab());
-    t->ctx = ctx;
-    t->nrows = nrows;
-    t->nelems = nelems;
-    t->nchars = elem_offsets[nelems];
-    HIP_TRY(hipSetDevice(ctx->device));
-    if (hipMalloc(&t->chars, std::max<size_t>(t->nchars, 1)) != hipSuccess ||
-        hipMalloc(&t->elem_off, (nelems + 1) * 8) != hipSuccess ||
-        hipMalloc(&t->row_off, (nrows + 1) * 8) != hipSuccess ||
-        hipMalloc(&t->fp, std::max<size_t>(nelems, 1) * 4) != hipSuccess)
-      return fail(DDS_E_NOMEM, "string table allocation");
-    WorkerLease wl(ctx);
-    int rc;
-    if ((rc = wl.acquire())) return rc;
-    if (t->nchars) HIP_TRY(hipMemcpyAsync(t->chars, chars, t->nchars, hipMemcpyHostToDevice, wl.st));
-    HIP_TRY(hipMemcpyAsync(t->elem_off, elem_offsets, (nelems + 1) * 8, hipMemcpyHostToDevice, wl.st));
-    HIP_TRY(hipMemcpyAsync(t->row_off, row_offsets, (nrows + 1) * 8, hipMemcpyHostToDevice, wl.st));
-    HIP_TRY(launch_str_digest(t->chars, t->elem_off, nelems, t->fp, wl.st));
-    HIP_TRY(hipStreamSynchronize(wl.st));
-    *out = t.release();
-    return DDS_OK;
-  } catch (const std::bad_alloc&) {
-    return fail(DDS_E_NOMEM, "host allocation");
-  }
-}
-
-int dds_strtab_destroy(dds_strtab* tab) {
-  delete tab;
-  return DDS_OK;
-}
-
-namespace {
-// scan -> int64 row flags -> stable compaction of the rows with flag > 0 (the OPE kernels)
-int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values, const size_t* lens, int nvalues,
-             int mode, uint64_t position, int negate, uint32_t* out_rows, size_t* out_n, bool device_out) {
-  StrNeedles nd{};
-  nd.n = nvalues;
-  std::vector<uint8_t> nb;
-  for (int j = 0; j < nvalues; ++j) {
-    if (!values[j] && lens[j]) return fail(DDS_E_ARG, "NULL value");
-    nd.off[j] = nb.size();
-    nd.len[j] = lens[j];
-    nd.h[j] = str_digest((const uint8_t*)values[j], lens[j]);
-    nb.insert(nb.end(), (const uint8_t*)values[j], (const uint8_t*)values[j] + lens[j]);
-  }
-  dds_ctx* ctx = t->ctx;
-  WorkerLease wl(ctx);
-  int rc;
-  if ((rc = wl.acquire())) return rc;
-  Worker* w = wl.w;
-  HIP_TRY(w->in2.ensure(std::max<size_t>(nb.size(), 1)));
-  HIP_TRY(w->x.ensure(nrows * 4));
-  HIP_TRY(w->misc.ensure(ope_scratch_bytes(nrows)));
-  HIP_TRY(w->flags.ensure(16));
-  if (!device_out) HIP_TRY(w->out.ensure(nrows * 4));
-  if (!nb.empty()) HIP_TRY(hipMemcpyAsync(w->in2.p, nb.data(), nb.size(), hipMemcpyHostToDevice, wl.st));
-  record_time(ctx, w, wl.st, true, 2);
-  uint32_t* flags = w->x.as<uint32_t>();
-  if (mode == 0) {  // SearchEq / NEq: over the position-major index of `position` (built on first use)
-    dds_strtab::PosIdx* px = nullptr;
-    for (auto it = t->pos.begin(); it != t->pos.end(); ++it)
-      if (it->position == position) {
-        const dds_strtab::PosIdx x = *it;  // most recent last
-        t->pos.erase(it);
-        t->pos.push_back(x);
-        px = &t->pos.back();
-        break;
-      }
-    if (!px) {
-      if (t->pos.size() >= dds_strtab::kPosIdx) {  // evict the least recent (its last query has synchronised)
-        (void)hipFree(t->pos.front().fp);
-        (void)hipFree(t->pos.front().present);
-        t->pos.erase(t->pos.begin());
-      }
-      dds_strtab::PosIdx x;
-      x.position = position;
-      if (hipMalloc(&x.fp, std::max<size_t>(t->nrows, 1) * 4) != hipSuccess) return fail(DDS_E_NOMEM, "position index");
-      if (hipMalloc(&x.present, ((t->nrows + 63) / 64 + 1) * 8) != hipSuccess) {
-        (void)hipFree(x.fp);
-        return fail(DDS_E_NOMEM, "position index");
-      }
-      t->pos.push_back(x);
-      px = &t->pos.back();
-      HIP_TRY(launch_str_posfp(t->row_off, t->nrows, t->fp, position, px->fp, px->present, wl.st));
-    }
-    uint32_t* dst = device_out ? out_rows : w->out.as<uint32_t>();
-    HIP_TRY(launch_str_eq_compact(px->fp, px->present, row0, nrows, t->row_off, t->elem_off, t->chars,
-                                  w->in2.as<uint8_t>(), nd, position, negate, w->misc.p, w->flags.as<uint64_t>(), dst,
-                                  wl.st));
-  } else {
-    uint64_t e_first = 0, e_last = 0;  // element range of rows [row0, row0 + nrows)
-    HIP_TRY(hipMemcpy(&e_first, t->row_off + row0, 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(&e_last, t->row_off + row0 + nrows, 8, hipMemcpyDeviceToHost));
-    if (row0 == 0 && nrows == t->nrows) {
-      e_first = 0;
-      e_last = t->nelems;
-    }
-    HIP_TRY(launch_str_any(t->fp, e_first, e_last - e_first, t->row_off + row0, nrows, t->elem_off, t->chars,
-                           w->in2.as<uint8_t>(), nd, reinterpret_cast<uint8_t*>(flags), wl.st));
-  }
-  uint32_t* dst = device_out ? out_rows : w->out.as<uint32_t>();
-  if (mode != 0) {  // SearchEq compacted above, straight from its position index
-    const uint32_t req = mode == 2 ? (1u << nvalues) - 1u : 0u;  // AND: every needle's bit
-    HIP_TRY(launch_byte_compact(reinterpret_cast<const uint8_t*>(flags), nrows, 0xFFu, w->misc.p,
-                                w->flags.as<uint64_t>(), dst, wl.st, req));
-  }
-  record_time(ctx, w, wl.st, false, 2);
-  uint64_t total = 0;
-  HIP_TRY(read_sync(w, wl.st, w->flags.p, &total, 8));
-  if (!device_out && total) HIP_TRY(hipMemcpy(out_rows, dst, total * 4, hipMemcpyDeviceToHost));
-  if (ctx->timing.load()) {
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, w->ev[2], w->ev[3]) == hipSuccess) {
-      std::lock_guard<std::mutex> lk(ctx->tmu);
-      ctx->total_ms += ms;
-    }
-  }
-  *out_n = (size_t)total;
-  return DDS_OK;
-}
-}  // namespace
-
-int dds_search_eq(dds_strtab* tab, size_t position, const char* value, size_t len, int negate, uint32_t* out_rows,
-                  size_t* out_n) {
-  try {
-    if (!tab || !out_n || (len && !value) || (tab->nrows && !out_rows)) return fail(DDS_E_ARG, "bad arguments");
-    *out_n = 0;
-    if (tab->nrows == 0) return DDS_OK;
-    std::lock_guard<std::mutex> lk(tab->mu);
-    const char* v[1] = {value};
-    size_t l[1] = {len};
-    return str_scan(tab, 0, tab->nrows, v, l, 1, 0, position, negate, out_rows, out_n, false);
-  } catch (const std::bad_alloc&) {
-    return fail(DDS_E_NOMEM, "host allocation");
-  }
-}
-
-int dds_search_entry(dds_strtab* tab, const char* const* values, const size_t* lens, size_t nvalues, int require_all,
-                     uint32_t* out_rows, size_t* out_n) {
-  try {
-    if (!tab || !out_n || !values || !lens || nvalues == 0 || nvalues > 3 || (tab->nrows && !out_rows))
-      return fail(DDS_E_ARG, "bad arguments");
-    *out_n = 0;
-    if (tab->nrows == 0) return DDS_OK;
-    if (require_all) {  // SearchEntryAND needs 3 distinct matched strings (DDSRestServer.scala:924)
-      for (size_t i = 0; i < nvalues; ++i)
-        for (size_t j = i + 1; j < nvalues; ++j)
-          if (lens[i] == lens[j] && memcmp(values[i], values[j], lens[i]) == 0) return DDS_OK;
-      if (nvalues != 3) return fail(DDS_E_ARG, "SearchEntryAND takes three values");
-    }
-    std::lock_guard<std::mutex> lk(tab->mu);
-    return str_scan(tab, 0, tab->nrows, values, lens, (int)nvalues, require_all ? 2 : 1, 0, 0, out_rows, out_n,
-                    false);
-  } catch (const std::bad_alloc&) {
-    return fail(DDS_E_NOMEM, "host allocation");
-  }
-}
-
-int dds_is_element(dds_strtab* tab, size_t row, const char* value, size_t len, int* found) {
-  try {
-    if (!tab || !found || (len && !value)) return fail(DDS_E_ARG, "bad arguments");
-    if (row >= tab->nrows) return fail(DDS_E_EMPTY, "no such row");
-    std::lock_guard<std::mutex> lk(tab->mu);
-    const char* v[1] = {value};
-    size_t l[1] = {len};
-    uint32_t id = 0;
-    size_t n = 0;
-    int rc = str_scan(tab, row, 1, v, l, 1, 1, 0, 0, &id, &n, false);
-    if (rc) return rc;
-    *found = n ? 1 : 0;
-    return DDS_OK;
-  } catch (const std::bad_alloc&) {
-    return fail(DDS_E_NOMEM, "host allocation");
-  }
-}
+// ---- deterministic-equality scans: ddshe_strtab.cpp -------------------------------------
 
 // ---- decimal route entry points ----------------------------------------------------
 namespace {

@@ -235,6 +235,11 @@ struct dds_ctx {
   std::mutex pmu;
   std::map<ddshe::bn::Limbs, std::shared_ptr<ddshe::host::PairQueue>> pair_queues;
   std::atomic<uint64_t> pair_calls{0}, pair_launches{0};
+  // caller output buffers registered with dds_host_register (page-locked): base -> bytes. Results
+  // bound for them are DMA'd straight in, with no pinned staging buffer and no second host copy.
+  std::mutex regmu;
+  std::map<uintptr_t, size_t> host_regs;
+  ~dds_ctx();
 };
 
 struct dds_col {
@@ -481,6 +486,8 @@ bn::Limbs low_bits(const bn::Limbs& x, size_t t);
 int fold_even_modulus(dds_ctx* ctx, const bn::Limbs& M, const std::vector<bn::Limbs>& xs, const std::vector<bool>& negs,
                       bn::Limbs* out);
 void record_time(dds_ctx* ctx, Worker* w, hipStream_t st, bool begin, int slot);
+// [p, p + bytes) lies inside one buffer the caller registered with dds_host_register
+bool host_registered(dds_ctx* ctx, const void* p, size_t bytes);
 int pick_tpi(int S);
 size_t max_fold_groups(dds_ctx* ctx, int S);
 // Leaves of the reduction tree: X[l * xs + g * gs] (g = ids[k] when ids), l < Sin limbs of Win bits,

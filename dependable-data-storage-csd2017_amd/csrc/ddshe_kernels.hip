@@ -659,7 +659,7 @@ __global__ void __launch_bounds__(kOpeBlock) k_ope_count(const int64_t* __restri
 // writes no per-row flags.
 __global__ void __launch_bounds__(kOpeBlock) k_str_eq_count(const uint32_t* __restrict__ posfp,
                                                             const uint64_t* __restrict__ present, size_t row0, size_t n,
-                                                            const uint64_t* __restrict__ row_off,
+                                                            const uint64_t* __restrict__ row_beg,
                                                             const uint64_t* __restrict__ elem_off,
                                                             const uint8_t* __restrict__ chars,
                                                             const uint8_t* __restrict__ nchars, StrNeedles nd,
@@ -700,7 +700,7 @@ __global__ void __launch_bounds__(kOpeBlock) k_str_eq_count(const uint32_t* __re
     for (int j = 0; j < 4; ++j) {
       if (!((pb[k] >> j) & 1u)) continue;
       const size_t r = row0 + t0 + (size_t)k * 4 * kOpeBlock + j;
-      const bool eq = f[4 * k + j] == want && str_hit(row_off[r] + position, 0, elem_off, chars, nchars, nd);
+      const bool eq = f[4 * k + j] == want && str_hit(row_beg[r] + position, 0, elem_off, chars, nchars, nd);
       if (eq != (negate != 0)) m |= 1u << (4 * k + j);
     }
   ope_store_mask(m, masks, counts, blockIdx.x);
@@ -1321,14 +1321,14 @@ size_t ope_blocks(size_t n) { return (n + kOpeTile - 1) / kOpeTile; }
 size_t ope_scratch_bytes(size_t n) { return ope_blocks(n) * (4 + 4 * kOpeBlock) + 8; }
 
 hipError_t launch_str_eq_compact(const uint32_t* posfp, const uint64_t* present, size_t row0, size_t nrows,
-                                 const uint64_t* row_off, const uint64_t* elem_off, const uint8_t* chars,
+                                 const uint64_t* row_beg, const uint64_t* elem_off, const uint8_t* chars,
                                  const uint8_t* nchars, const StrNeedles& nd, uint64_t position, int negate,
                                  void* scratch, uint64_t* total, uint32_t* out, hipStream_t st) {
   const size_t nb = ope_blocks(nrows);
   if (nb == 0) return hipSuccess;
   uint32_t* counts = (uint32_t*)scratch;
   uint32_t* masks = counts + nb;
-  hipLaunchKernelGGL(k_str_eq_count, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, posfp, present, row0, nrows, row_off,
+  hipLaunchKernelGGL(k_str_eq_count, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, posfp, present, row0, nrows, row_beg,
                      elem_off, chars, nchars, nd, position, negate, masks, counts);
   hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, masks, counts, out, total);
   return hipGetLastError();

@@ -170,21 +170,38 @@ __device__ __forceinline__ bool str_hit(uint64_t e, int j, const uint64_t* __res
   return b - a == nd.len[j] && str_equal(chars + a, nchars + nd.off[j], nd.len[j]);
 }
 #endif
+constexpr uint32_t kStrDead = 0xFFFFFFFFu;  // elem_row of a superseded element (ddshe_strscan.hip)
 // SearchEq/NEq over a position index straight into the compaction masks (k_str_eq_count, the tile
-// layout of k_ope_count) + k_ope_scatter: ascending row ids (relative to row0) of the matching rows
+// layout of k_ope_count) + k_ope_scatter: ascending row ids (relative to row0) of the matching rows;
+// row_beg[r]: the first heap element of row r's current version
 hipError_t launch_str_eq_compact(const uint32_t* posfp, const uint64_t* present, size_t row0, size_t nrows,
-                                 const uint64_t* row_off, const uint64_t* elem_off, const uint8_t* chars,
+                                 const uint64_t* row_beg, const uint64_t* elem_off, const uint8_t* chars,
                                  const uint8_t* nchars, const StrNeedles& nd, uint64_t position, int negate,
                                  void* scratch, uint64_t* total, uint32_t* out, hipStream_t st);
 // SearchEq's position-major index (ddshe_strscan.hip): per row the fingerprint of element `position`
-// and a present bit (length - 1 > position); queried by launch_str_eq_compact
-hipError_t launch_str_posfp(const uint64_t* row_off, size_t nrows, const uint32_t* fp, uint64_t position,
-                            uint32_t* posfp, uint64_t* present, hipStream_t st);
-// SearchEntry/OR/AND/IsElement: flag byte of row |= bit j for every element equal to needle j (flags
-// zeroed by the launcher, 4-byte aligned); elements [e_first, e_first + nelems), rows [0, nrows) of row_off
-hipError_t launch_str_any(const uint32_t* fp, uint64_t e_first, size_t nelems, const uint64_t* row_off, size_t nrows,
-                          const uint64_t* elem_off, const uint8_t* chars, const uint8_t* nchars, const StrNeedles& nd,
-                          uint8_t* flags, hipStream_t st);
+// and a present bit (live and length - 1 > position) for rows [r_first, r_first + count) (r_first a
+// multiple of 64), or patched for the distinct rows ids[0..n)
+hipError_t launch_str_posfp(const uint64_t* row_beg, const uint32_t* row_len, const uint8_t* live, size_t r_first,
+                            size_t count, const uint32_t* fp, uint64_t position, uint32_t* posfp, uint64_t* present,
+                            hipStream_t st);
+hipError_t launch_str_posfp_ids(const uint32_t* ids, size_t n, const uint64_t* row_beg, const uint32_t* row_len,
+                                const uint8_t* live, const uint32_t* fp, uint64_t position, uint32_t* posfp,
+                                uint64_t* present, hipStream_t st);
+// string-table mutations: row descriptors of distinct rows ids[i] <- (beg[i], len[i]), live; heap
+// elements of superseded versions killed; heap compaction into fresh buffers (one wave per row)
+hipError_t launch_str_rows_set(const uint32_t* ids, const uint64_t* beg, const uint32_t* len, size_t n,
+                               uint64_t* row_beg, uint32_t* row_len, uint8_t* live, hipStream_t st);
+hipError_t launch_str_kill(const uint64_t* beg, const uint32_t* len, size_t n, uint32_t* elem_row, hipStream_t st);
+hipError_t launch_str_compact(size_t nrows, const uint64_t* old_beg, const uint32_t* len, const uint64_t* new_beg,
+                              const uint64_t* new_cbeg, const uint64_t* elem_off, const uint32_t* fp,
+                              const uint8_t* chars, uint64_t* nelem_off, uint32_t* nfp, uint32_t* nelem_row,
+                              uint8_t* nchars, hipStream_t st);
+// SearchEntry/OR/AND/IsElement: flag byte r - row0 |= bit j for every heap element in [e_first,
+// e_first + nelems) equal to needle j whose owner r is live and in [row0, row0 + nrows) (flags zeroed by
+// the launcher, 4-byte aligned)
+hipError_t launch_str_any(const uint32_t* fp, uint64_t e_first, size_t nelems, const uint32_t* elem_row,
+                          const uint8_t* live, size_t row0, size_t nrows, const uint64_t* elem_off, const uint8_t* chars,
+                          const uint8_t* nchars, const StrNeedles& nd, uint8_t* flags, hipStream_t st);
 hipError_t launch_plain_sum(const uint32_t* X, size_t stride, size_t count, int S, size_t nthreads, uint64_t* part,
                             uint64_t* out, hipStream_t st);
 // unbounded product tree level: rows (2p, 2p+1) of A[count][len] (radix 2^16 in u32)

@@ -31,7 +31,10 @@ struct dds_opecol {
   int64_t* d_val = nullptr;
   uint8_t* d_flg = nullptr;
   uint8_t* d_dead = nullptr;                            // 1 = removed set (allocated with the first one)
-  std::mutex mu;
+  // Search / Order / live_count hold it shared (concurrent requests on one column run side by side on
+  // their own worker streams, as the reference's routes do on the ForkJoin pool, DDSRestServer.scala:21);
+  // appends, row writes, liveness changes and truncation hold it exclusively
+  std::shared_mutex mu;
   std::vector<uint8_t> hflg;                            // host mirror of the class bytes (dead rows too)
   std::vector<uint8_t> hdead;                           // host mirror of d_dead (empty: none dead yet)
   size_t ndead = 0;
@@ -247,7 +250,7 @@ size_t dds_opecol_count(const dds_opecol* col) { return col ? col->count : 0; }
 
 int dds_opecol_truncate(dds_opecol* col, size_t count) {
   if (!col) return fail(DDS_E_ARG, "bad arguments");
-  std::lock_guard<std::mutex> lk(col->mu);
+  std::unique_lock<std::shared_mutex> lk(col->mu);
   if (count > col->count) return fail(DDS_E_ARG, "truncate beyond the row count");
   size_t undead = 0;
   for (size_t i = count; i < col->count; ++i) {
@@ -272,7 +275,7 @@ int dds_opecol_truncate(dds_opecol* col, size_t count) {
 int dds_opecol_append(dds_opecol* col, const int64_t* values, const uint8_t* cls, size_t count) {
   try {
     if (!col || (count && !values)) return fail(DDS_E_ARG, "bad arguments");
-    std::lock_guard<std::mutex> lk(col->mu);
+    std::unique_lock<std::shared_mutex> lk(col->mu);
     if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
     if (count == 0) return DDS_OK;
     std::vector<uint8_t> f(count);
@@ -291,7 +294,7 @@ int dds_opecol_append_dec(dds_opecol* col, const char* const* values, const uint
                           size_t count) {
   try {
     if (!col || (count && !values)) return fail(DDS_E_ARG, "bad arguments");
-    std::lock_guard<std::mutex> lk(col->mu);
+    std::unique_lock<std::shared_mutex> lk(col->mu);
     if (col->count + count > col->capacity) return fail(DDS_E_ARG, "column capacity exceeded");
     if (count == 0) return DDS_OK;
     OpeRows rows;
@@ -415,7 +418,7 @@ int dds_opecol_write_rows(dds_opecol* col, const uint64_t* row_ids, const int64_
                           size_t n) {
   try {
     if (!col || (n && (!row_ids || !values))) return fail(DDS_E_ARG, "bad arguments");
-    std::lock_guard<std::mutex> lk(col->mu);
+    std::unique_lock<std::shared_mutex> lk(col->mu);
     int rc = check_ids(col, row_ids, n);
     if (rc || n == 0) return rc;
     std::vector<uint8_t> f;
@@ -430,7 +433,7 @@ int dds_opecol_write_rows_dec(dds_opecol* col, const uint64_t* row_ids, const ch
                               const uint8_t* cls, const uint8_t* is_string, size_t n) {
   try {
     if (!col || (n && (!row_ids || !values))) return fail(DDS_E_ARG, "bad arguments");
-    std::lock_guard<std::mutex> lk(col->mu);
+    std::unique_lock<std::shared_mutex> lk(col->mu);
     int rc = check_ids(col, row_ids, n);
     if (rc || n == 0) return rc;
     OpeRows rows;
@@ -446,7 +449,7 @@ int dds_opecol_write_rows_dec(dds_opecol* col, const uint64_t* row_ids, const ch
 int dds_opecol_set_live(dds_opecol* col, const uint64_t* row_ids, size_t n, const uint8_t* live) {
   try {
     if (!col || (n && (!row_ids || !live))) return fail(DDS_E_ARG, "bad arguments");
-    std::lock_guard<std::mutex> lk(col->mu);
+    std::unique_lock<std::shared_mutex> lk(col->mu);
     int rc = check_ids(col, row_ids, n);
     if (rc || n == 0) return rc;
     return set_dead(col, row_ids, n, live);
@@ -457,7 +460,7 @@ int dds_opecol_set_live(dds_opecol* col, const uint64_t* row_ids, size_t n, cons
 
 size_t dds_opecol_live_count(dds_opecol* col) {
   if (!col) return 0;
-  std::lock_guard<std::mutex> lk(col->mu);
+  std::shared_lock<std::shared_mutex> lk(col->mu);
   return col->count - col->ndead;
 }
 
@@ -465,7 +468,7 @@ int dds_opecol_search(dds_opecol* col, const char* bound_dec, int op, uint32_t* 
   try {
     if (!col || !out_n || op < 0 || op > 3 || (col->count && !out_idx)) return fail(DDS_E_ARG, "bad arguments");
     *out_n = 0;
-    std::lock_guard<std::mutex> lk(col->mu);
+    std::shared_lock<std::shared_mutex> lk(col->mu);
     SearchBound sb;
     int rc = search_bound(col, bound_dec, op, &sb);
     if (rc || sb.none) return rc;
@@ -507,7 +510,7 @@ int dds_opecol_search_mask(dds_opecol* col, const char* bound_dec, int op, uint6
   try {
     if (!col || !out_n || op < 0 || op > 3) return fail(DDS_E_ARG, "bad arguments");
     *out_n = 0;
-    std::lock_guard<std::mutex> lk(col->mu);
+    std::shared_lock<std::shared_mutex> lk(col->mu);
     const size_t n = col->count, words = (n + 63) / 64;
     if (mask_words < words || (words && !mask)) return fail(DDS_E_BUFSIZE, "mask needs ceil(count / 64) words");
     SearchBound sb;
@@ -532,15 +535,26 @@ int dds_opecol_search_mask(dds_opecol* col, const char* bound_dec, int op, uint6
     HIP_TRY(launch_ope_mask(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, dtotal, wl.st, kSearch, kWide));
     record_time(ctx, w, wl.st, false, 2);
     uint8_t* h = (uint8_t*)w->hbig.p;
-    HIP_TRY(hipMemcpyAsync(h, mw, bytes, hipMemcpyDeviceToHost, wl.st));
-    HIP_TRY(hipMemcpyAsync(h + bytes, dtotal, 8, hipMemcpyDeviceToHost, wl.st));
-    HIP_TRY(hipStreamSynchronize(wl.st));
     uint64_t total = 0;
-    memcpy(&total, h + bytes, 8);
-    if (bytes >= ((size_t)1 << 20)) {
-      CopyPool::get().parallel_for(bytes, 4096, [&](size_t a, size_t e) { memcpy((char*)mask + a, h + a, e - a); });
+    if (host_registered(ctx, mask, bytes)) {
+      // the caller's buffer is page-locked (dds_host_register): one DMA straight into it, the count
+      // through the worker's pinned stage
+      uint32_t* stg = nullptr;
+      HIP_TRY(stage_ptr(w, &stg));
+      HIP_TRY(hipMemcpyAsync(mask, mw, bytes, hipMemcpyDeviceToHost, wl.st));
+      HIP_TRY(hipMemcpyAsync(stg, dtotal, 8, hipMemcpyDeviceToHost, wl.st));
+      HIP_TRY(hipStreamSynchronize(wl.st));
+      memcpy(&total, stg, 8);
     } else {
-      memcpy(mask, h, bytes);
+      HIP_TRY(hipMemcpyAsync(h, mw, bytes, hipMemcpyDeviceToHost, wl.st));
+      HIP_TRY(hipMemcpyAsync(h + bytes, dtotal, 8, hipMemcpyDeviceToHost, wl.st));
+      HIP_TRY(hipStreamSynchronize(wl.st));
+      memcpy(&total, h + bytes, 8);
+      if (bytes >= ((size_t)1 << 20)) {
+        CopyPool::get().parallel_for(bytes, 4096, [&](size_t a, size_t e) { memcpy((char*)mask + a, h + a, e - a); });
+      } else {
+        memcpy(mask, h, bytes);
+      }
     }
     add_filter_time(ctx, w);
     for (uint32_t r : wide_matches(col, sb, op)) {
@@ -557,7 +571,7 @@ int dds_opecol_search_mask(dds_opecol* col, const char* bound_dec, int op, uint6
 int dds_opecol_order(dds_opecol* col, int descending, uint32_t* out_idx, size_t* out_n) {
   try {
     if (!col || (col->count && !out_idx)) return fail(DDS_E_ARG, "bad arguments");
-    std::lock_guard<std::mutex> lk(col->mu);
+    std::shared_lock<std::shared_mutex> lk(col->mu);
     const size_t n = col->count;
     if (out_n) *out_n = 0;
     if (n == 0) return DDS_OK;

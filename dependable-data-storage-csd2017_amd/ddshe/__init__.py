@@ -59,6 +59,8 @@ EXPORTS = [
     "dds_mcol_write_rows", "dds_mcol_write_rows_dec", "dds_mcol_set_live", "dds_mcol_live_count",
     "dds_opecol_write_rows", "dds_opecol_write_rows_dec", "dds_opecol_set_live", "dds_opecol_live_count",
     "dds_opecol_search_mask", "dds_ctx_cache_stats",
+    "dds_strtab_append", "dds_strtab_write_rows", "dds_strtab_set_live", "dds_strtab_rows", "dds_strtab_live_count",
+    "dds_strtab_stats", "dds_strtab_truncate", "dds_host_register", "dds_host_unregister",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -108,6 +110,15 @@ _sig("dds_ope_order", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int,
 _sig("dds_ope_order_device", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_int, C.c_void_p)
 _sig("dds_strtab_create", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_void_p, _sz, C.POINTER(C.c_void_p))
 _sig("dds_strtab_destroy", C.c_int, C.c_void_p)
+_sig("dds_strtab_append", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _sz, C.c_void_p, _sz)
+_sig("dds_strtab_write_rows", C.c_int, C.c_void_p, C.c_void_p, _sz, C.c_void_p, C.c_void_p, _sz, C.c_void_p)
+_sig("dds_strtab_set_live", C.c_int, C.c_void_p, C.c_void_p, _sz, C.c_void_p)
+_sig("dds_strtab_rows", _sz, C.c_void_p)
+_sig("dds_strtab_live_count", _sz, C.c_void_p)
+_sig("dds_strtab_stats", C.c_int, C.c_void_p, C.c_void_p, _sz)
+_sig("dds_strtab_truncate", C.c_int, C.c_void_p, _sz)
+_sig("dds_host_register", C.c_int, C.c_void_p, C.c_void_p, _sz)
+_sig("dds_host_unregister", C.c_int, C.c_void_p, C.c_void_p)
 _sig("dds_search_eq", C.c_int, C.c_void_p, _sz, C.c_char_p, _sz, C.c_int, C.c_void_p, _szp)
 _sig("dds_search_entry", C.c_int, C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), _sz, C.c_int, C.c_void_p,
      _szp)
@@ -454,6 +465,13 @@ class Engine:
         raw = bytes(out)
         return [int.from_bytes(raw[i * mb:(i + 1) * mb], "big") for i in range(len(bases))]
 
+    def host_register(self, arr: np.ndarray):
+        """dds_host_register: page-lock a reusable output array (results DMA'd straight into it)."""
+        _check(_lib.dds_host_register(self._h, arr.ctypes.data_as(C.c_void_p), arr.nbytes), "dds_host_register")
+
+    def host_unregister(self, arr: np.ndarray):
+        _check(_lib.dds_host_unregister(self._h, arr.ctypes.data_as(C.c_void_p)), "dds_host_unregister")
+
     def strtab(self, rows) -> "StrTable":
         """Device-resident string table of the rows' contents (lists of values, str()-ed)."""
         return StrTable(self, rows)
@@ -677,9 +695,11 @@ class OpeColumn:
                                       out.ctypes.data_as(C.c_void_p), C.byref(got)), "dds_opecol_search")
         return out[: got.value].copy()
 
-    def search_mask(self, bound, op: str):
-        """dds_opecol_search_mask: (uint64 words, bit r%64 of word r/64 = row r matches; match count)."""
-        words = np.zeros(max(1, (len(self) + 63) // 64), dtype=np.uint64)
+    def search_mask(self, bound, op: str, out: np.ndarray | None = None):
+        """dds_opecol_search_mask: (uint64 words, bit r%64 of word r/64 = row r matches; match count).
+        out: a reusable uint64 buffer of at least ceil(rows / 64) words (Engine.host_register it once to
+        have the mask DMA'd straight in)."""
+        words = np.zeros(max(1, (len(self) + 63) // 64), dtype=np.uint64) if out is None else out
         got = C.c_size_t()
         _check(_lib.dds_opecol_search_mask(self._h, None if bound is None else str(bound).encode(), OPE_OPS[op],
                                            words.ctypes.data_as(C.c_void_p), len(words), C.byref(got)),
@@ -820,27 +840,79 @@ class MColumn(_Mutable):
         return out.value.decode()
 
 
+def element_text(v) -> str:
+    """``toString`` of a DDSSet element as AnyJsonFormat reads it (DDSJsonProtocol.scala:22-28): String as
+    is, Int in decimal, Boolean ``true``/``false``, JsNull ``None`` (the text HomoDet.compare sees)."""
+    if v is None:
+        return "None"
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    return str(v)
+
+
+def _flatten(rows):
+    """(chars, elem_off, row_off) of rows (lists of elements) in the dds_strtab batch layout"""
+    enc = [[element_text(v).encode() for v in row] for row in rows]
+    lens = np.fromiter((len(x) for row in enc for x in row), dtype=np.uint64)
+    elem_off = np.zeros(len(lens) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=elem_off[1:])
+    row_off = np.zeros(len(enc) + 1, dtype=np.uint64)
+    np.cumsum(np.fromiter((len(r) for r in enc), dtype=np.uint64, count=len(enc)), out=row_off[1:])
+    return b"".join(x for row in enc for x in row), elem_off, row_off
+
+
+STRTAB_STATS = ("rows", "live", "heap_elems", "elems", "heap_bytes", "bytes", "compactions", "pos_indexes")
+
+
 class StrTable:
-    """Device-resident contents of DDSSet rows for the deterministic-equality scans (dds_strtab)."""
+    """Device-resident contents of DDSSet rows for the deterministic-equality scans (dds_strtab); follows
+    the write routes in place (append / write_rows / set_live)."""
 
     def __init__(self, eng: Engine, rows=None, *, chars: bytes | None = None, elem_off=None, row_off=None):
         if rows is not None:
-            enc = [[str(v).encode() for v in row] for row in rows]
-            lens = np.fromiter((len(x) for row in enc for x in row), dtype=np.uint64)
-            elem_off = np.zeros(len(lens) + 1, dtype=np.uint64)
-            np.cumsum(lens, out=elem_off[1:])
-            row_off = np.zeros(len(enc) + 1, dtype=np.uint64)
-            np.cumsum(np.fromiter((len(r) for r in enc), dtype=np.uint64, count=len(enc)), out=row_off[1:])
-            chars = b"".join(x for row in enc for x in row)
-        self.elem_off = np.ascontiguousarray(elem_off, dtype=np.uint64)
-        self.row_off = np.ascontiguousarray(row_off, dtype=np.uint64)
-        self.nrows = len(self.row_off) - 1
-        self._chars = chars or b"\0"
+            chars, elem_off, row_off = _flatten(rows)
+        elem_off = np.ascontiguousarray(elem_off, dtype=np.uint64)
+        row_off = np.ascontiguousarray(row_off, dtype=np.uint64)
         h = C.c_void_p()
-        _check(_lib.dds_strtab_create(eng._h, C.c_char_p(self._chars), self.elem_off.ctypes.data_as(C.c_void_p),
-                                      len(self.elem_off) - 1, self.row_off.ctypes.data_as(C.c_void_p), self.nrows,
+        _check(_lib.dds_strtab_create(eng._h, C.c_char_p(chars or b"\0"), elem_off.ctypes.data_as(C.c_void_p),
+                                      len(elem_off) - 1, row_off.ctypes.data_as(C.c_void_p), len(row_off) - 1,
                                       C.byref(h)), "dds_strtab_create")
         self._h = h
+
+    @property
+    def nrows(self) -> int:
+        return _lib.dds_strtab_rows(self._h)
+
+    def live_count(self) -> int:
+        return _lib.dds_strtab_live_count(self._h)
+
+    def stats(self) -> dict:
+        out = np.zeros(len(STRTAB_STATS), dtype=np.uint64)
+        _check(_lib.dds_strtab_stats(self._h, out.ctypes.data_as(C.c_void_p), len(out)), "dds_strtab_stats")
+        return dict(zip(STRTAB_STATS, (int(x) for x in out)))
+
+    def append(self, rows):
+        chars, eo, ro = _flatten(rows)
+        _check(_lib.dds_strtab_append(self._h, C.c_char_p(chars or b"\0"), eo.ctypes.data_as(C.c_void_p), len(eo) - 1,
+                                      ro.ctypes.data_as(C.c_void_p), len(ro) - 1), "dds_strtab_append")
+
+    def write_rows(self, ids, rows):
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        chars, eo, ro = _flatten(rows)
+        if len(ro) - 1 != len(ids):
+            raise ValueError("one row per id")
+        _check(_lib.dds_strtab_write_rows(self._h, ids.ctypes.data_as(C.c_void_p), len(ids), C.c_char_p(chars or b"\0"),
+                                          eo.ctypes.data_as(C.c_void_p), len(eo) - 1, ro.ctypes.data_as(C.c_void_p)),
+               "dds_strtab_write_rows")
+
+    def truncate(self, rows: int = 0):
+        _check(_lib.dds_strtab_truncate(self._h, rows), "dds_strtab_truncate")
+
+    def set_live(self, ids, live):
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        lv = np.broadcast_to(np.asarray(live, dtype=np.uint8), ids.shape).copy()
+        _check(_lib.dds_strtab_set_live(self._h, ids.ctypes.data_as(C.c_void_p), len(ids), lv.ctypes.data_as(C.c_void_p)),
+               "dds_strtab_set_live")
 
     def close(self):
         if self._h:
@@ -854,7 +926,7 @@ class StrTable:
             pass
 
     def search_eq(self, position: int, value, negate: bool = False) -> np.ndarray:
-        v = str(value).encode()
+        v = element_text(value).encode()
         out = np.empty(max(1, self.nrows), dtype=np.uint32)
         n = C.c_size_t()
         _check(_lib.dds_search_eq(self._h, position, v, len(v), int(negate), out.ctypes.data_as(C.c_void_p),
@@ -862,7 +934,7 @@ class StrTable:
         return out[: n.value].copy()
 
     def search_entry(self, values, require_all: bool = False) -> np.ndarray:
-        vs = [str(v).encode() for v in values]
+        vs = [element_text(v).encode() for v in values]
         arr = (C.c_char_p * len(vs))(*vs)
         lens = (C.c_size_t * len(vs))(*[len(v) for v in vs])
         out = np.empty(max(1, self.nrows), dtype=np.uint32)
@@ -872,7 +944,7 @@ class StrTable:
         return out[: n.value].copy()
 
     def is_element(self, row: int, value) -> bool:
-        v = str(value).encode()
+        v = element_text(value).encode()
         f = C.c_int()
         _check(_lib.dds_is_element(self._h, row, v, len(v), C.byref(f)), "dds_is_element")
         return bool(f.value)

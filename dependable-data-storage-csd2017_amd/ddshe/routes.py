@@ -18,7 +18,7 @@ follows the write routes: ``ddshe.store.ResidentStore``.
 """
 from __future__ import annotations
 
-from . import DDSError, Engine
+from . import DDSError, Engine, element_text
 from . import NotFound as _EngineNotFound
 from . import OPE_CLS_INNER, OPE_CLS_LACKS, OPE_CLS_LAST
 from .x509 import rsa_modulus
@@ -244,6 +244,12 @@ def search_eq(eng: Engine, route: str, keyed_rows, position: int, value) -> list
     return [keys[i] for i in idx]
 
 
+def entry_needle(value) -> str:
+    """SearchEntry compares ``item.toString`` (DDSRestServer.scala:845), the DDSItem case class's text
+    ``DDSItem(<value>)`` (DDSJsonProtocol.scala:7); OR / AND / IsElement compare the values themselves."""
+    return "DDSItem(" + element_text(value) + ")"
+
+
 def search_entry(eng: Engine, route: str, keyed_rows, values) -> list:
     """POST /SearchEntry (one value) | /SearchEntryOR | /SearchEntryAND (three) —
     DDSRestServer.scala:831-938."""
@@ -252,9 +258,10 @@ def search_entry(eng: Engine, route: str, keyed_rows, values) -> list:
     keys, rows = _live(keyed_rows)
     if not keys:
         return []
+    values = [entry_needle(values[0])] if route == "SearchEntry" else list(values)
     tab = eng.strtab(rows)
     try:
-        idx = _call(tab.search_entry, list(values), route == "SearchEntryAND")
+        idx = _call(tab.search_entry, values, route == "SearchEntryAND")
     finally:
         tab.close()
     return [keys[i] for i in idx]

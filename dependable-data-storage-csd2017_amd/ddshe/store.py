@@ -18,10 +18,13 @@ its content (SumAll/MultAll collapse equal sets: ``Future.sequence`` over a Set,
 C-ABI keeps the live mask on the device (``dds_col_set_live``) and folds only live rows; row values
 change by ``dds_col_write_rows_dec``. The OPE column carries each row's class (lacks the position /
 last element / elements follow) and a live flag (set present), ``dds_opecol_write_rows_dec`` /
-``dds_opecol_set_live``. Requests the resident columns cannot answer bit for bit (another modulus than
-the column's, the plain add / multiply branch without ``nsqr`` / ``pubkey``, a position without a
-column) go through ``ddshe.routes`` over the mirrored rows, which is the same batched engine path the
-route would take without a resident column.
+``dds_opecol_set_live``. The string table (``dds_strtab``) holds every row's contents for the
+deterministic-equality scans (SearchEq/NEq :607-681, SearchEntry/OR/AND :831-938, IsElement
+:322-353): a write gives the row new contents (``dds_strtab_write_rows``), RemoveSet clears its live
+byte (``dds_strtab_set_live``). Requests the resident columns cannot answer bit for bit (another
+modulus than the column's, the plain add / multiply branch without ``nsqr`` / ``pubkey``, a position
+without a column) go through ``ddshe.routes`` over the mirrored rows, which is the same batched engine
+path the route would take without a resident column.
 """
 from __future__ import annotations
 
@@ -29,10 +32,10 @@ import hashlib
 
 import numpy as np
 
-from . import DDSError, Engine, OPE_CLS_INNER, OPE_CLS_LACKS, OPE_CLS_LAST
+from . import DDSError, Engine, OPE_CLS_INNER, OPE_CLS_LACKS, OPE_CLS_LAST, StrTable
 from . import NotFound as _EngineNotFound
 from . import routes
-from .routes import NotFound, ServerError, _dec_text, _value_key
+from .routes import NotFound, ServerError, _dec_text, _value_key, entry_needle
 from .x509 import rsa_modulus
 
 
@@ -96,11 +99,12 @@ class ResidentStore:
     paillier: {position: n^2} — SumAll columns (the client's ``nsqr``, DDSHttpClient.scala:228-240)
     rsa:      {position: n}   — MultAll columns (the modulus of the client's ``pubkey``)
     ope:      positions of OPE columns (Search{Gt,GtEq,Lt,LtEq}, OrderLS/OrderSL)
+    strings:  keep a resident string table (SearchEq/NEq, SearchEntry/OR/AND, IsElement)
     Keys are derived as the reference derives them (SHA-512 of the set's text); the mirror's row order
     is insertion order.
     """
 
-    def __init__(self, eng: Engine, paillier=None, rsa=None, ope=(), capacity: int = 1 << 16):
+    def __init__(self, eng: Engine, paillier=None, rsa=None, ope=(), capacity: int = 1 << 16, strings: bool = True):
         self.eng, self.capacity = eng, capacity
         self.keys: list[str] = []
         self.row: dict[str, int] = {}
@@ -111,12 +115,15 @@ class ResidentStore:
         self.by_pos_sum = {c.position: c for c in self.cols[:len(paillier or {})]}
         self.by_pos_mult = {c.position: c for c in self.cols[len(paillier or {}):]}
         self.ope = {p: eng.opecol(capacity) for p in ope}
+        self.tab = StrTable(eng, []) if strings else None
 
     def close(self):
         for c in self.cols:
             c.col.close()
         for oc in self.ope.values():
             oc.close()
+        if self.tab is not None:
+            self.tab.close()
 
     # ---- row state ----
     @staticmethod
@@ -185,7 +192,8 @@ class ResidentStore:
             oc.set_live(ids, [1 if lv else 0 for _, _, _, lv in st])
 
     def _append(self, keys, contents):
-        """new rows for new keys (one batched append per column)"""
+        """new rows for new keys (one batched append per column); a failed append leaves the store and
+        every column as they were"""
         r0 = len(self.keys)
         if r0 + len(keys) > self.capacity:
             raise ServerError("resident store capacity exceeded")
@@ -197,28 +205,65 @@ class ResidentStore:
         for i, cont in enumerate(contents):
             touched |= self._regroup(r0 + i, None, self.val[r0 + i])
         new = range(r0, r0 + len(keys))
-        for c in self.cols:
-            st = [self._cipher_state(c, r) for r in new]
-            c.col.append_dec([t for t, _, _ in st])
-            for r, (_, lv, bad) in zip(new, st):
-                c.mark(r, lv, bad)
-            dead = [r for r, (_, lv, _) in zip(new, st) if not lv]
-            if dead:
-                c.col.set_live(np.asarray(dead, dtype=np.uint64), 0)
-        for p, oc in self.ope.items():
-            st = [self._ope_state(p, r) for r in new]
-            oc.append_dec([t for t, _, _, _ in st], [k for _, k, _, _ in st], [s for _, _, s, _ in st])
-            dead = [r for r, (_, _, _, lv) in zip(new, st) if not lv]
-            if dead:
-                oc.set_live(np.asarray(dead, dtype=np.uint64), 0)
+        try:
+            for c in self.cols:
+                st = [self._cipher_state(c, r) for r in new]
+                c.col.append_dec([t for t, _, _ in st])
+                for r, (_, lv, bad) in zip(new, st):
+                    c.mark(r, lv, bad)
+                dead = [r for r, (_, lv, _) in zip(new, st) if not lv]
+                if dead:
+                    c.col.set_live(np.asarray(dead, dtype=np.uint64), 0)
+            for p, oc in self.ope.items():
+                st = [self._ope_state(p, r) for r in new]
+                oc.append_dec([t for t, _, _, _ in st], [k for _, k, _, _ in st], [s for _, _, s, _ in st])
+                dead = [r for r, (_, _, _, lv) in zip(new, st) if not lv]
+                if dead:
+                    oc.set_live(np.asarray(dead, dtype=np.uint64), 0)
+            if self.tab is not None:
+                self.tab.append([self.val[r] or [] for r in new])
+                dead = [r for r in new if self.val[r] is None]
+                if dead:
+                    self.tab.set_live(np.asarray(dead, dtype=np.uint64), 0)
+        except Exception:
+            self._rollback(r0)
+            raise
         old = touched - set(new)  # (a new row never displaces an earlier group member; kept general)
         if old:
             self._apply(old)
+
+    def _rollback(self, r0):
+        """drop rows r0.. from the mirror and from every device column (an append that raised)"""
+        for r in range(len(self.keys) - 1, r0 - 1, -1):
+            s = self._sig(self.val[r])
+            if s is not None:
+                g = self.groups[s]
+                g.remove(r)
+                if not g:
+                    del self.groups[s]
+            del self.row[self.keys[r]]
+            for c in self.cols:
+                if r < len(c.live):
+                    c.mark(r, False, False)
+        del self.keys[r0:]
+        del self.val[r0:]
+        for c in self.cols:
+            c.col.truncate(r0)
+        for oc in self.ope.values():
+            oc.truncate(r0)
+        if self.tab is not None:
+            self.tab.truncate(r0)
 
     def _set(self, r, contents):
         old = self.val[r]
         self.val[r] = None if contents is None else list(contents)
         self._apply(self._regroup(r, old, self.val[r]))
+        if self.tab is not None:
+            ids = np.asarray([r], dtype=np.uint64)
+            if self.val[r] is None:
+                self.tab.set_live(ids, 0)  # RemoveSet: the register holds None
+            else:
+                self.tab.write_rows(ids, [self.val[r]])
 
     # ---- write routes ----
     def put_sets(self, sets) -> list[str]:
@@ -357,3 +402,44 @@ class ResidentStore:
         except DDSError as e:
             raise ServerError(str(e)) from e
         return [self.keys[i] for i in idx]
+
+    def search_eq(self, route: str, position: int, value) -> list[str]:
+        """POST /SearchEq|/SearchNEq?position (:607-681): keys in row order (the reference's order is
+        unspecified)"""
+        if route not in ("SearchEq", "SearchNEq"):
+            raise ValueError(route)
+        if self.tab is None:
+            return routes.search_eq(self.eng, route, self.keyed_rows(), position, value)
+        try:
+            idx = self.tab.search_eq(position, value, route == "SearchNEq")
+        except DDSError as e:
+            raise ServerError(str(e)) from e
+        return [self.keys[i] for i in idx]
+
+    def search_entry(self, route: str, values) -> list[str]:
+        """POST /SearchEntry (one value, compared as ``DDSItem(value)``, :845) | /SearchEntryOR |
+        /SearchEntryAND (three, :831-938)"""
+        if route not in ("SearchEntry", "SearchEntryOR", "SearchEntryAND"):
+            raise ValueError(route)
+        if self.tab is None:
+            return routes.search_entry(self.eng, route, self.keyed_rows(), values)
+        needles = [entry_needle(values[0])] if route == "SearchEntry" else list(values)
+        try:
+            idx = self.tab.search_entry(needles, route == "SearchEntryAND")
+        except DDSError as e:
+            raise ServerError(str(e)) from e
+        return [self.keys[i] for i in idx]
+
+    def is_element(self, key: str, value) -> bool:
+        """POST /IsElement/{key} (:322-353): 404 for an unknown key or a removed set"""
+        r = self.row.get(key)
+        if r is None or self.val[r] is None:
+            raise NotFound()
+        if self.tab is None:
+            return routes.is_element(self.eng, self.val[r], value)
+        try:
+            return self.tab.is_element(r, value)
+        except _EngineNotFound as e:
+            raise NotFound() from e
+        except DDSError as e:
+            raise ServerError(str(e)) from e

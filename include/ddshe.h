@@ -108,6 +108,13 @@ int dds_pair_stats(dds_ctx* ctx, uint64_t* calls, uint64_t* launches);
 /* Sizes of the per-request caches: modulus constants (LRU, at most DDSHE_MAX_MODULI, default 64) and
  * pairwise queues (one per modulus with calls in flight; dropped when idle). */
 int dds_ctx_cache_stats(dds_ctx* ctx, size_t* moduli, size_t* pair_queues);
+/* Page-lock a caller output buffer the caller reuses across requests (a JNA Memory, a direct
+ * ByteBuffer): results bound for it (dds_opecol_search_mask's bitmask, row-id lists of the searches
+ * and orders) are then DMA'd straight in, without a pinned staging buffer and a second host copy.
+ * Registered ranges must not overlap; the buffer must stay allocated until dds_host_unregister (or
+ * dds_ctx_destroy, which unregisters every buffer). */
+int dds_host_register(dds_ctx* ctx, void* ptr, size_t bytes);
+int dds_host_unregister(dds_ctx* ctx, void* ptr);
 /* SumAll without nsqr (plain BigInteger add, DDSRestServer.scala:425): sum of count
  * operands; result big-endian in out (min(out_cap) = width + 8 is always enough). */
 int dds_bigint_sum(dds_ctx* ctx, const uint8_t* operands_be, size_t width, size_t count, uint8_t* out,
@@ -308,8 +315,10 @@ int dds_ope_order_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_va
  * HomoDet.compare (hlib, absent) is taken as equality of the ciphertext strings.
  * A string table holds the rows' contents: element e is chars[elem_offsets[e], elem_offsets[e+1]),
  * row r is elements [row_offsets[r], row_offsets[r+1]) (its DDSSet.contents, in column order;
- * DDSSet.scala:3). The table is device-resident with a 64-bit digest per element; results are
- * exact (bytes are compared on a digest hit). out_rows receives ascending row ids (capacity nrows).
+ * DDSSet.scala:3). The table is device-resident with a 32-bit fingerprint per element; results are
+ * exact (bytes are compared on a fingerprint hit). out_rows receives ascending ids of live rows
+ * (capacity: the table's rows when the scan runs; a caller that appends to the table from another
+ * thread sizes it for the rows after those appends).
  *   dds_search_eq     SearchEq / SearchNEq (negate != 0), DDSRestServer.scala:607-681: rows with
  *                     length-1 > position whose element `position` equals / differs from value.
  *   dds_search_entry  SearchEntry (1 value), SearchEntryOR (3, require_all = 0) and
@@ -319,6 +328,27 @@ int dds_ope_order_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_va
 int dds_strtab_create(dds_ctx* ctx, const char* chars, const uint64_t* elem_offsets, size_t nelems,
                       const uint64_t* row_offsets, size_t nrows, dds_strtab** out);
 int dds_strtab_destroy(dds_strtab* tab);
+/* The table follows the write routes in place (DDSRestServer.scala:170-321), as the resident columns
+ * do. Batches use the create layout (chars, elem_offsets[nelems+1], row_offsets[nrows+1], both from 0).
+ *   dds_strtab_append      PutSet of new keys: rows nrows.. (live)
+ *   dds_strtab_write_rows  PutSet of a stored key / AddElement / WriteElement: row row_ids[i] takes the
+ *                          contents of batch row i (a repeated id takes its last row) and is live again
+ *   dds_strtab_set_live    RemoveSet (live 0: the register holds None, every scan skips the row and
+ *                          IsElement answers DDS_E_EMPTY) and its revival (live 1, last contents)
+ *   dds_strtab_truncate    drop the rows from `rows` on (a failed batched PutSet rolled back)
+ *   dds_strtab_stats       out[0..n) of: rows, live rows, heap elements, elements of the rows' current
+ *                          contents, heap bytes, bytes of the current contents, heap compactions,
+ *                          cached SearchEq position indexes
+ * Scans on one table run concurrently with each other; a write waits for them (and they for it). */
+int dds_strtab_append(dds_strtab* tab, const char* chars, const uint64_t* elem_offsets, size_t nelems,
+                      const uint64_t* row_offsets, size_t nrows);
+int dds_strtab_write_rows(dds_strtab* tab, const uint64_t* row_ids, size_t n, const char* chars,
+                          const uint64_t* elem_offsets, size_t nelems, const uint64_t* row_offsets);
+int dds_strtab_set_live(dds_strtab* tab, const uint64_t* row_ids, size_t n, const uint8_t* live);
+size_t dds_strtab_rows(dds_strtab* tab);
+size_t dds_strtab_live_count(dds_strtab* tab);
+int dds_strtab_truncate(dds_strtab* tab, size_t rows);
+int dds_strtab_stats(dds_strtab* tab, uint64_t* out, size_t n);
 int dds_search_eq(dds_strtab* tab, size_t position, const char* value, size_t len, int negate, uint32_t* out_rows,
                   size_t* out_n);
 int dds_search_entry(dds_strtab* tab, const char* const* values, const size_t* lens, size_t nvalues, int require_all,

@@ -334,7 +334,16 @@ def order(route: str, keyed_rows, position: int) -> list:
 # deterministic scheme compares ciphertexts by equality, so compare(a, b) := a == b on the
 # strings (unpinned beyond that assumption).
 def homo_det_compare(a, b) -> bool:
-    return str(a) == str(b)
+    """HomoDet.compare(a.toString, b.toString) as string equality (both sides as AnyJsonFormat reads
+    them, ``DDSJsonProtocol.scala:22-28``)."""
+    return element_to_string(a) == element_to_string(b)
+
+
+def entry_needle(value) -> str:
+    """The text SearchEntry compares (``DDSRestServer.scala:845``): ``item.toString`` of the DDSItem case
+    class (``DDSJsonProtocol.scala:7``), i.e. ``DDSItem(<value>)`` -- not ``item.value.toString`` as
+    SearchEntryOR/AND (``:881-883``, ``:918-920``) and IsElement (``:338``) use."""
+    return "DDSItem(" + element_to_string(value) + ")"
 
 
 def search_eq(route: str, keyed_rows, position: int, value) -> set:
@@ -355,18 +364,23 @@ def search_entry(route: str, keyed_rows, values) -> set:
     """``POST /SearchEntry`` (one value), ``/SearchEntryOR`` and ``/SearchEntryAND`` (three) —
     ``DDSRestServer.scala:831-938``: a row qualifies when some element equals the value (Entry),
     any of the three (OR, ``:881-883``), or when the set of its elements equal to one of the three
-    reaches size 3 (AND, ``:918-927``: all three present and pairwise distinct). The per-row
-    ``break`` (``:851,886,926``) is read as "stop scanning this row"."""
-    values = [str(v) for v in values]
+    reaches size 3 (AND, ``:918-927``: all three present and pairwise distinct). SearchEntry's single
+    value is compared as ``item.toString`` (``entry_needle``). The per-row ``break``
+    (``:851,886,926``) is read as "stop scanning this row" (literally it throws Breaks'
+    BreakControl outside any ``breakable``)."""
+    if route == "SearchEntry":
+        values = [entry_needle(values[0])]
+    else:
+        values = [element_to_string(v) for v in values]
     out = set()
     for key, row in keyed_rows:
         if row is None:
             continue
         if route == "SearchEntryAND":
-            found = {str(e) for e in row if str(e) in values}
+            found = {element_to_string(e) for e in row if element_to_string(e) in values}
             if len(found) == 3:
                 out.add(key)
-        elif any(str(e) in values for e in row):
+        elif any(element_to_string(e) in values for e in row):
             out.add(key)
     return out
 

@@ -242,7 +242,27 @@ def _reads(st: homo.Store, nsq: int, pubkey: str, bound: str):
         out[route] = keys_of(_outcome(homo.search, route, keyed, MUT_OPE_POS, bound), True)
     for route in ("OrderLS", "OrderSL"):
         out[route] = keys_of(_outcome(homo.order, route, keyed, MUT_OPE_POS), False)
+    # deterministic-equality scans (VERDICT r03 "next" 2): the string table follows the same writes
+    for route, pos, value in MUT_EQ_READS:
+        out[f"{route}@{pos}:{value}"] = keys_of(_outcome(homo.search_eq, route, keyed, pos, value), True)
+    for route, values in MUT_ENTRY_READS:
+        out[f"{route}:{','.join(values)}"] = keys_of(_outcome(homo.search_entry, route, keyed, values), True)
+    probes = [i for i in range(min(3, len(st.keys)))] + [idx[k] for k in ("E" * 128,) if k in idx] + [-1]
+    res = []
+    for i in probes:
+        for value in MUT_ISELEM_VALUES:
+            row = st.val.get(st.keys[i]) if i >= 0 else None
+            res.append([i, value, _outcome(homo.is_element, row, value)])
+    out["IsElement"] = res
     return out
+
+
+# string-scan reads after every mutation step: CHE column 1 ("che<i>"), the OPE column 0 as text, and
+# the trailing "x" / "y" elements; "DDSItem(x)" is the text SearchEntry compares for the value "x"
+MUT_EQ_READS = (("SearchEq", 1, "che1"), ("SearchNEq", 1, "che1"), ("SearchEq", 0, "7"), ("SearchNEq", 4, "x"))
+MUT_ENTRY_READS = (("SearchEntry", ("x",)), ("SearchEntry", ("che2",)), ("SearchEntryOR", ("che3", "zz", "w")),
+                   ("SearchEntryAND", ("x", "y", "che0")), ("SearchEntryAND", ("x", "x", "che0")))
+MUT_ISELEM_VALUES = ("x", "che1", "DDSItem(x)")
 
 
 def mutation_vectors(pk, rsa, seed=2026, n_random=240):
@@ -304,6 +324,8 @@ def mutation_vectors(pk, rsa, seed=2026, n_random=240):
     step("write", key="F" * 128, position=0, value="1")  # unknown key: 404
     step("write", key=a, position=-1, value="1")  # IndexOutOfBounds: 500, nothing written
     step("write", key=a, position=3, value=str(n + 17))  # RSA operand above n (reduced by the fold)
+    step("write", key=b, position=6, value="DDSItem(x)")  # SearchEntry("x") compares item.toString (:845)
+    step("add", key=d, value="che1")             # a second "che1" element, not at position 1
     for k in (b, c, d, f):
         step("remove", key=k)
     step("write", key=a, position=2, value=str(nsq + 5))  # one live operand >= nsq: returned unreduced
@@ -336,6 +358,8 @@ def mutation_vectors(pk, rsa, seed=2026, n_random=240):
             val = {0: ope[rng.randrange(10)], 2: pc[rng.randrange(12)], 3: rc[rng.randrange(12)]}.get(at, "v")
             if rng.random() < 0.03:
                 val = "bad"
+            elif at in (1, 4, 5, 6) and rng.random() < 0.5:  # string elements the equality scans look for
+                val = rng.choice(["che1", "che2", "che3", "x", "y", "zz", "w", "DDSItem(x)"])
             step("write", key=k, position=pos, value=val)
         else:
             step("remove", key=rng.choice(keys))

@@ -76,6 +76,20 @@ def test_mutation_sequences_golden(eng):
             for route in ("OrderLS", "OrderSL"):
                 r = _outcome(st.order, route, pos["ope"])
                 got[route] = r if isinstance(r, dict) else [idx[k] for k in r]
+            # the resident string table under the same writes (SearchEq/NEq, SearchEntry/OR/AND, IsElement)
+            for name in want:
+                if name.startswith("SearchEq@") or name.startswith("SearchNEq@"):
+                    route, rest = name.split("@")
+                    p, value = rest.split(":", 1)
+                    r = _outcome(st.search_eq, route, int(p), value)
+                elif name.startswith("SearchEntry"):
+                    route, values = name.split(":", 1)
+                    r = _outcome(st.search_entry, route, values.split(","))
+                else:
+                    continue
+                got[name] = r if isinstance(r, dict) else sorted(idx[k] for k in r)
+            got["IsElement"] = [[ki, value, _outcome(st.is_element, st.keys[ki] if ki >= 0 else "F" * 128, value)]
+                                for ki, value, _ in want["IsElement"]]
             for route, w in want.items():
                 if got[route] != w:
                     bad.append((i, op, route, str(w)[:80], str(got[route])[:80]))
