@@ -214,11 +214,23 @@ class _Workload:
         for i in range(parts):
             fold_share(i)
         share_ms = med(lambda: fold_share(0))
+        # the share's first level alone (HIP events around its k_fold launch): the rest of share_ms is
+        # its tail (reduction of the level-1 partials to one device partial) plus the host call
+        self.eng.set_timing(True)
+        self.eng.reset_timing()
+        for _ in range(5):
+            fold_share(0)
+        lvl_ms, lvl_n, _, _ = self.eng.timing()
+        self.eng.set_timing(False)
+        level1_ms = lvl_ms / lvl_n if lvl_n else None
         rows = [cnt] * parts
         got = self.eng.combine_partials_device(self.nsq, buf.data_ptr(), rows)
         comb_ms = med(lambda: self.eng.combine_partials_device(self.nsq, buf.data_ptr(), rows))
+        tail_ms = share_ms - level1_ms if level1_ms else None
         return {"rows_per_share": cnt, "shares": parts, "share_fold_partial_ms": share_ms,
+                "share_level1_ms": level1_ms, "share_fold_tail_ms": tail_ms,
                 "combine_ms": comb_ms, "combined_equals_full_fold": got == full if cnt * parts == self.mine else None,
+                "tail_plus_combine_share": (tail_ms + comb_ms) / (share_ms + comb_ms) if tail_ms else None,
                 "note": "an 8-GPU strong-split step is about share_fold_partial_ms + one all-gather of "
                         f"{parts}x{4 * pw} B + combine_ms (host wall clock, each call synchronised)"}
 
@@ -995,7 +1007,35 @@ class OrderWorkload(_Workload):
                           elapsed, "ope_orderls_10M", {})
         out.update(data="synthetic (seeded OPE map of U[1,10^4) plaintexts, 5% rows lacking the position)",
                    dtype="int64", roofline=roof, cpu_baseline=cpu, verified=ok)
+        if self.world == 1:
+            try:
+                out["resident_opecol_order"] = self.resident_order()
+            except Exception as e:  # noqa: BLE001
+                out["resident_opecol_order"] = {"error": repr(e)}
         return out
+
+    def resident_order(self):
+        """The serving form: OrderLS on the same rows as a resident OPE column (dds_opecol_order: the
+        column's value bounds are kept on its writes, so no min/max pass; ids back in host memory)."""
+        import numpy as np
+        oc = self.eng.opecol(max(1, self.mine))
+        try:
+            oc.append(self.col, np.where(self.valid != 0, 2, 0).astype(np.uint8))
+            ts = []
+            for _ in range(7):
+                t = time.perf_counter()
+                perm = oc.order(True)
+                ts.append((time.perf_counter() - t) * 1e3)
+            ts.sort()
+            ok = bool(np.array_equal(perm, self.d_out.cpu().numpy().view(np.uint32))) if self.args.verify else None
+            med = ts[len(ts) // 2]
+            return {"median_ms": med, "matches_raw_array_order": ok,
+                    "route_roofline": {"bound": "hbm", "achieved": 13 * self.mine / (med / 1e3) / 1e9, "peak": 8000.0,
+                                       "unit": "GB/s", "frac": 13 * self.mine / (med / 1e3) / 1e9 / 8000.0,
+                                       "note": "13 B/row / whole call time (host clock), the 40 MB id read-back included"},
+                    "path": "dds_opecol_order (no k_rs_prep: bounds kept on writes) + D2H of the permutation"}
+        finally:
+            oc.close()
 
 
 class EntrySearchWorkload(_Workload):
@@ -1016,9 +1056,57 @@ class EntrySearchWorkload(_Workload):
         chars = self.vocab[self.pick].tobytes()
         elem_off = np.arange(nel + 1, dtype=np.uint64) * self.WIDTH
         row_off = np.arange(self.mine + 1, dtype=np.uint64) * self.ELEMS
+        t = time.perf_counter()
         self.tab = self.ddshe.StrTable(self.eng, chars=chars, elem_off=elem_off, row_off=row_off)
+        self.build_s = time.perf_counter() - t
         del chars
         self.needles = [self.vocab[j].tobytes().decode() for j in (11, 222, 3333)]
+
+    def _batch(self, picks):
+        """(chars, elem_off, row_off) of rows given as vocabulary indices (rows x ELEMS)"""
+        import numpy as np
+        n = picks.shape[0]
+        return (self.vocab[picks.reshape(-1)].tobytes(), np.arange(n * self.ELEMS + 1, dtype=np.uint64) * self.WIDTH,
+                np.arange(n + 1, dtype=np.uint64) * self.ELEMS)
+
+    def mutations(self):
+        """The table under the write routes (outside the timed region): the per-request build the parity
+        form pays without a resident table, then row rewrites / removals / appends on the resident table
+        (C calls on batches already in the table layout), then the scans again, verified."""
+        import numpy as np
+        rng = np.random.default_rng(self.args.seed + 1)
+        out = {"table_build_ms": self.build_s * 1e3,
+               "table_build_note": "dds_strtab_create of the whole table from host buffers (upload + fingerprints): "
+                                   "what a request pays without the resident table (routes.search_* parity form)"}
+        p = self.pick.reshape(self.mine, self.ELEMS)
+        live = np.ones(self.mine, dtype=bool)
+
+        def timed(fn, reps=5):
+            ts = []
+            for _ in range(reps):
+                t = time.perf_counter()
+                fn()
+                ts.append((time.perf_counter() - t) * 1e3)
+            ts.sort()
+            return ts[len(ts) // 2]
+
+        for nrow in (1, 1000, 100_000):
+            ids = rng.choice(self.mine, nrow, replace=False).astype(np.uint64)
+            picks = rng.integers(0, self.VOCAB, size=(nrow, self.ELEMS))
+            batch = self._batch(picks)
+            out[f"write_rows_{nrow}_ms"] = timed(lambda: self.tab.write_rows_flat(ids, *batch))
+            p[ids.astype(np.int64)] = picks
+        ids = rng.choice(self.mine, 1000, replace=False).astype(np.uint64)
+        out["set_live_1000_ms"] = timed(lambda: self.tab.set_live(ids, 0))
+        live[ids.astype(np.int64)] = False
+        out["search_after_writes_ms"] = timed(lambda: self.tab.search_entry(self.needles, False), 3)
+        got_or = self.tab.search_entry(self.needles, False)
+        got_eq = self.tab.search_eq(3, self.needles[0])
+        want_or = np.nonzero(np.isin(p, [11, 222, 3333]).any(axis=1) & live)[0]
+        want_eq = np.nonzero((p[:, 3] == 11) & live)[0]
+        out["verified_after_writes"] = bool(np.array_equal(got_or, want_or) and np.array_equal(got_eq, want_eq))
+        out["stats"] = self.tab.stats()
+        return out
 
     def step(self):
         a = self.tab.search_entry(self.needles, False)
@@ -1043,7 +1131,7 @@ class EntrySearchWorkload(_Workload):
         alg_or = self.mine * 4 * self.ELEMS + 4 * len(res[0])
         alg_eq = self.mine * (8 + 4) + 4 * len(res[1])
         alg = (alg_or + alg_eq) / 2
-        roof = {"bound": "hbm", "kernel": "k_str_any / k_str_eq + k_flag_count/k_ope_scatter (device time)",
+        roof = {"bound": "hbm", "kernel": "k_str_any + k_byte_count/k_ope_scatter (OR), k_str_eq_count + k_ope_scatter (Eq); device time",
                 "achieved": alg / scan_s / 1e9, "peak": 8000.0, "unit": "GB/s", "frac": alg / scan_s / 1e9 / 8000.0,
                 "avg_scan_ms": scan_s * 1e3, "algorithmic_bytes": alg, "traffic": None}
         cpu = None
@@ -1063,6 +1151,11 @@ class EntrySearchWorkload(_Workload):
                           {"elements_per_row": self.ELEMS, "element_bytes": self.WIDTH})
         out.update(data="synthetic (seeded 32-hex-char ciphertext vocabulary)", dtype="u64 digest + u8",
                    roofline=roof, cpu_baseline=cpu, verified=ok, matches={"or": len(res[0]), "eq": len(res[1])})
+        if self.world == 1:
+            try:
+                out["resident_mutations"] = self.mutations()
+            except Exception as e:  # noqa: BLE001  (reported in the line, not lost)
+                out["resident_mutations"] = {"error": repr(e)}
         return out
 
     def close(self):

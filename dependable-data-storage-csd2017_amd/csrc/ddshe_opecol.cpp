@@ -39,6 +39,17 @@ struct dds_opecol {
   std::vector<uint8_t> hdead;                           // host mirror of d_dead (empty: none dead yet)
   size_t ndead = 0;
   std::map<size_t, std::pair<bn::Limbs, bool>> wide;  // kWide rows: exact value (magnitude, negative)
+  // [ulo, uhi]: bounds of every value ever stored in d_val, in unsigned order (v ^ 2^63); a superset
+  // of the holders' keys, kept on writes so Order starts its passes without a min/max pass over the
+  // column and its host round trip (only the pass count depends on how tight the bounds are)
+  uint64_t ulo = ~0ull, uhi = 0;
+  void widen(const int64_t* v, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+      const uint64_t u = (uint64_t)v[i] ^ 0x8000000000000000ull;
+      ulo = std::min(ulo, u);
+      uhi = std::max(uhi, u);
+    }
+  }
   size_t n_search = 0, n_hold = 0;
   size_t n_search_bad = 0;  // kSearch rows that Search's BigInteger parse rejects
   size_t n_hold_bad = 0;    // kHold rows that Order's asInstanceOf[String].toLong rejects
@@ -119,6 +130,7 @@ int append_rows(dds_opecol* col, const int64_t* vals, const uint8_t* flg, size_t
   HIP_TRY(hipMemcpyAsync(col->d_val + col->count, vals, count * 8, hipMemcpyHostToDevice, wl.st));
   HIP_TRY(hipMemcpyAsync(col->d_flg + col->count, flg, count, hipMemcpyHostToDevice, wl.st));
   HIP_TRY(hipStreamSynchronize(wl.st));
+  col->widen(vals, count);
   col->hflg.insert(col->hflg.end(), flg, flg + count);
   for (size_t i = 0; i < count; ++i) col->account(flg[i], +1);
   col->count += count;
@@ -203,6 +215,7 @@ int write_rows(dds_opecol* col, const uint64_t* ids, const int64_t* vals, const 
   HIP_TRY(launch_scatter_u64(w->ids.as<uint32_t>(), w->in.as<uint64_t>(), m, (uint64_t*)col->d_val, wl.st));
   HIP_TRY(launch_scatter_bytes(w->ids.as<uint32_t>(), w->in2.as<uint8_t>(), m, col->d_flg, wl.st));
   HIP_TRY(hipStreamSynchronize(wl.st));
+  col->widen(v.data(), m);
   for (auto& kv : last) {
     const size_t r = (size_t)kv.first, i = kv.second;
     if (!col->dead(r)) {
@@ -587,7 +600,9 @@ int dds_opecol_order(dds_opecol* col, int descending, uint32_t* out_idx, size_t*
     HIP_TRY(w->out.ensure(n * 4));
     // the sort's valid test is flag != 0, i.e. kHold (rows lacking the position have no other bit; a
     // removed set's device byte is 0, so it sorts with them)
-    HIP_TRY(launch_ope_order(col->d_val, col->d_flg, n, descending ? 1 : 0, w->tab.p, w->out.as<uint32_t>(), wl.st));
+    const uint64_t ub[2] = {col->ulo, col->uhi};
+    HIP_TRY(launch_ope_order(col->d_val, col->d_flg, n, descending ? 1 : 0, w->tab.p, w->out.as<uint32_t>(), wl.st,
+                             ub));
     const uint32_t* res = w->out.as<uint32_t>();
     size_t m = n;
     if (col->ndead) {  // drop removed sets from the permutation, order kept (filter(nonEmpty), :553, :586)

@@ -673,7 +673,7 @@ static bool msd_enabled(size_t n, int sb) {
 }
 
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
-                            uint32_t* out_ids, hipStream_t st) {
+                            uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds) {
   if (n == 0) return hipSuccess;
   const size_t nb = rs_blocks(n);
   uint64_t* ka = (uint64_t*)scratch;
@@ -691,15 +691,21 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   uint32_t* mmulti = mend + kMsdBuckets;
   uint32_t* mctl = mmulti + kMsdBuckets;  // right after the multi flags: one memset clears both
   uint32_t* mbig = mctl + 8;
-  if (((uintptr_t)col & 15) == 0 && ((uintptr_t)valid & 1) == 0)
-    hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
-  else
-    hipLaunchKernelGGL(k_rs_prep_rows, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
-  hipLaunchKernelGGL(k_rs_red, dim3(1), dim3(1024), 0, st, part, pb, red);
   uint64_t hred[2];
-  hipError_t e = hipMemcpyAsync(hred, red, sizeof(hred), hipMemcpyDeviceToHost, st);
-  if (e != hipSuccess) return e;
-  if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+  hipError_t e = hipSuccess;
+  if (ubounds) {  // bounds of the raw values from the caller: the keys' bounds follow (desc: complemented)
+    hred[0] = ubounds[0] <= ubounds[1] ? (desc ? ~ubounds[1] : ubounds[0]) : 1;
+    hred[1] = ubounds[0] <= ubounds[1] ? (desc ? ~ubounds[0] : ubounds[1]) : 0;
+  } else {
+    if (((uintptr_t)col & 15) == 0 && ((uintptr_t)valid & 1) == 0)
+      hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
+    else
+      hipLaunchKernelGGL(k_rs_prep_rows, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
+    hipLaunchKernelGGL(k_rs_red, dim3(1), dim3(1024), 0, st, part, pb, red);
+    e = hipMemcpyAsync(hred, red, sizeof(hred), hipMemcpyDeviceToHost, st);
+    if (e != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+  }
   // the bytes of max - min (at least one pass when rows may lack the position: its last pass buckets them)
   const uint64_t kmin = hred[0] <= hred[1] ? hred[0] : 0ull;
   const uint64_t span = hred[0] <= hred[1] ? hred[1] - hred[0] : 0ull;

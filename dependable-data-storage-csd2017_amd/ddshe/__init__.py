@@ -892,13 +892,23 @@ class StrTable:
         return dict(zip(STRTAB_STATS, (int(x) for x in out)))
 
     def append(self, rows):
-        chars, eo, ro = _flatten(rows)
+        self.append_flat(*_flatten(rows))
+
+    def append_flat(self, chars: bytes, elem_off, row_off):
+        """dds_strtab_append on a batch already in the table layout"""
+        eo = np.ascontiguousarray(elem_off, dtype=np.uint64)
+        ro = np.ascontiguousarray(row_off, dtype=np.uint64)
         _check(_lib.dds_strtab_append(self._h, C.c_char_p(chars or b"\0"), eo.ctypes.data_as(C.c_void_p), len(eo) - 1,
                                       ro.ctypes.data_as(C.c_void_p), len(ro) - 1), "dds_strtab_append")
 
     def write_rows(self, ids, rows):
+        self.write_rows_flat(ids, *_flatten(rows))
+
+    def write_rows_flat(self, ids, chars: bytes, elem_off, row_off):
+        """dds_strtab_write_rows on a batch already in the table layout (one batch row per id)"""
         ids = np.ascontiguousarray(ids, dtype=np.uint64)
-        chars, eo, ro = _flatten(rows)
+        eo = np.ascontiguousarray(elem_off, dtype=np.uint64)
+        ro = np.ascontiguousarray(row_off, dtype=np.uint64)
         if len(ro) - 1 != len(ids):
             raise ValueError("one row per id")
         _check(_lib.dds_strtab_write_rows(self._h, ids.ctypes.data_as(C.c_void_p), len(ids), C.c_char_p(chars or b"\0"),
