@@ -88,6 +88,11 @@ struct Worker {
   DevBuf pk, gather;         // multi-device fold: packed partial (shard side), gathered partials (combiner)
   DevBuf tree;               // reduction tree: node values + arrival flags
   hipEvent_t ev_peer = {};   // shard partial copied to the combining device
+  // a device counter kept at zero between uses (the Search bitmask's match count: the count kernel's
+  // tiles add into it, it is read, then re-zeroed on the stream after the read); ev_done marks the read
+  DevBuf ctr;
+  bool ctr_zero = false;
+  hipEvent_t ev_done = {};
   DevBuf crt[7];  // CRT encryption scratch (see encrypt_crt_device)
   hipEvent_t ev[4] = {};
   // decimal codec: double-buffered pinned chunks (chars, offsets), their device copies,
@@ -109,6 +114,7 @@ struct Worker {
     for (auto e : ev_dec)
       if (e) (void)hipEventDestroy(e);
     if (ev_peer) (void)hipEventDestroy(ev_peer);
+    if (ev_done) (void)hipEventDestroy(ev_done);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -350,7 +356,8 @@ struct WorkerLease {
         if (hipEventCreate(&e) != hipSuccess) return fail(DDS_E_HIP, "hipEventCreate");
       for (auto& e : nw->ev_dec)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(DDS_E_HIP, "hipEventCreate");
-      if (hipEventCreateWithFlags(&nw->ev_peer, hipEventDisableTiming) != hipSuccess)
+      if (hipEventCreateWithFlags(&nw->ev_peer, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&nw->ev_done, hipEventDisableTiming) != hipSuccess)
         return fail(DDS_E_HIP, "hipEventCreate");
       w = nw.get();
       ctx->workers.push_back(std::move(nw));

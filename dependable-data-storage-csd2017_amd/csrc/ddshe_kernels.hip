@@ -614,7 +614,7 @@ __device__ __forceinline__ uint32_t ope_thread_mask(const int64_t* __restrict__ 
 // tile with one block-wide scan of 256 popcounts instead of 32 ballots per thread. Also writes the
 // tile's match count.
 __device__ __forceinline__ void ope_store_mask(uint32_t m, uint32_t* __restrict__ masks, uint32_t* __restrict__ counts,
-                                               size_t tile) {
+                                               size_t tile, unsigned long long* __restrict__ total = nullptr) {
   __shared__ uint8_t nib[kOpeGroups * kOpeBlock];
   __shared__ uint32_t wsum[kOpeBlock / 64];
   const int tid = threadIdx.x;
@@ -633,6 +633,7 @@ __device__ __forceinline__ void ope_store_mask(uint32_t m, uint32_t* __restrict_
     uint32_t c = 0;
     for (int w = 0; w < kOpeBlock / 64; ++w) c += wsum[w];
     counts[tile] = c;
+    if (total && c) atomicAdd(total, (unsigned long long)c);  // the Search bitmask's match count
   }
 }
 
@@ -643,14 +644,17 @@ __device__ __forceinline__ void ope_store_mask(uint32_t m, uint32_t* __restrict_
 //   k_ope_scatter: each block sums the counts of the tiles before it (<= a few thousand u32 from
 //                  L2), reloads its masks, ranks its matches in row order (k*256 + tid) and
 //                  writes the row ids; the last block writes the total.
+// total (nullable, zeroed by the caller): every tile also adds its count to it (one atomic per tile),
+// so the Search bitmask route has its match count without a reduction launch
 template <bool HasValid>
 __global__ void __launch_bounds__(kOpeBlock) k_ope_count(const int64_t* __restrict__ col,
                                                          const uint8_t* __restrict__ valid, size_t n, int64_t bound,
                                                          int op, uint32_t vmask, uint32_t vbad,
-                                                         uint32_t* __restrict__ masks, uint32_t* __restrict__ counts) {
+                                                         uint32_t* __restrict__ masks, uint32_t* __restrict__ counts,
+                                                         unsigned long long* __restrict__ total) {
   const bool vec = ((uintptr_t)col % 16 == 0) && (!HasValid || (uintptr_t)valid % 4 == 0);
   const uint32_t m = ope_thread_mask<HasValid>(col, valid, n, bound, op, blockIdx.x, vec, vmask, vbad);
-  ope_store_mask(m, masks, counts, blockIdx.x);
+  ope_store_mask(m, masks, counts, blockIdx.x, total);
 }
 
 // SearchEq/NEq front end (ddshe_strscan.hip's position index): same tile layout and masks as
@@ -1359,17 +1363,18 @@ void ope_code(int64_t bound, int op, int64_t* t, int* code) {
   }
 }
 void ope_count(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, uint32_t* masks,
-               uint32_t* counts, hipStream_t st, uint32_t vmask, uint32_t vbad) {
+               uint32_t* counts, hipStream_t st, uint32_t vmask, uint32_t vbad,
+               unsigned long long* total = nullptr) {
   const size_t nb = ope_blocks(n);
   int64_t t;
   int code;
   ope_code(bound, op, &t, &code);
   if (valid)
     hipLaunchKernelGGL(k_ope_count<true>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, t, code, vmask,
-                       vbad, masks, counts);
+                       vbad, masks, counts, total);
   else
     hipLaunchKernelGGL(k_ope_count<false>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, t, code, vmask,
-                       vbad, masks, counts);
+                       vbad, masks, counts, total);
 }
 }  // namespace
 
@@ -1387,10 +1392,14 @@ hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n,
 uint32_t* ope_mask_words(void* scratch, size_t n) { return (uint32_t*)scratch + ope_blocks(n); }
 
 hipError_t launch_ope_mask(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
-                           uint64_t* total, hipStream_t st, uint32_t vmask, uint32_t vbad) {
+                           uint64_t* total, hipStream_t st, uint32_t vmask, uint32_t vbad, bool total_zeroed) {
   const size_t nb = ope_blocks(n);
   if (nb == 0) return hipSuccess;
   uint32_t* counts = (uint32_t*)scratch;
+  if (total_zeroed) {  // the tiles add their counts into *total themselves
+    ope_count(col, valid, n, bound, op, counts + nb, counts, st, vmask, vbad, (unsigned long long*)total);
+    return hipGetLastError();
+  }
   ope_count(col, valid, n, bound, op, counts + nb, counts, st, vmask, vbad);
   hipLaunchKernelGGL(k_count_total, dim3(1), dim3(1024), 0, st, counts, nb, total);
   return hipGetLastError();

@@ -117,8 +117,10 @@ hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n,
                              uint32_t vbad = 0u);
 // Search as a row bitmask (no id scatter): after it, ope_mask_words(scratch, n)[w] bit b = row 32w + b
 // matches (words in row order; bits past n are 0) and *total (device) the number of matches
+// total_zeroed: *total is 0 on entry and the count kernel's tiles add into it (no reduction launch)
 hipError_t launch_ope_mask(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
-                           uint64_t* total, hipStream_t st, uint32_t vmask = 0xFFu, uint32_t vbad = 0u);
+                           uint64_t* total, hipStream_t st, uint32_t vmask = 0xFFu, uint32_t vbad = 0u,
+                           bool total_zeroed = false);
 uint32_t* ope_mask_words(void* scratch, size_t n);
 // rows i with (bytes[i] & vmask) != 0 -> ascending ids in out, count in *total (device); scratch as above
 hipError_t launch_byte_compact(const uint8_t* bytes, size_t n, uint32_t vmask, void* scratch, uint64_t* total,

@@ -538,31 +538,35 @@ int dds_opecol_search_mask(dds_opecol* col, const char* bound_dec, int op, uint6
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
     // match words in row order (u32 word k = rows [32k, 32k + 32), little-endian: two of them are the
-    // u64 word of the caller's layout) + the match count, back in one copy
+    // u64 word of the caller's layout). The match count: the count kernel's tiles add into the worker's
+    // zeroed counter (no reduction launch), re-zeroed on the stream after it is read.
     const size_t bytes = words * 8;
     HIP_TRY(w->misc.ensure(ope_scratch_bytes(n) + 64));
-    HIP_TRY(w->hbig.ensure(bytes + 8));
+    HIP_TRY(w->ctr.ensure(64));
     uint32_t* mw = ope_mask_words(w->misc.p, n);
-    uint64_t* dtotal = (uint64_t*)(((uintptr_t)w->misc.p + ope_scratch_bytes(n) + 7) & ~(uintptr_t)7);  // past the masks
+    uint64_t* dtotal = w->ctr.as<uint64_t>();
+    if (!w->ctr_zero) HIP_TRY(hipMemsetAsync(dtotal, 0, 8, wl.st));
+    w->ctr_zero = false;
+    uint32_t* stg = nullptr;
+    HIP_TRY(stage_ptr(w, &stg));
     record_time(ctx, w, wl.st, true, 2);
-    HIP_TRY(launch_ope_mask(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, dtotal, wl.st, kSearch, kWide));
+    HIP_TRY(launch_ope_mask(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, dtotal, wl.st, kSearch, kWide, true));
     record_time(ctx, w, wl.st, false, 2);
-    uint8_t* h = (uint8_t*)w->hbig.p;
+    const bool direct = host_registered(ctx, mask, bytes);  // page-locked caller buffer: one DMA into it
+    uint8_t* h = nullptr;
+    if (!direct) {
+      HIP_TRY(w->hbig.ensure(bytes));
+      h = (uint8_t*)w->hbig.p;
+    }
+    HIP_TRY(hipMemcpyAsync(stg, dtotal, 8, hipMemcpyDeviceToHost, wl.st));
+    HIP_TRY(hipMemcpyAsync(direct ? (void*)mask : (void*)h, mw, bytes, hipMemcpyDeviceToHost, wl.st));
+    HIP_TRY(hipEventRecord(w->ev_done, wl.st));
+    HIP_TRY(hipMemsetAsync(dtotal, 0, 8, wl.st));  // off the reply's path: the caller waits for ev_done only
+    w->ctr_zero = true;
+    HIP_TRY(hipEventSynchronize(w->ev_done));
     uint64_t total = 0;
-    if (host_registered(ctx, mask, bytes)) {
-      // the caller's buffer is page-locked (dds_host_register): one DMA straight into it, the count
-      // through the worker's pinned stage
-      uint32_t* stg = nullptr;
-      HIP_TRY(stage_ptr(w, &stg));
-      HIP_TRY(hipMemcpyAsync(mask, mw, bytes, hipMemcpyDeviceToHost, wl.st));
-      HIP_TRY(hipMemcpyAsync(stg, dtotal, 8, hipMemcpyDeviceToHost, wl.st));
-      HIP_TRY(hipStreamSynchronize(wl.st));
-      memcpy(&total, stg, 8);
-    } else {
-      HIP_TRY(hipMemcpyAsync(h, mw, bytes, hipMemcpyDeviceToHost, wl.st));
-      HIP_TRY(hipMemcpyAsync(h + bytes, dtotal, 8, hipMemcpyDeviceToHost, wl.st));
-      HIP_TRY(hipStreamSynchronize(wl.st));
-      memcpy(&total, h + bytes, 8);
+    memcpy(&total, stg, 8);
+    if (!direct) {
       if (bytes >= ((size_t)1 << 20)) {
         CopyPool::get().parallel_for(bytes, 4096, [&](size_t a, size_t e) { memcpy((char*)mask + a, h + a, e - a); });
       } else {
