@@ -209,25 +209,8 @@ int put_rows(dds_strtab* t, const uint32_t* ids, size_t nb, const char* chars, c
   const size_t nc = eoff[ne];
   const size_t r_first = t->nrows;
   if (!ids && (rc = grow_rows(t, t->nrows + nb, st))) return rc;
-  if (ids) {  // the rows' current versions become garbage
-    std::vector<uint64_t> ob(nb);
-    std::vector<uint32_t> ol(nb);
-    for (size_t i = 0; i < nb; ++i) {
-      const uint32_t r = ids[i];
-      ob[i] = t->h_beg[r];
-      ol[i] = t->h_len[r];
-      t->vel -= t->h_len[r];
-      t->vch -= t->h_bytes[r];
-      t->h_len[r] = 0;
-      t->h_bytes[r] = 0;
-    }
-    HIP_TRY(w->misc.ensure(nb * 12));
-    HIP_TRY(hipMemcpyAsync(w->misc.p, ob.data(), nb * 8, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(w->misc.as<uint8_t>() + nb * 8, ol.data(), nb * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_str_kill(w->misc.as<uint64_t>(), reinterpret_cast<const uint32_t*>(w->misc.as<uint8_t>() + nb * 8),
-                            nb, t->elem_row, st));
-    HIP_TRY(hipStreamSynchronize(st));  // staged from host vectors; also before a compaction reads the heap
-  }
+  // room for the new elements first (a compaction that fails leaves the table as it was; it still
+  // copies the versions this write replaces, so it is sized for them too)
   if (t->nheap + ne > t->ecap || t->nchars + nc > t->ccap) {
     // a fresh table is sized to its first batch (+1/16); later growth leaves half the live size free
     const bool first = t->nheap == 0 && t->ecap == 0;
@@ -235,6 +218,25 @@ int put_rows(dds_strtab* t, const uint32_t* ids, size_t nb, const char* chars, c
     const size_t ecap = std::max(kStrMinCap, first ? le + le / 16 : le + le / 2);
     const size_t ccap = std::max(kStrMinCap, first ? lc + lc / 16 : lc + lc / 2);
     if ((rc = compact(t, ecap, ccap, w, st))) return rc;
+  }
+  if (ids) {  // the rows' current versions become garbage
+    std::vector<uint64_t> ob(nb);
+    std::vector<uint32_t> ol(nb);
+    for (size_t i = 0; i < nb; ++i) {
+      ob[i] = t->h_beg[ids[i]];
+      ol[i] = t->h_len[ids[i]];
+    }
+    HIP_TRY(w->misc.ensure(nb * 12));
+    HIP_TRY(hipMemcpyAsync(w->misc.p, ob.data(), nb * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(w->misc.as<uint8_t>() + nb * 8, ol.data(), nb * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_str_kill(w->misc.as<uint64_t>(), reinterpret_cast<const uint32_t*>(w->misc.as<uint8_t>() + nb * 8),
+                            nb, t->elem_row, st));
+    HIP_TRY(hipStreamSynchronize(st));  // staged from host vectors (misc is reused below)
+    for (size_t i = 0; i < nb; ++i) {
+      const uint32_t r = ids[i];
+      t->vel -= t->h_len[r];
+      t->vch -= t->h_bytes[r];
+    }
   }
   // bytes, rebased element offsets, fingerprints and owners of the new elements
   const uint64_t e0 = t->nheap, c0 = t->nchars;
