@@ -331,7 +331,7 @@ class SumWorkload(_Workload):
         if traffic is not None:
             traffic *= self.mine / 1e7
         roof.update(traffic=traffic, traffic_unit=f"HBM bytes per launch (PMC, profiles/{PMC_FILE})")
-        for vname in ("r03_pmc_valu_fold.json", "r01_pmc_valu_fold.json"):
+        for vname in ("r04_pmc_valu_fold.json", "r03_pmc_valu_fold.json", "r01_pmc_valu_fold.json"):
             vf = os.path.join(ROOT, "profiles", vname)
             if os.path.exists(vf):  # rocprofv3 VALU counters of the same kernel (north star: VALU-roofline fraction)
                 dv = json.load(open(vf))["derived"]
@@ -345,7 +345,7 @@ class SumWorkload(_Workload):
         e2e = None
         if self.world == 1 and not a.no_e2e:
             e2e = self.end_to_end(res)
-        split = self.strong_split_line(res) if self.world == 1 else None
+        split = self.strong_split_line(res) if self.world == 1 and not a.no_extras else None
         out = self.common("Paillier homomorphic adds/sec (2048-bit key, mod n^2)",
                           (self.total - 1) * a.steps / elapsed, "HomoAdd/s", elapsed,
                           "paillier_sumall_fold_10M_2048bit",

@@ -10,4 +10,4 @@ for c in SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32; do
 done
 echo "extra counters:$EXTRA"
 exec tools/gpu_steps.sh \
-  "200 pmc_valu rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY$EXTRA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/prof/pmc_valu -o run -- python3 bench.py --no-cpu-baseline --no-e2e --steps 1 --warmup 0 --verify 0"
+  "200 pmc_valu rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY$EXTRA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/prof/pmc_valu -o run -- python3 bench.py --no-cpu-baseline --no-e2e --no-extras --steps 1 --warmup 0 --verify 0"
