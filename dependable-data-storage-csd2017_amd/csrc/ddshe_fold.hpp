@@ -118,12 +118,22 @@ __global__ void __launch_bounds__(256, 2) k_fold(const uint32_t* __restrict__ X,
     g.load_col(a, X, xstride, rowat(grp));
   if (grp + ngroups < count) {
     uint32_t pre[2][M::kPF];  // first limb blocks of the next row, requested one row ahead
-    uint32_t row = rowat(grp + ngroups);
-    M::load_blocks2(pre, X, xstride, row);
-    for (size_t pos = grp + ngroups; pos < count; pos += ngroups) {
-      const uint32_t nxt = pos + ngroups < count ? rowat(pos + ngroups) : row;  // last row: a harmless re-read
-      M::template mul_col_chain<Narrow>(a, n, X, xstride, row, nxt, pre, n0, g.top, g.bottom, sin);
-      row = nxt;
+    if constexpr (!Idx) {
+      // rows grp, grp + G, ...: the loop of round 1 (the row is the loop variable)
+      M::load_blocks2(pre, X, xstride, (uint32_t)(grp + ngroups));
+      for (size_t row = grp + ngroups; row < count; row += ngroups) {
+        const size_t nxt = row + ngroups < count ? row + ngroups : row;  // last row: a harmless re-read
+        M::template mul_col_chain<Narrow>(a, n, X, xstride, (uint32_t)row, (uint32_t)nxt, pre, n0, g.top, g.bottom,
+                                          sin);
+      }
+    } else {
+      uint32_t row = rowat(grp + ngroups);
+      M::load_blocks2(pre, X, xstride, row);
+      for (size_t pos = grp + ngroups; pos < count; pos += ngroups) {
+        const uint32_t nxt = pos + ngroups < count ? rowat(pos + ngroups) : row;  // last row: a harmless re-read
+        M::template mul_col_chain<Narrow>(a, n, X, xstride, row, nxt, pre, n0, g.top, g.bottom, sin);
+        row = nxt;
+      }
     }
   }
   M::normalize(a, g.bottom);
