@@ -393,3 +393,19 @@ def test_x509_jdk_key_length_check():
                 x509.rsa_modulus(h)
             with pytest.raises(homo.ServerError):
                 homo.rsa_modulus_from_pubkey_hex(h)
+
+
+def test_equality_scan_semantics():
+    """HomoDet.compare on AnyJsonFormat texts (DDSJsonProtocol.scala:22-28) and SearchEntry's needle:
+    item.toString of the DDSItem case class (DDSRestServer.scala:845), unlike SearchEntryOR/AND."""
+    from oracle import homo
+    assert homo.homo_det_compare(True, "true") and homo.homo_det_compare(None, "None")
+    assert not homo.homo_det_compare(True, "True")
+    assert homo.entry_needle("x") == "DDSItem(x)" and homo.entry_needle(7) == "DDSItem(7)"
+    rows = [("a", ["x", "y"]), ("b", ["DDSItem(x)"]), ("c", None), ("d", [True, "z"])]
+    assert homo.search_entry("SearchEntry", rows, ["x"]) == {"b"}
+    assert homo.search_entry("SearchEntryOR", rows, ["x", "q", "true"]) == {"a", "d"}
+    assert homo.search_entry("SearchEntryAND", rows, ["x", "y", "q"]) == set()
+    assert homo.search_eq("SearchEq", rows, 0, "x") == {"a"}  # strict guard: length - 1 > position
+    assert homo.search_eq("SearchNEq", rows, 0, "x") == {"d"}
+    assert homo.is_element(["x", True], "true") and not homo.is_element(["x"], "y")
