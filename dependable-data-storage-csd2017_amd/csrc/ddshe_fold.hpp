@@ -295,12 +295,20 @@ __global__ void __launch_bounds__(256, 2) k_fold1(const uint32_t* __restrict__ X
   for (int l = 0; l < S; ++l) a[l] = X[(size_t)l * xstride + r0];
   if (grp + ngroups < count) {
     uint32_t pre[2][M::PF];
-    uint32_t row = rowat(grp + ngroups);
-    M::load_blocks2(pre, X, xstride, row);
-    for (size_t pos = grp + ngroups; pos < count; pos += ngroups) {
-      const uint32_t nxt = pos + ngroups < count ? rowat(pos + ngroups) : row;
-      M::mul_row_chain(a, n, X, xstride, row, nxt, pre, n0);
-      row = nxt;
+    if constexpr (!Idx) {  // the row is the loop variable (k_fold: the row-id loop form cost 4.5 % there)
+      M::load_blocks2(pre, X, xstride, (uint32_t)(grp + ngroups));
+      for (size_t row = grp + ngroups; row < count; row += ngroups) {
+        const size_t nxt = row + ngroups < count ? row + ngroups : row;
+        M::mul_row_chain(a, n, X, xstride, (uint32_t)row, (uint32_t)nxt, pre, n0);
+      }
+    } else {
+      uint32_t row = rowat(grp + ngroups);
+      M::load_blocks2(pre, X, xstride, row);
+      for (size_t pos = grp + ngroups; pos < count; pos += ngroups) {
+        const uint32_t nxt = pos + ngroups < count ? rowat(pos + ngroups) : row;
+        M::mul_row_chain(a, n, X, xstride, row, nxt, pre, n0);
+        row = nxt;
+      }
     }
   }
 #pragma unroll

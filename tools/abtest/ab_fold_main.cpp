@@ -2,6 +2,8 @@
 // (tool, not product). The modulus is a QP modulus N~ = N·n0 (N~ = -1 mod 2^28) of an odd ~4095-bit N,
 // as the engine uses at the committed key's shape, so every build computes the same residues: outputs
 // must agree bit for bit. Usage: ab_fold [rows=10000000] [rounds=7] [groups=0: 256 CUs x 2 x 64]
+// Built with -DAB_FOLD1: the k_fold1<74, 28, false> builds instead (a ~2048-bit odd N, plain CIOS quotient,
+// one bignum per lane: groups default 256 CUs x 2 x 256).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -23,7 +25,13 @@ DECL(0) DECL(1) DECL(2) DECL(3)
   } while (0)
 
 int main(int argc, char** argv) {
+#ifdef AB_FOLD1
+  const int S = 74, W = 28;
+  const bool qp = false;
+#else
   const int S = 148, W = 28;
+  const bool qp = true;
+#endif
   const uint32_t mask = (1u << W) - 1;
   const size_t count = argc > 1 ? atoll(argv[1]) : 10000000;
   const int rounds = argc > 2 ? atoi(argv[2]) : 7;
@@ -32,7 +40,7 @@ int main(int argc, char** argv) {
   launch_t fns[4] = {k_ab0_launch, k_ab1_launch, k_ab2_launch, k_ab3_launch};
   hipDeviceProp_t prop;
   CK(hipGetDeviceProperties(&prop, 0));
-  if (!G) G = (size_t)prop.multiProcessorCount * 2 * 64;  // 2 blocks of 256 threads per CU, 4 lanes per bignum
+  if (!G) G = (size_t)prop.multiProcessorCount * 2 * (qp ? 64 : 256);  // 2 blocks of 256 threads per CU
   if (G > count) G = count;
   const size_t stride = (count + 63) / 64 * 64;
   // N: odd, ~4095 bits (top limb 2^10 | 5); N~ = N * n0 with n0 = -N^-1 mod 2^W (N~ = -1 mod 2^W, < 2^4123)
@@ -47,11 +55,11 @@ int main(int argc, char** argv) {
   const uint32_t n0 = (0u - inv) & mask;
   uint64_t carry = 0;
   for (int l = 0; l < S; ++l) {
-    const uint64_t v = (uint64_t)N[l] * n0 + carry;
-    C[l] = (uint32_t)v & mask;  // kConstN block = N~
-    carry = v >> W;
+    const uint64_t v = qp ? (uint64_t)N[l] * n0 + carry : N[l];
+    C[l] = (uint32_t)v & mask;  // kConstN block = N~ (QP) or N
+    carry = qp ? v >> W : 0;
   }
-  if (carry || C[0] != mask) {
+  if (carry || (qp && C[0] != mask)) {
     fprintf(stderr, "bad QP modulus\n");
     return 1;
   }
