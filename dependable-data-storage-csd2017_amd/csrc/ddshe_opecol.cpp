@@ -605,6 +605,7 @@ int dds_opecol_order(dds_opecol* col, int descending, uint32_t* out_idx, size_t*
     // the sort's valid test is flag != 0, i.e. kHold (rows lacking the position have no other bit; a
     // removed set's device byte is 0, so it sorts with them)
     const uint64_t ub[2] = {col->ulo, col->uhi};
+    record_time(col->ctx, w, wl.st, true, 2);
     HIP_TRY(launch_ope_order(col->d_val, col->d_flg, n, descending ? 1 : 0, w->tab.p, w->out.as<uint32_t>(), wl.st,
                              ub));
     const uint32_t* res = w->out.as<uint32_t>();
@@ -622,12 +623,15 @@ int dds_opecol_order(dds_opecol* col, int descending, uint32_t* out_idx, size_t*
       HIP_TRY(launch_gather_u32(res, w->ids.as<uint32_t>(), m, w->p1.as<uint32_t>(), wl.st));
       res = w->p1.as<uint32_t>();
     }
+    record_time(col->ctx, w, wl.st, false, 2);
+    const bool direct = m && host_registered(col->ctx, out_idx, m * 4);  // page-locked reply buffer: one DMA
     if (m) {
-      HIP_TRY(w->hbig.ensure(m * 4));
-      HIP_TRY(hipMemcpyAsync(w->hbig.p, res, m * 4, hipMemcpyDeviceToHost, wl.st));
+      if (!direct) HIP_TRY(w->hbig.ensure(m * 4));
+      HIP_TRY(hipMemcpyAsync(direct ? (void*)out_idx : w->hbig.p, res, m * 4, hipMemcpyDeviceToHost, wl.st));
     }
     HIP_TRY(hipStreamSynchronize(wl.st));
-    if (m) CopyPool::get().copy(out_idx, w->hbig.p, m * 4);
+    add_filter_time(col->ctx, w);  // device time of the ordering (HIP events), for dds_ctx_get_timing
+    if (m && !direct) CopyPool::get().copy(out_idx, w->hbig.p, m * 4);
     if (out_n) *out_n = m;
     return DDS_OK;
   } catch (const std::bad_alloc&) {

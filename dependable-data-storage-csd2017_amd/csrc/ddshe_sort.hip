@@ -398,8 +398,7 @@ constexpr uint32_t kMsdBuckets = 1u << kMsdBits;
 constexpr uint32_t kMsdWaveMax = 512;
 constexpr uint32_t kMsdBlockMax = 8192;
 constexpr int kMsdBigBlocks = 512;  // grid of the block path (grid-stride over the big buckets)
-enum { kMsdCtlBig = 0, kMsdCtlOverflow = 1, kMsdCtlList = 2 };
-constexpr int kMsdLocalBlocks = 1024;  // k_msd_local grid: 4096 waves over the list of multi-key buckets
+enum { kMsdCtlBig = 0, kMsdCtlOverflow = 1 };
 
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
   const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
@@ -468,15 +467,13 @@ __device__ __forceinline__ void msd_holders(const uint32_t* __restrict__ dtot, s
 }
 
 // first[b] / end[b]: first row / one past the last row of non-empty bucket b (read only where multi[b]);
-// multi[b] = 1 when bucket b holds two distinct keys (preset to 0), and such a bucket is appended once
-// to list[] (count in ctl[kMsdCtlList]), so k_msd_local visits only those buckets. Neighbouring keys
-// come from the adjacent lanes; 4 rows per thread (loads in flight together).
+// multi[b] = 1 when bucket b holds two distinct keys (preset to 0). Neighbouring keys come from the
+// adjacent lanes; 4 rows per thread (loads in flight together); block 0 also clears the control words.
 constexpr int kMsdBoundsRows = 4;
 __global__ void __launch_bounds__(256) k_msd_bounds(const uint64_t* __restrict__ keys, size_t n, int s1,
                                                     const uint32_t* __restrict__ dtot, int desc, bool has_valid,
                                                     uint32_t* __restrict__ first, uint32_t* __restrict__ end,
-                                                    uint32_t* __restrict__ multi, uint32_t* __restrict__ list,
-                                                    uint32_t* __restrict__ ctl) {
+                                                    uint32_t* __restrict__ multi) {
   size_t h0, h1;
   msd_holders(dtot, n, desc, has_valid, &h0, &h1);
   const int lane = threadIdx.x & 63;
@@ -495,7 +492,7 @@ __global__ void __launch_bounds__(256) k_msd_bounds(const uint64_t* __restrict__
     const uint32_t b = msd_bucket_of(k[r], s1);
     const bool head = i == h0 || msd_bucket_of(kp, s1) != b;
     if (head) first[b] = (uint32_t)i;
-    else if (kp != k[r] && atomicCAS(&multi[b], 0u, 1u) == 0u) list[atomicAdd(&ctl[kMsdCtlList], 1u)] = b;
+    else if (kp != k[r]) multi[b] = 1u;
     if (i == h1 - 1 || msd_bucket_of(kn, s1) != b) end[b] = (uint32_t)(i + 1);
   }
 }
@@ -576,19 +573,16 @@ __device__ __forceinline__ void msd_wave_sort(const uint64_t* __restrict__ keys,
   }
 }
 
-// One wave per multi-key bucket of list[] (the others are final after the last pass). The grid is
-// fixed (kMsdLocalBlocks): a wave takes list entries q, q + 4096, ...; with the OPE columns' few
-// multi-key buckets each wave has at most one (a grid of one wave per bucket index, 65,536 waves that
-// mostly exit at once, cost ~40 us of block dispatch).
 __global__ void __launch_bounds__(256) k_msd_local(const uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
                                                    uint32_t* __restrict__ ids, const uint32_t* __restrict__ first,
                                                    const uint32_t* __restrict__ end,
-                                                   const uint32_t* __restrict__ list, int s1,
+                                                   const uint32_t* __restrict__ multi, int s1,
                                                    uint32_t* __restrict__ ctl, uint32_t* __restrict__ big) {
   const int lane = threadIdx.x & 63;
-  const uint32_t nlist = ctl[kMsdCtlList], nwaves = gridDim.x * 4;
-  for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < nlist; q += nwaves) {
-    const uint32_t b = list[q];
+  {  // one wave per bucket (a grid-stride loop over the buckets measured 34 -> 56 us: the multi-key
+     // buckets' rounds serialise within a wave)
+    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (!multi[b]) return;  // empty, or one key: the last pass already put its rows in their place
     const uint32_t lo = first[b], m = end[b] - lo;
     // this bucket's grouped ids to the side buffer (free after the last pass), read from there below
     for (uint32_t p0 = 0; p0 < m; p0 += 512) {  // 8 loads in flight per lane, then their stores
@@ -605,10 +599,10 @@ __global__ void __launch_bounds__(256) k_msd_local(const uint64_t* __restrict__ 
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's copies land before its lanes read them
-    if (msd_wave_partition(keys, src, ids, lo, m, lane, m <= kMsdWaveMax ? 2 : 16)) continue;
+    if (msd_wave_partition(keys, src, ids, lo, m, lane, m <= kMsdWaveMax ? 2 : 16)) return;
     if (m > kMsdWaveMax) {
       if (lane == 0) big[atomicAdd(&ctl[kMsdCtlBig], 1u)] = b;
-      continue;
+      return;
     }
     const uint64_t rmask = (1ull << s1) - 1ull;
     if (m <= 64) msd_wave_sort<1, 6>(keys, src, ids, lo, m, rmask, lane);
@@ -666,7 +660,7 @@ size_t rs_scratch_bytes(size_t n) {
   // MSD bucket starts + control words + big-bucket list
   return 2 * n * 8 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 1024 +
          (size_t)kRsDigits * ((rs_blocks(n) + kScanTiles - 1) / kScanTiles) * 4 + 256 +
-         16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows)) + 768 + (5 * (size_t)kMsdBuckets + 8) * 4;
+         16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows)) + 768 + (4 * (size_t)kMsdBuckets + 8) * 4;
 }
 
 // the MSD path pays off from 4 LSD passes on (a span of > 24 bits) and enough rows to fill the buckets
@@ -697,7 +691,6 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   uint32_t* mmulti = mend + kMsdBuckets;
   uint32_t* mctl = mmulti + kMsdBuckets;  // right after the multi flags: one memset clears both
   uint32_t* mbig = mctl + 8;
-  uint32_t* mlist = mbig + kMsdBuckets;
   uint64_t hred[2];
   hipError_t e = hipSuccess;
   if (ubounds) {  // bounds of the raw values from the caller: the keys' bounds follow (desc: complemented)
@@ -747,8 +740,8 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     if ((e = hipMemsetAsync(mmulti, 0, (kMsdBuckets + 8) * 4, st)) != hipSuccess) return e;  // flags + control
     const size_t nbd = (n + 256 * kMsdBoundsRows - 1) / (256 * kMsdBoundsRows);  // over <= n holder rows
     hipLaunchKernelGGL(k_msd_bounds, dim3((unsigned)nbd), dim3(256), 0, st, sorted, n, s1, dtot, desc, valid != nullptr,
-                       mfirst, mend, mmulti, mlist, mctl);
-    hipLaunchKernelGGL(k_msd_local, dim3(kMsdLocalBlocks), dim3(256), 0, st, sorted, ib, out_ids, mfirst, mend, mlist,
+                       mfirst, mend, mmulti);
+    hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / 4), dim3(256), 0, st, sorted, ib, out_ids, mfirst, mend, mmulti,
                        s1, mctl, mbig);
     hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, sorted, ib, out_ids, mfirst, mend, s1, mctl,
                        mbig);

@@ -706,12 +706,15 @@ class OpeColumn:
                "dds_opecol_search_mask")
         return words, got.value
 
-    def order(self, descending: bool) -> np.ndarray:
-        out = np.empty(max(1, len(self)), dtype=np.uint32)
+    def order(self, descending: bool, out: np.ndarray | None = None) -> np.ndarray:
+        """dds_opecol_order: the live rows' permutation. out: a reusable uint32 buffer of at least
+        len(self) entries (Engine.host_register it once to have the ids DMA'd straight in); the result
+        is then a view of it."""
+        buf = np.empty(max(1, len(self)), dtype=np.uint32) if out is None else out
         got = C.c_size_t()
-        _check(_lib.dds_opecol_order(self._h, int(descending), out.ctypes.data_as(C.c_void_p), C.byref(got)),
+        _check(_lib.dds_opecol_order(self._h, int(descending), buf.ctypes.data_as(C.c_void_p), C.byref(got)),
                "dds_opecol_order")
-        return out[: got.value].copy()
+        return buf[: got.value] if out is not None else buf[: got.value].copy()
 
     def write_rows(self, row_ids, values, cls=None):
         ids = _ids(row_ids)
