@@ -667,7 +667,7 @@ def run_extra_configs(main_wl):
 
 
 # tools/profile_all.sh passes, summarised by tools/pmc_summary.py (newest round first)
-PMC_FILE = next((f for f in ("r03_pmc.json", "r02_pmc_filter_order.json")
+PMC_FILE = next((f for f in ("r04_pmc.json", "r03_pmc.json", "r02_pmc_filter_order.json")
                  if os.path.exists(os.path.join(ROOT, "profiles", f))), "r02_pmc_filter_order.json")
 
 
@@ -691,6 +691,19 @@ def pmc_traffic(workload, kernels, per_step=False, largest=False):
         else:
             tot += d["hbm_bytes_per_dispatch"] * (d["dispatches"] if per_step else 1)
     return tot
+
+
+def order_pmc_traffic():
+    """HBM bytes of one OrderLS call on raw arrays from the PMC pass of the order bench: that pass runs
+    one raw call (k_rs_prep + k_rs_red once) and the resident line's calls (no prep), so the other
+    kernels' bytes are divided by the calls (one k_msd_bounds dispatch per call)."""
+    once = pmc_traffic("order", ("k_rs_prep", "k_rs_red"), per_step=True)
+    rest = pmc_traffic("order", ("k_rs_hist", "k_rs_scan_tiles", "k_rs_scan_chunks", "k_rs_scatter", "k_msd_bounds",
+                                 "k_msd_local", "k_msd_big"), per_step=True)
+    calls = (pmc_entry(["order"], "k_msd_bounds") or (None, 0))[1]
+    if once is None or rest is None or not calls:
+        return None
+    return once + rest / calls
 
 
 def pmc_entry(workloads, kernel):
@@ -994,8 +1007,7 @@ class OrderWorkload(_Workload):
                 "algorithmic_bytes": alg,
                 # prep 9 + 2 passes x (hist 8 + scatter 24) + bounds 8 (+ the multi-key buckets' rounds)
                 "issued_bytes_est": self.mine * (9 + 2 * 32 + 8),
-                "traffic": pmc_traffic("order", ("k_rs_prep", "k_rs_red", "k_rs_hist", "k_rs_scan_tiles", "k_rs_scan_chunks", "k_rs_scatter",
-                                                 "k_msd_bounds", "k_msd_local", "k_msd_big"), per_step=True),
+                "traffic": order_pmc_traffic(),
                 "traffic_unit": "HBM bytes per OrderLS call (PMC, profiles/" + PMC_FILE + ")"}
         roof["issued_GBps"] = roof["issued_bytes_est"] / step_s / 1e9  # what the MSD-split design moves
         roof["issued_frac"] = roof["issued_GBps"] / 8000.0

@@ -397,7 +397,8 @@ constexpr int kMsdBits = 16;
 constexpr uint32_t kMsdBuckets = 1u << kMsdBits;
 constexpr uint32_t kMsdWaveMax = 512;
 constexpr uint32_t kMsdBlockMax = 8192;
-constexpr int kMsdBigBlocks = 512;  // grid of the block path (grid-stride over the big buckets)
+constexpr int kMsdBigBlocks = 256;  // grid of the block path (grid-stride over the big buckets; one per CU:
+                                     // a launch that finds no big bucket costs its dispatch, 13 us at 512)
 enum { kMsdCtlBig = 0, kMsdCtlOverflow = 1 };
 
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
