@@ -275,13 +275,22 @@ def test_search_mask_registered_buffer(eng):
     try:
         with pytest.raises(DDSError):
             eng.host_register(buf[10:])
-        for op, f in (("gt", np.greater), ("le", np.less_equal)):
-            words, cnt = col.search_mask("12345", op, out=buf)
+        # the count kernel writes the registered buffer through its device mapping (no copy): every reply
+        # must be complete when the call returns, whatever the previous contents
+        rng2 = np.random.default_rng(12)
+        for it in range(60):
+            op, f = (("gt", np.greater), ("le", np.less_equal), ("ge", np.greater_equal), ("lt", np.less))[it % 4]
+            bound = int(rng2.integers(-(1 << 40), 1 << 40)) if it % 7 else 12345
+            buf[:] = np.uint64(0xFFFFFFFFFFFFFFFF) if it % 2 else np.uint64(0)
+            words, cnt = col.search_mask(str(bound), op, out=buf)
             assert words is buf
-            bits = np.unpackbits(buf.view(np.uint8), bitorder="little")[:n].astype(bool)
-            assert np.array_equal(bits, f(vals, 12345)) and cnt == int(bits.sum())
-            staged, cnt2 = col.search_mask("12345", op)
-            assert np.array_equal(staged, buf) and cnt2 == cnt
+            bits = np.unpackbits(buf.view(np.uint8), bitorder="little")
+            want = f(vals, bound)
+            assert np.array_equal(bits[:n].astype(bool), want) and not bits[n:].any(), (it, op, bound)
+            assert cnt == int(want.sum())
+            if it < 4:
+                staged, cnt2 = col.search_mask(str(bound), op)
+                assert np.array_equal(staged, buf) and cnt2 == cnt
     finally:
         eng.host_unregister(buf)
         col.close()
