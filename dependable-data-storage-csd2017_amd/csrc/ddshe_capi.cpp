@@ -185,7 +185,17 @@ bool host_registered(dds_ctx* ctx, const void* p, size_t bytes) {
   auto it = ctx->host_regs.upper_bound(b);
   if (it == ctx->host_regs.begin()) return false;
   --it;
-  return b + bytes <= it->first + it->second;
+  return b + bytes <= it->first + it->second.bytes;
+}
+
+void* host_device_ptr(dds_ctx* ctx, const void* p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(ctx->regmu);
+  const uintptr_t b = (uintptr_t)p;
+  auto it = ctx->host_regs.upper_bound(b);
+  if (it == ctx->host_regs.begin()) return nullptr;
+  --it;
+  if (b + bytes > it->first + it->second.bytes || !it->second.dptr) return nullptr;
+  return (char*)it->second.dptr + (b - it->first);
 }
 
 void record_time(dds_ctx* ctx, Worker* w, hipStream_t st, bool begin, int slot) {
@@ -1127,13 +1137,16 @@ int dds_host_register(dds_ctx* ctx, void* ptr, size_t bytes) {
   auto it = ctx->host_regs.upper_bound(b);
   if (it != ctx->host_regs.begin()) {
     auto pv = std::prev(it);
-    if (pv->first == b && pv->second == bytes) return DDS_OK;  // already registered
-    if (pv->first + pv->second > b) return fail(DDS_E_ARG, "overlaps a registered buffer");
+    if (pv->first == b && pv->second.bytes == bytes) return DDS_OK;  // already registered
+    if (pv->first + pv->second.bytes > b) return fail(DDS_E_ARG, "overlaps a registered buffer");
   }
   if (it != ctx->host_regs.end() && it->first < b + bytes) return fail(DDS_E_ARG, "overlaps a registered buffer");
   HIP_TRY(hipSetDevice(ctx->device));
-  HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
-  ctx->host_regs[b] = bytes;
+  HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterMapped));
+  void* dptr = nullptr;
+  if (hipHostGetDevicePointer(&dptr, ptr, 0) != hipSuccess) dptr = nullptr;  // DMA copies still work
+  (void)hipGetLastError();
+  ctx->host_regs[b] = dds_ctx::HostReg{bytes, dptr};
   return DDS_OK;
 }
 

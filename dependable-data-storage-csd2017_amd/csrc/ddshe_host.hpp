@@ -65,6 +65,7 @@ struct DevBuf {
 struct HostBuf {  // pinned staging (truly asynchronous H2D)
   void* p = nullptr;
   size_t cap = 0;
+  unsigned flags = 0;  // hipHostMalloc flags (set before the first ensure)
   ~HostBuf() {
     if (p) (void)hipHostFree(p);
   }
@@ -75,7 +76,7 @@ struct HostBuf {  // pinned staging (truly asynchronous H2D)
       p = nullptr;
       cap = 0;
     }
-    hipError_t e = hipHostMalloc(&p, bytes, 0);
+    hipError_t e = hipHostMalloc(&p, bytes, flags);
     if (e == hipSuccess) cap = bytes;
     return e;
   }
@@ -99,6 +100,8 @@ struct Worker {
   // per-row status bytes, and the event after each slot's last use
   HostBuf hch[2], hoff[2];
   HostBuf hstage;  // fold finalize: Y in, result out (pinned: no staging copies on the latency path)
+  HostBuf hcnt;    // coherent + mapped: the Search bitmask's match count, stored by the device
+  HostBuf hpair;   // pairwise batches: operands and results, coherent + mapped (k_pairs_sos reads and writes it)
   HostBuf hbig;    // large read-backs (Search ids / match masks, Order permutations) before the caller's copy
   DevBuf dch[2], doff[2], rflags;
   hipEvent_t ev_dec[2] = {};
@@ -241,10 +244,17 @@ struct dds_ctx {
   std::mutex pmu;
   std::map<ddshe::bn::Limbs, std::shared_ptr<ddshe::host::PairQueue>> pair_queues;
   std::atomic<uint64_t> pair_calls{0}, pair_launches{0};
+  // where a batch's time goes (dds_pair_timing): leader time per batch (gather, codec, GPU round trip,
+  // hand-back), its GPU round trip alone (H2D + k_pairs + D2H + sync), the longest batch
+  std::atomic<uint64_t> pair_batch_ns{0}, pair_gpu_ns{0}, pair_max_batch_ns{0};
   // caller output buffers registered with dds_host_register (page-locked): base -> bytes. Results
   // bound for them are DMA'd straight in, with no pinned staging buffer and no second host copy.
   std::mutex regmu;
-  std::map<uintptr_t, size_t> host_regs;
+  struct HostReg {
+    size_t bytes;
+    void* dptr;  // the range's device address (mapped), or null
+  };
+  std::map<uintptr_t, HostReg> host_regs;
   ~dds_ctx();
 };
 
@@ -495,6 +505,8 @@ int fold_even_modulus(dds_ctx* ctx, const bn::Limbs& M, const std::vector<bn::Li
 void record_time(dds_ctx* ctx, Worker* w, hipStream_t st, bool begin, int slot);
 // [p, p + bytes) lies inside one buffer the caller registered with dds_host_register
 bool host_registered(dds_ctx* ctx, const void* p, size_t bytes);
+// the device address of p when [p, p + bytes) lies in a registered, device-mapped buffer, else null
+void* host_device_ptr(dds_ctx* ctx, const void* p, size_t bytes);
 int pick_tpi(int S);
 size_t max_fold_groups(dds_ctx* ctx, int S);
 // Leaves of the reduction tree: X[l * xs + g * gs] (g = ids[k] when ids), l < Sin limbs of Win bits,

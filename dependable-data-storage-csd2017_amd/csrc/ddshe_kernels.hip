@@ -613,8 +613,12 @@ __device__ __forceinline__ uint32_t ope_thread_mask(const int64_t* __restrict__ 
 // [32w, 32w + 32) (group k = w / 32, the nibbles of threads 8(w % 32) .. +7), so the scatter ranks a
 // tile with one block-wide scan of 256 popcounts instead of 32 ballots per thread. Also writes the
 // tile's match count.
+// hlimit != 0: masks is a host buffer mapped into the device (a registered Search reply buffer) of hlimit
+// words: the words go out as system-scope stores (written through to host memory, the reply needs no
+// copy) and words past its end (the last tile's) are dropped
 __device__ __forceinline__ void ope_store_mask(uint32_t m, uint32_t* __restrict__ masks, uint32_t* __restrict__ counts,
-                                               size_t tile, unsigned long long* __restrict__ total = nullptr) {
+                                               size_t tile, unsigned long long* __restrict__ total = nullptr,
+                                               size_t hlimit = 0) {
   __shared__ uint8_t nib[kOpeGroups * kOpeBlock];
   __shared__ uint32_t wsum[kOpeBlock / 64];
   const int tid = threadIdx.x;
@@ -628,7 +632,11 @@ __device__ __forceinline__ void ope_store_mask(uint32_t m, uint32_t* __restrict_
   uint32_t word = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) word |= (uint32_t)((eight >> (8 * i)) & 0xFu) << (4 * i);
-  masks[tile * kOpeBlock + tid] = word;
+  const size_t wi = tile * kOpeBlock + tid;
+  if (hlimit == 0)
+    masks[wi] = word;
+  else if (wi < hlimit)
+    __hip_atomic_store(masks + wi, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid == 0) {
     uint32_t c = 0;
     for (int w = 0; w < kOpeBlock / 64; ++w) c += wsum[w];
@@ -651,10 +659,10 @@ __global__ void __launch_bounds__(kOpeBlock) k_ope_count(const int64_t* __restri
                                                          const uint8_t* __restrict__ valid, size_t n, int64_t bound,
                                                          int op, uint32_t vmask, uint32_t vbad,
                                                          uint32_t* __restrict__ masks, uint32_t* __restrict__ counts,
-                                                         unsigned long long* __restrict__ total) {
+                                                         unsigned long long* __restrict__ total, size_t hlimit) {
   const bool vec = ((uintptr_t)col % 16 == 0) && (!HasValid || (uintptr_t)valid % 4 == 0);
   const uint32_t m = ope_thread_mask<HasValid>(col, valid, n, bound, op, blockIdx.x, vec, vmask, vbad);
-  ope_store_mask(m, masks, counts, blockIdx.x, total);
+  ope_store_mask(m, masks, counts, blockIdx.x, total, hlimit);
 }
 
 // SearchEq/NEq front end (ddshe_strscan.hip's position index): same tile layout and masks as
@@ -758,6 +766,16 @@ __global__ void __launch_bounds__(1024) k_count_total(const uint32_t* __restrict
     uint64_t t = 0;
     for (int w = 0; w < 16; ++w) t += ws[w];
     *total = t;
+  }
+}
+
+// The Search bitmask's match count into a mapped host word (system-scope store), and the device counter
+// re-zeroed for the next call: one tiny launch instead of an 8-byte D2H copy and a memset
+__global__ void __launch_bounds__(64) k_total_handoff(uint64_t* __restrict__ total, uint64_t* __restrict__ htotal) {
+  if (threadIdx.x == 0) {
+    const uint64_t v = *total;
+    __hip_atomic_store(htotal, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    *total = 0;
   }
 }
 
@@ -1364,17 +1382,17 @@ void ope_code(int64_t bound, int op, int64_t* t, int* code) {
 }
 void ope_count(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, uint32_t* masks,
                uint32_t* counts, hipStream_t st, uint32_t vmask, uint32_t vbad,
-               unsigned long long* total = nullptr) {
+               unsigned long long* total = nullptr, size_t hlimit = 0) {
   const size_t nb = ope_blocks(n);
   int64_t t;
   int code;
   ope_code(bound, op, &t, &code);
   if (valid)
     hipLaunchKernelGGL(k_ope_count<true>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, t, code, vmask,
-                       vbad, masks, counts, total);
+                       vbad, masks, counts, total, hlimit);
   else
     hipLaunchKernelGGL(k_ope_count<false>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, t, code, vmask,
-                       vbad, masks, counts, total);
+                       vbad, masks, counts, total, hlimit);
 }
 }  // namespace
 
@@ -1392,10 +1410,17 @@ hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n,
 uint32_t* ope_mask_words(void* scratch, size_t n) { return (uint32_t*)scratch + ope_blocks(n); }
 
 hipError_t launch_ope_mask(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
-                           uint64_t* total, hipStream_t st, uint32_t vmask, uint32_t vbad, bool total_zeroed) {
+                           uint64_t* total, hipStream_t st, uint32_t vmask, uint32_t vbad, bool total_zeroed,
+                           uint32_t* hmask, size_t hwords, uint64_t* htotal) {
   const size_t nb = ope_blocks(n);
   if (nb == 0) return hipSuccess;
   uint32_t* counts = (uint32_t*)scratch;
+  if (hmask) {  // the words straight into the caller's mapped reply buffer (hwords u32 words)
+    if (!total_zeroed || hwords < (n + 31) / 32) return hipErrorInvalidValue;
+    ope_count(col, valid, n, bound, op, hmask, counts, st, vmask, vbad, (unsigned long long*)total, hwords);
+    if (htotal) hipLaunchKernelGGL(k_total_handoff, dim3(1), dim3(64), 0, st, total, htotal);
+    return hipGetLastError();
+  }
   if (total_zeroed) {  // the tiles add their counts into *total themselves
     ope_count(col, valid, n, bound, op, counts + nb, counts, st, vmask, vbad, (unsigned long long*)total);
     return hipGetLastError();

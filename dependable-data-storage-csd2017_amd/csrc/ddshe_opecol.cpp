@@ -549,19 +549,38 @@ int dds_opecol_search_mask(dds_opecol* col, const char* bound_dec, int op, uint6
     w->ctr_zero = false;
     uint32_t* stg = nullptr;
     HIP_TRY(stage_ptr(w, &stg));
+    // a registered caller buffer is written by the count kernel itself through its device mapping (no
+    // copy); DDSHE_MASK_ZEROCOPY=0 keeps one DMA into it instead
+    static const bool zc = [] {
+      const char* e = getenv("DDSHE_MASK_ZEROCOPY");
+      return !(e && e[0] == '0');
+    }();
+    uint32_t* hm = zc ? (uint32_t*)host_device_ptr(ctx, mask, bytes) : nullptr;
+    const bool direct = hm || host_registered(ctx, mask, bytes);  // page-locked caller buffer
+    uint64_t* hcnt = nullptr;  // zero-copy: the count arrives in a mapped host word (no copies at all)
+    if (hm) {
+      w->hcnt.flags = hipHostMallocCoherent | hipHostMallocMapped;
+      HIP_TRY(w->hcnt.ensure(64));
+      void* dp = nullptr;
+      HIP_TRY(hipHostGetDevicePointer(&dp, w->hcnt.p, 0));
+      hcnt = (uint64_t*)dp;
+      stg = (uint32_t*)w->hcnt.p;
+    }
     record_time(ctx, w, wl.st, true, 2);
-    HIP_TRY(launch_ope_mask(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, dtotal, wl.st, kSearch, kWide, true));
+    HIP_TRY(launch_ope_mask(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, dtotal, wl.st, kSearch, kWide, true,
+                            hm, hm ? 2 * words : 0, hcnt));
     record_time(ctx, w, wl.st, false, 2);
-    const bool direct = host_registered(ctx, mask, bytes);  // page-locked caller buffer: one DMA into it
     uint8_t* h = nullptr;
     if (!direct) {
       HIP_TRY(w->hbig.ensure(bytes));
       h = (uint8_t*)w->hbig.p;
     }
-    HIP_TRY(hipMemcpyAsync(stg, dtotal, 8, hipMemcpyDeviceToHost, wl.st));
-    HIP_TRY(hipMemcpyAsync(direct ? (void*)mask : (void*)h, mw, bytes, hipMemcpyDeviceToHost, wl.st));
+    if (!hm) {
+      HIP_TRY(hipMemcpyAsync(stg, dtotal, 8, hipMemcpyDeviceToHost, wl.st));
+      HIP_TRY(hipMemcpyAsync(direct ? (void*)mask : (void*)h, mw, bytes, hipMemcpyDeviceToHost, wl.st));
+    }
     HIP_TRY(hipEventRecord(w->ev_done, wl.st));
-    HIP_TRY(hipMemsetAsync(dtotal, 0, 8, wl.st));  // off the reply's path: the caller waits for ev_done only
+    if (!hm) HIP_TRY(hipMemsetAsync(dtotal, 0, 8, wl.st));  // off the reply's path: the caller waits for ev_done only
     w->ctr_zero = true;
     HIP_TRY(hipEventSynchronize(w->ev_done));
     uint64_t total = 0;

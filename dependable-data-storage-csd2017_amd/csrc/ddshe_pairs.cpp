@@ -32,6 +32,10 @@ namespace {
 
 constexpr size_t kTailPairs = 256;
 
+uint64_t since_ns(std::chrono::steady_clock::time_point t0) {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+}
+
 // the batch in the tree (latency) shape from limbs already < M: one workgroup product per pair
 int tail_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& batch) {
   const size_t mb = bn::byte_length(M), n = batch.size();
@@ -46,25 +50,44 @@ int tail_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& ba
   Worker* w = wl.w;
   const int S3 = mc.S3;  // one workgroup per pair in the tree shape (k_pairs_sos)
   const size_t words = (size_t)S3 * n;
-  HIP_TRY(w->hch[1].ensure(3 * words * 4));
-  HIP_TRY(w->x2.ensure(3 * words * 4));
-  uint32_t* h = (uint32_t*)w->hch[1].p;
+  // zero-copy (default): the operands and results live in coherent, device-mapped host memory that
+  // k_pairs_sos reads and writes over PCIe (a few hundred bytes per pair), so a batch is one launch and
+  // one synchronisation instead of an H2D copy, the launch, a D2H copy and the synchronisation.
+  // DDSHE_PAIR_ZEROCOPY=0: the staged copies.
+  static const bool zc = [] {
+    const char* e = getenv("DDSHE_PAIR_ZEROCOPY");
+    return !e || atoi(e) != 0;
+  }();
+  HostBuf& hb = zc ? w->hpair : w->hch[1];
+  if (zc) hb.flags = hipHostMallocCoherent | hipHostMallocMapped;
+  HIP_TRY(hb.ensure(3 * words * 4));
+  uint32_t* h = (uint32_t*)hb.p;
   for (size_t i = 0; i < n; ++i) {
     const std::vector<uint32_t> ra = bn::to_rw(batch[i]->a, S3, mc.W3), rb = bn::to_rw(batch[i]->b, S3, mc.W3);
     std::copy(ra.begin(), ra.end(), h + i * S3);
     std::copy(rb.begin(), rb.end(), h + words + i * S3);
   }
-  uint32_t* d = w->x2.as<uint32_t>();
-  HIP_TRY(hipMemcpyAsync(d, h, 2 * words * 4, hipMemcpyHostToDevice, wl.st));
-  HIP_TRY(launch_pairs_sos(S3, d, d + words, n, mc.d3, mc.d3 + 5 * (size_t)S3, d + 2 * words, wl.st));
-  HIP_TRY(hipMemcpyAsync(h + 2 * words, d + 2 * words, words * 4, hipMemcpyDeviceToHost, wl.st));
+  const auto g0 = std::chrono::steady_clock::now();
+  if (zc) {
+    void* dp = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dp, h, 0));
+    uint32_t* d = (uint32_t*)dp;
+    HIP_TRY(launch_pairs_sos(S3, d, d + words, n, mc.d3, mc.d3 + 5 * (size_t)S3, d + 2 * words, wl.st));
+  } else {
+    HIP_TRY(w->x2.ensure(3 * words * 4));
+    uint32_t* d = w->x2.as<uint32_t>();
+    HIP_TRY(hipMemcpyAsync(d, h, 2 * words * 4, hipMemcpyHostToDevice, wl.st));
+    HIP_TRY(launch_pairs_sos(S3, d, d + words, n, mc.d3, mc.d3 + 5 * (size_t)S3, d + 2 * words, wl.st));
+    HIP_TRY(hipMemcpyAsync(h + 2 * words, d + 2 * words, words * 4, hipMemcpyDeviceToHost, wl.st));
+  }
   HIP_TRY(hipStreamSynchronize(wl.st));
+  ctx->pair_gpu_ns.fetch_add(since_ns(g0));
   for (size_t i = 0; i < n; ++i) batch[i]->r = bn::from_rw(h + 2 * words + i * S3, S3, mc.W3);
   return DDS_OK;
 }
 
 // one k_pairs launch for the batch: results into each request (rc on failure)
-void run_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& batch) {
+void run_batch_(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& batch) {
   const size_t mb = bn::byte_length(M), n = batch.size();
   if (n <= kTailPairs) {
     const int rc = tail_batch(ctx, M, batch);
@@ -83,6 +106,16 @@ void run_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& ba
   for (size_t i = 0; i < n; ++i) {
     batch[i]->rc = rc;
     if (!rc) batch[i]->r = bn::from_be(O.data() + i * mb, mb);
+  }
+}
+
+void run_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& batch) {
+  const auto t0 = std::chrono::steady_clock::now();
+  run_batch_(ctx, M, batch);
+  const uint64_t ns = since_ns(t0);
+  ctx->pair_batch_ns.fetch_add(ns);
+  uint64_t mx = ctx->pair_max_batch_ns.load();
+  while (ns > mx && !ctx->pair_max_batch_ns.compare_exchange_weak(mx, ns)) {
   }
 }
 
@@ -221,6 +254,14 @@ int dds_pair_stats(dds_ctx* ctx, uint64_t* calls, uint64_t* launches) {
   if (!ctx) return fail(DDS_E_ARG, "bad arguments");
   if (calls) *calls = ctx->pair_calls.load();
   if (launches) *launches = ctx->pair_launches.load();
+  return DDS_OK;
+}
+
+int dds_pair_timing(dds_ctx* ctx, uint64_t* batch_ns, uint64_t* gpu_ns, uint64_t* max_batch_ns) {
+  if (!ctx) return fail(DDS_E_ARG, "bad arguments");
+  if (batch_ns) *batch_ns = ctx->pair_batch_ns.load();
+  if (gpu_ns) *gpu_ns = ctx->pair_gpu_ns.load();
+  if (max_batch_ns) *max_batch_ns = ctx->pair_max_batch_ns.load();
   return DDS_OK;
 }
 

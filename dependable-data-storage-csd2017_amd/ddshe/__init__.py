@@ -54,7 +54,7 @@ EXPORTS = [
     "dds_mctx_create", "dds_mctx_create_devices", "dds_mctx_destroy", "dds_mctx_shards", "dds_mcol_create",
     "dds_mcol_destroy", "dds_mcol_count", "dds_mcol_append", "dds_mcol_append_dec", "dds_mcol_fill_paillier_synth",
     "dds_mcol_fold", "dds_mcol_fold_rows", "dds_mcol_fold_dec",
-    "dds_pair_modmul_dec", "dds_pair_stats",
+    "dds_pair_modmul_dec", "dds_pair_stats", "dds_pair_timing",
     "dds_col_write_rows", "dds_col_write_rows_dec", "dds_col_set_live", "dds_col_live_count",
     "dds_mcol_write_rows", "dds_mcol_write_rows_dec", "dds_mcol_set_live", "dds_mcol_live_count",
     "dds_opecol_write_rows", "dds_opecol_write_rows_dec", "dds_opecol_set_live", "dds_opecol_live_count",
@@ -137,6 +137,7 @@ for _n in ("dds_sum_all_dec", "dds_mult_all_dec"):
 _u64p = C.POINTER(C.c_uint64)
 _sig("dds_pair_modmul_dec", C.c_int, C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, _sz, _szp)
 _sig("dds_pair_stats", C.c_int, C.c_void_p, _u64p, _u64p)
+_sig("dds_pair_timing", C.c_int, C.c_void_p, _u64p, _u64p, _u64p)
 _sig("dds_ctx_cache_stats", C.c_int, C.c_void_p, _szp, _szp)
 _sig("dds_col_fold_rows", C.c_int, C.c_void_p, _u64p, _sz, _u8p, _sz, _szp)
 _sig("dds_col_fold_dec", C.c_int, C.c_void_p, _u64p, _sz, C.c_char_p, _sz, _szp)
@@ -390,6 +391,12 @@ class Engine:
         calls, launches = C.c_uint64(), C.c_uint64()
         _check(_lib.dds_pair_stats(self._h, C.byref(calls), C.byref(launches)), "dds_pair_stats")
         return calls.value, launches.value
+
+    def pair_timing(self):
+        """(leader ns over all batches, GPU round-trip ns, longest batch ns) of pair_modmul_dec"""
+        b, g, m = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(_lib.dds_pair_timing(self._h, C.byref(b), C.byref(g), C.byref(m)), "dds_pair_timing")
+        return b.value, g.value, m.value
 
     def cache_stats(self):
         """(cached modulus constants, live pairwise queues) of this engine"""

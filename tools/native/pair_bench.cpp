@@ -55,8 +55,9 @@ int main(int argc, char** argv) {
       return 1;
     }
   }
-  uint64_t c0 = 0, l0 = 0, c1 = 0, l1 = 0;
+  uint64_t c0 = 0, l0 = 0, c1 = 0, l1 = 0, b0 = 0, g0 = 0, b1 = 0, g1 = 0, mx = 0;
   dds_pair_stats(ctx, &c0, &l0);
+  dds_pair_timing(ctx, &b0, &g0, nullptr);
   std::vector<std::vector<double>> lat(T);
   std::atomic<int> ready{0}, errors{0};
   std::atomic<bool> go{false};
@@ -85,6 +86,8 @@ int main(int argc, char** argv) {
   for (auto& x : th) x.join();
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   dds_pair_stats(ctx, &c1, &l1);
+  dds_pair_timing(ctx, &b1, &g1, &mx);
+  const double nl = l1 > l0 ? (double)(l1 - l0) : 1.0;
   std::vector<double> all;
   for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
   std::sort(all.begin(), all.end());
@@ -93,10 +96,14 @@ int main(int argc, char** argv) {
   dds_ctx_cache_stats(ctx, &moduli, &queues);
   printf("{\"threads\": %d, \"calls\": %llu, \"launches\": %llu, \"calls_per_launch\": %.2f, \"pairs_per_s\": %.1f, "
          "\"p50_ms\": %.4f, \"p99_ms\": %.4f, \"max_ms\": %.4f, \"errors\": %d, \"modulus_digits\": %zu, "
-         "\"cached_moduli\": %zu, \"pair_queues_after\": %zu, \"hw_threads\": %u, \"samples\": [",
+         "\"cached_moduli\": %zu, \"pair_queues_after\": %zu, \"hw_threads\": %u, "
+         "\"batch_us_per_launch\": %.2f, \"gpu_round_trip_us_per_launch\": %.2f, \"wall_us_per_launch\": %.2f, "
+         "\"mean_batches_in_flight\": %.3f, \"max_batch_ms\": %.3f, \"samples\": [",
          T, (unsigned long long)(c1 - c0), (unsigned long long)(l1 - l0),
          (l1 > l0) ? (double)(c1 - c0) / (double)(l1 - l0) : 0.0, (double)all.size() / secs, pct(0.5), pct(0.99),
-         all.empty() ? 0.0 : all.back(), errors.load(), mod.size(), moduli, queues, std::thread::hardware_concurrency());
+         all.empty() ? 0.0 : all.back(), errors.load(), mod.size(), moduli, queues, std::thread::hardware_concurrency(),
+         (double)(b1 - b0) / nl * 1e-3, (double)(g1 - g0) / nl * 1e-3, secs / nl * 1e6, (double)(b1 - b0) * 1e-9 / secs,
+         (double)mx * 1e-6);
   bool first = true;
   for (int t = 0; t < std::min(T, 4); ++t)
     for (size_t i = 0; i < R[t].size(); ++i) {
