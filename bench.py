@@ -838,7 +838,8 @@ class ProductFilterWorkload(_Workload):
                                           "path": "dds_opecol_search (device filter + D2H of the matching row ids)"}
         # the route-shaped answer as a row bitmask (dds_opecol_search_mask): 1 bit per row crosses PCIe
         mk_ms, mk_ok = [], True
-        # the caller's reusable mask buffer, page-locked once (dds_host_register): the mask is DMA'd into it
+        # the caller's reusable mask buffer, page-locked and device-mapped once (dds_host_register): the
+        # count kernel writes the mask into it
         mbuf = np.zeros(max(1, (self.mine + 63) // 64), dtype=np.uint64)
         self.eng.host_register(mbuf)
         for op, f in (("gt", np.greater), ("ge", np.greater_equal), ("lt", np.less), ("le", np.less_equal)):
@@ -857,8 +858,10 @@ class ProductFilterWorkload(_Workload):
             "route_roofline": {"bound": "hbm", "achieved": route_bytes / (med / 1e3) / 1e9, "peak": 8000.0,
                                "unit": "GB/s", "frac": route_bytes / (med / 1e3) / 1e9 / 8000.0,
                                "note": "column bytes / whole call time (host clock), mask read-back included"},
-            "path": "dds_opecol_search_mask (k_ope_count with the match count added per tile, one D2H of n/8 bytes "
-                    "straight into the caller's registered buffer + the count)"}
+            "path": "dds_opecol_search_mask (one k_ope_count launch stores the mask words through the device "
+                    "mapping of the caller's registered buffer and the per-tile counts into a mapped host array "
+                    "the host adds up: no copies" + (")" if os.environ.get("DDSHE_MASK_ZEROCOPY", "1") != "0"
+                                                     else "; DDSHE_MASK_ZEROCOPY=0: one D2H of n/8 bytes + the count)")}
         self.eng.host_unregister(mbuf)
         out.update(data="synthetic (seeded RSA ciphertexts of U[1,10^4) plaintexts, seeded OPE map)",
                    roofline=roof, filter_roofline=filt, cpu_baseline=cpu, verified=ok,

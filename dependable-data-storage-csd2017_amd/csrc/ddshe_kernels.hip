@@ -614,8 +614,9 @@ __device__ __forceinline__ uint32_t ope_thread_mask(const int64_t* __restrict__ 
 // tile with one block-wide scan of 256 popcounts instead of 32 ballots per thread. Also writes the
 // tile's match count.
 // hlimit != 0: masks is a host buffer mapped into the device (a registered Search reply buffer) of hlimit
-// words: the words go out as system-scope stores (written through to host memory, the reply needs no
-// copy) and words past its end (the last tile's) are dropped
+// words and counts a mapped host array: the words and the tile's count go out as system-scope stores
+// (written through to host memory, the reply needs no copy; the host adds the counts up) and words
+// past the buffer's end (the last tile's) are dropped
 __device__ __forceinline__ void ope_store_mask(uint32_t m, uint32_t* __restrict__ masks, uint32_t* __restrict__ counts,
                                                size_t tile, unsigned long long* __restrict__ total = nullptr,
                                                size_t hlimit = 0) {
@@ -640,7 +641,10 @@ __device__ __forceinline__ void ope_store_mask(uint32_t m, uint32_t* __restrict_
   if (tid == 0) {
     uint32_t c = 0;
     for (int w = 0; w < kOpeBlock / 64; ++w) c += wsum[w];
-    counts[tile] = c;
+    if (hlimit == 0)
+      counts[tile] = c;
+    else
+      __hip_atomic_store(counts + tile, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (total && c) atomicAdd(total, (unsigned long long)c);  // the Search bitmask's match count
   }
 }
@@ -766,16 +770,6 @@ __global__ void __launch_bounds__(1024) k_count_total(const uint32_t* __restrict
     uint64_t t = 0;
     for (int w = 0; w < 16; ++w) t += ws[w];
     *total = t;
-  }
-}
-
-// The Search bitmask's match count into a mapped host word (system-scope store), and the device counter
-// re-zeroed for the next call: one tiny launch instead of an 8-byte D2H copy and a memset
-__global__ void __launch_bounds__(64) k_total_handoff(uint64_t* __restrict__ total, uint64_t* __restrict__ htotal) {
-  if (threadIdx.x == 0) {
-    const uint64_t v = *total;
-    __hip_atomic_store(htotal, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    *total = 0;
   }
 }
 
@@ -1411,14 +1405,13 @@ uint32_t* ope_mask_words(void* scratch, size_t n) { return (uint32_t*)scratch + 
 
 hipError_t launch_ope_mask(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
                            uint64_t* total, hipStream_t st, uint32_t vmask, uint32_t vbad, bool total_zeroed,
-                           uint32_t* hmask, size_t hwords, uint64_t* htotal) {
+                           uint32_t* hmask, size_t hwords, uint32_t* hcounts) {
   const size_t nb = ope_blocks(n);
   if (nb == 0) return hipSuccess;
   uint32_t* counts = (uint32_t*)scratch;
-  if (hmask) {  // the words straight into the caller's mapped reply buffer (hwords u32 words)
-    if (!total_zeroed || hwords < (n + 31) / 32) return hipErrorInvalidValue;
-    ope_count(col, valid, n, bound, op, hmask, counts, st, vmask, vbad, (unsigned long long*)total, hwords);
-    if (htotal) hipLaunchKernelGGL(k_total_handoff, dim3(1), dim3(64), 0, st, total, htotal);
+  if (hmask) {  // words and tile counts straight into mapped host memory (hwords u32 words, nb counts)
+    if (!hcounts || hwords < (n + 31) / 32) return hipErrorInvalidValue;
+    ope_count(col, valid, n, bound, op, hmask, hcounts, st, vmask, vbad, nullptr, hwords);
     return hipGetLastError();
   }
   if (total_zeroed) {  // the tiles add their counts into *total themselves

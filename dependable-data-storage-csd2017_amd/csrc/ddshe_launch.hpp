@@ -118,13 +118,13 @@ hipError_t launch_ope_filter(const int64_t* col, const uint8_t* valid, size_t n,
 // Search as a row bitmask (no id scatter): after it, ope_mask_words(scratch, n)[w] bit b = row 32w + b
 // matches (words in row order; bits past n are 0) and *total (device) the number of matches
 // total_zeroed: *total is 0 on entry and the count kernel's tiles add into it (no reduction launch);
-// hmask (device pointer of a mapped host buffer of hwords u32 words, needs total_zeroed): the mask words
-// are written straight into it instead of into the scratch; htotal (with hmask: device pointer of a
-// mapped host u64): the match count is stored there and *total re-zeroed by one more tiny launch
+// hmask (device pointer of a mapped host buffer of hwords u32 words) with hcounts (device pointer of a
+// mapped host array of ope_blocks(n) u32): the mask words and the per-tile match counts are written
+// straight into host memory (total unused: the caller adds the counts up)
 hipError_t launch_ope_mask(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, void* scratch,
                            uint64_t* total, hipStream_t st, uint32_t vmask = 0xFFu, uint32_t vbad = 0u,
                            bool total_zeroed = false, uint32_t* hmask = nullptr, size_t hwords = 0,
-                           uint64_t* htotal = nullptr);
+                           uint32_t* hcounts = nullptr);
 uint32_t* ope_mask_words(void* scratch, size_t n);
 // rows i with (bytes[i] & vmask) != 0 -> ascending ids in out, count in *total (device); scratch as above
 hipError_t launch_byte_compact(const uint8_t* bytes, size_t n, uint32_t vmask, void* scratch, uint64_t* total,

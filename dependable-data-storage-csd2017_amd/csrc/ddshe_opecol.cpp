@@ -537,59 +537,63 @@ int dds_opecol_search_mask(dds_opecol* col, const char* bound_dec, int op, uint6
     WorkerLease wl(ctx);
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
-    // match words in row order (u32 word k = rows [32k, 32k + 32), little-endian: two of them are the
-    // u64 word of the caller's layout). The match count: the count kernel's tiles add into the worker's
-    // zeroed counter (no reduction launch), re-zeroed on the stream after it is read.
     const size_t bytes = words * 8;
-    HIP_TRY(w->misc.ensure(ope_scratch_bytes(n) + 64));
-    HIP_TRY(w->ctr.ensure(64));
-    uint32_t* mw = ope_mask_words(w->misc.p, n);
-    uint64_t* dtotal = w->ctr.as<uint64_t>();
-    if (!w->ctr_zero) HIP_TRY(hipMemsetAsync(dtotal, 0, 8, wl.st));
-    w->ctr_zero = false;
-    uint32_t* stg = nullptr;
-    HIP_TRY(stage_ptr(w, &stg));
-    // a registered caller buffer is written by the count kernel itself through its device mapping (no
-    // copy); DDSHE_MASK_ZEROCOPY=0 keeps one DMA into it instead
+    // a registered caller buffer is written by the count kernel itself through its device mapping, and
+    // the per-tile counts go to a mapped host array the host adds up: one launch, no copies at all.
+    // DDSHE_MASK_ZEROCOPY=0 keeps one DMA into it instead
     static const bool zc = [] {
       const char* e = getenv("DDSHE_MASK_ZEROCOPY");
       return !(e && e[0] == '0');
     }();
     uint32_t* hm = zc ? (uint32_t*)host_device_ptr(ctx, mask, bytes) : nullptr;
-    const bool direct = hm || host_registered(ctx, mask, bytes);  // page-locked caller buffer
-    uint64_t* hcnt = nullptr;  // zero-copy: the count arrives in a mapped host word (no copies at all)
+    uint64_t total = 0;
     if (hm) {
+      const size_t nb = ope_blocks(n);
       w->hcnt.flags = hipHostMallocCoherent | hipHostMallocMapped;
-      HIP_TRY(w->hcnt.ensure(64));
+      HIP_TRY(w->hcnt.ensure(std::max<size_t>(nb * 4, 64)));
       void* dp = nullptr;
       HIP_TRY(hipHostGetDevicePointer(&dp, w->hcnt.p, 0));
-      hcnt = (uint64_t*)dp;
-      stg = (uint32_t*)w->hcnt.p;
-    }
-    record_time(ctx, w, wl.st, true, 2);
-    HIP_TRY(launch_ope_mask(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, dtotal, wl.st, kSearch, kWide, true,
-                            hm, hm ? 2 * words : 0, hcnt));
-    record_time(ctx, w, wl.st, false, 2);
-    uint8_t* h = nullptr;
-    if (!direct) {
-      HIP_TRY(w->hbig.ensure(bytes));
-      h = (uint8_t*)w->hbig.p;
-    }
-    if (!hm) {
+      record_time(ctx, w, wl.st, true, 2);
+      HIP_TRY(launch_ope_mask(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, nullptr, wl.st, kSearch, kWide,
+                              false, hm, 2 * words, (uint32_t*)dp));
+      record_time(ctx, w, wl.st, false, 2);
+      HIP_TRY(hipStreamSynchronize(wl.st));
+      const uint32_t* c = (const uint32_t*)w->hcnt.p;
+      for (size_t t = 0; t < nb; ++t) total += c[t];
+    } else {
+      // match words in row order (u32 word k = rows [32k, 32k + 32), little-endian: two of them are the
+      // u64 word of the caller's layout). The match count: the count kernel's tiles add into the
+      // worker's zeroed counter (no reduction launch), re-zeroed on the stream after it is read.
+      HIP_TRY(w->misc.ensure(ope_scratch_bytes(n) + 64));
+      HIP_TRY(w->ctr.ensure(64));
+      uint32_t* mw = ope_mask_words(w->misc.p, n);
+      uint64_t* dtotal = w->ctr.as<uint64_t>();
+      if (!w->ctr_zero) HIP_TRY(hipMemsetAsync(dtotal, 0, 8, wl.st));
+      w->ctr_zero = false;
+      uint32_t* stg = nullptr;
+      HIP_TRY(stage_ptr(w, &stg));
+      const bool direct = host_registered(ctx, mask, bytes);  // page-locked caller buffer: one DMA
+      record_time(ctx, w, wl.st, true, 2);
+      HIP_TRY(launch_ope_mask(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, dtotal, wl.st, kSearch, kWide, true));
+      record_time(ctx, w, wl.st, false, 2);
+      uint8_t* h = nullptr;
+      if (!direct) {
+        HIP_TRY(w->hbig.ensure(bytes));
+        h = (uint8_t*)w->hbig.p;
+      }
       HIP_TRY(hipMemcpyAsync(stg, dtotal, 8, hipMemcpyDeviceToHost, wl.st));
       HIP_TRY(hipMemcpyAsync(direct ? (void*)mask : (void*)h, mw, bytes, hipMemcpyDeviceToHost, wl.st));
-    }
-    HIP_TRY(hipEventRecord(w->ev_done, wl.st));
-    if (!hm) HIP_TRY(hipMemsetAsync(dtotal, 0, 8, wl.st));  // off the reply's path: the caller waits for ev_done only
-    w->ctr_zero = true;
-    HIP_TRY(hipEventSynchronize(w->ev_done));
-    uint64_t total = 0;
-    memcpy(&total, stg, 8);
-    if (!direct) {
-      if (bytes >= ((size_t)1 << 20)) {
-        CopyPool::get().parallel_for(bytes, 4096, [&](size_t a, size_t e) { memcpy((char*)mask + a, h + a, e - a); });
-      } else {
-        memcpy(mask, h, bytes);
+      HIP_TRY(hipEventRecord(w->ev_done, wl.st));
+      HIP_TRY(hipMemsetAsync(dtotal, 0, 8, wl.st));  // off the reply's path: the caller waits for ev_done only
+      w->ctr_zero = true;
+      HIP_TRY(hipEventSynchronize(w->ev_done));
+      memcpy(&total, stg, 8);
+      if (!direct) {
+        if (bytes >= ((size_t)1 << 20)) {
+          CopyPool::get().parallel_for(bytes, 4096, [&](size_t a, size_t e) { memcpy((char*)mask + a, h + a, e - a); });
+        } else {
+          memcpy(mask, h, bytes);
+        }
       }
     }
     add_filter_time(ctx, w);

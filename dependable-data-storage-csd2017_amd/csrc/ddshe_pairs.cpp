@@ -60,7 +60,10 @@ int tail_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& ba
   }();
   HostBuf& hb = zc ? w->hpair : w->hch[1];
   if (zc) hb.flags = hipHostMallocCoherent | hipHostMallocMapped;
-  HIP_TRY(hb.ensure(3 * words * 4));
+  // sized once for the largest tail batch: re-pinning a growing buffer (hipHostFree + hipHostMalloc)
+  // stalls the leader for tens of ms (max batch 30-34 ms under 64 callers, tools/native/pairs_sweep.sh)
+  const size_t cap_bytes = 3 * (size_t)S3 * std::max(n, kTailPairs) * 4;
+  HIP_TRY(hb.ensure(cap_bytes));
   uint32_t* h = (uint32_t*)hb.p;
   for (size_t i = 0; i < n; ++i) {
     const std::vector<uint32_t> ra = bn::to_rw(batch[i]->a, S3, mc.W3), rb = bn::to_rw(batch[i]->b, S3, mc.W3);
@@ -74,7 +77,7 @@ int tail_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& ba
     uint32_t* d = (uint32_t*)dp;
     HIP_TRY(launch_pairs_sos(S3, d, d + words, n, mc.d3, mc.d3 + 5 * (size_t)S3, d + 2 * words, wl.st));
   } else {
-    HIP_TRY(w->x2.ensure(3 * words * 4));
+    HIP_TRY(w->x2.ensure(cap_bytes));
     uint32_t* d = w->x2.as<uint32_t>();
     HIP_TRY(hipMemcpyAsync(d, h, 2 * words * 4, hipMemcpyHostToDevice, wl.st));
     HIP_TRY(launch_pairs_sos(S3, d, d + words, n, mc.d3, mc.d3 + 5 * (size_t)S3, d + 2 * words, wl.st));
@@ -119,13 +122,15 @@ void run_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& ba
   }
 }
 
-// DDSHE_PAIR_SPIN_US (default 100): how long a caller in another leader's batch yields before it sleeps
-// (64 native callers, tools/native/pairs_sweep.sh: 400 us -> p99 9-19 ms, 100 us -> p99 0.8-1.0 ms at
-// the same 1.2-1.5e5 pairs/s: yielding threads crowd out the leaders on a 16-core host share)
+// DDSHE_PAIR_SPIN_US (default 0: sleep at once): how long a caller in another leader's batch yields
+// before it sleeps on its condition variable. 64 native callers (tools/native/pairs_sweep.sh, round 4,
+// warmed up, pre-sized batch buffers): 4 batches in flight 3.13e5 pairs/s at spin 0 against 2.94e5 at
+// 100 us (yielding threads take host cores the leaders and the decimal codec need); round 3, at 2 in
+// flight: 400 us -> p99 9-19 ms, 100 us -> 0.8-1.0 ms.
 int pair_spin_us() {
   static const int us = [] {
     const char* e = getenv("DDSHE_PAIR_SPIN_US");
-    return e ? atoi(e) : 100;
+    return e ? atoi(e) : 0;
   }();
   return us;
 }
@@ -261,7 +266,7 @@ int dds_pair_timing(dds_ctx* ctx, uint64_t* batch_ns, uint64_t* gpu_ns, uint64_t
   if (!ctx) return fail(DDS_E_ARG, "bad arguments");
   if (batch_ns) *batch_ns = ctx->pair_batch_ns.load();
   if (gpu_ns) *gpu_ns = ctx->pair_gpu_ns.load();
-  if (max_batch_ns) *max_batch_ns = ctx->pair_max_batch_ns.load();
+  if (max_batch_ns) *max_batch_ns = ctx->pair_max_batch_ns.exchange(0);  // window: since the last read
   return DDS_OK;
 }
 

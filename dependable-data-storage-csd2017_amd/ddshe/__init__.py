@@ -393,7 +393,8 @@ class Engine:
         return calls.value, launches.value
 
     def pair_timing(self):
-        """(leader ns over all batches, GPU round-trip ns, longest batch ns) of pair_modmul_dec"""
+        """(leader ns over all batches, GPU round-trip ns, longest batch ns since the last call) of
+        pair_modmul_dec"""
         b, g, m = C.c_uint64(), C.c_uint64(), C.c_uint64()
         _check(_lib.dds_pair_timing(self._h, C.byref(b), C.byref(g), C.byref(m)), "dds_pair_timing")
         return b.value, g.value, m.value

@@ -107,7 +107,8 @@ int dds_pair_modmul_dec(dds_ctx* ctx, const char* op1_dec, const char* op2_dec, 
 int dds_pair_stats(dds_ctx* ctx, uint64_t* calls, uint64_t* launches);
 /* Where the pairwise batches' time went, cumulative ns on this context: the leaders' time per batch
  * (operand repacking, GPU round trip, results), the GPU round trip alone (H2D + k_pairs + D2H +
- * synchronisation; batches of up to 256 pairs), and the longest batch. Against the wall clock of a
+ * synchronisation; batches of up to 256 pairs), and the longest batch since the previous call that
+ * asked for it (each such read starts a new window). Against the wall clock of a
  * run, batch_ns / wall is the mean number of batches in flight: near the in-flight limit the engine
  * bounds the rate, well below it the callers' own scheduling does. */
 int dds_pair_timing(dds_ctx* ctx, uint64_t* batch_ns, uint64_t* gpu_ns, uint64_t* max_batch_ns);

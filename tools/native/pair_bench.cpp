@@ -4,7 +4,7 @@
 // per-call latency distribution as one JSON line, plus a few (a, b, result) samples for the caller to
 // check (bench.py verifies them with Python ints).
 //
-//   pair_bench <modulus_dec> <threads> <calls_per_thread> [seed]
+//   pair_bench <modulus_dec> <threads> <calls_per_thread> [seed] [warmup_calls_per_thread=20]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -15,17 +15,19 @@
 #include <vector>
 #include <algorithm>
 #include <atomic>
+#include <sys/resource.h>
 
 #include "ddshe.h"
 
 int main(int argc, char** argv) {
   if (argc < 4) {
-    fprintf(stderr, "usage: %s <modulus_dec> <threads> <calls_per_thread> [seed]\n", argv[0]);
+    fprintf(stderr, "usage: %s <modulus_dec> <threads> <calls_per_thread> [seed] [warmup]\n", argv[0]);
     return 2;
   }
   const std::string mod = argv[1];
   const int T = atoi(argv[2]), K = atoi(argv[3]);
   const unsigned seed = argc > 4 ? (unsigned)atoi(argv[4]) : 7u;
+  const int WU = argc > 5 ? atoi(argv[5]) : 20;  // warm-up calls per thread, not timed
   dds_ctx* ctx = nullptr;
   if (dds_ctx_create(0, &ctx)) {
     fprintf(stderr, "dds_ctx_create: %s\n", dds_last_error());
@@ -56,8 +58,6 @@ int main(int argc, char** argv) {
     }
   }
   uint64_t c0 = 0, l0 = 0, c1 = 0, l1 = 0, b0 = 0, g0 = 0, b1 = 0, g1 = 0, mx = 0;
-  dds_pair_stats(ctx, &c0, &l0);
-  dds_pair_timing(ctx, &b0, &g0, nullptr);
   std::vector<std::vector<double>> lat(T);
   std::atomic<int> ready{0}, errors{0};
   std::atomic<bool> go{false};
@@ -66,6 +66,11 @@ int main(int argc, char** argv) {
     th.emplace_back([&, t] {
       std::vector<char> out(cap);
       size_t len = 0;
+      // warm-up under load: every caller's first calls (the workers, streams and pinned batch buffers
+      // the concurrent leaders need are set up here, as in a server that has been running)
+      for (int i = 0; i < WU; ++i)
+        if (dds_pair_modmul_dec(ctx, A[t][K].c_str(), B[t][K].c_str(), mod.c_str(), out.data(), cap, &len))
+          errors.fetch_add(1);
       ready.fetch_add(1);
       while (!go.load()) std::this_thread::yield();
       for (int i = 0; i < K; ++i) {
@@ -81,10 +86,17 @@ int main(int argc, char** argv) {
       }
     });
   while (ready.load() < T) std::this_thread::yield();
+  dds_pair_stats(ctx, &c0, &l0);
+  dds_pair_timing(ctx, &b0, &g0, &mx);  // also restarts the longest-batch window
+  struct rusage ru0, ru1;
+  getrusage(RUSAGE_SELF, &ru0);
   const auto t0 = std::chrono::steady_clock::now();
   go.store(true);
   for (auto& x : th) x.join();
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  getrusage(RUSAGE_SELF, &ru1);
+  auto tv = [](const timeval& a, const timeval& b) { return (double)(b.tv_sec - a.tv_sec) + 1e-6 * (double)(b.tv_usec - a.tv_usec); };
+  const double cpu_s = tv(ru0.ru_utime, ru1.ru_utime) + tv(ru0.ru_stime, ru1.ru_stime);
   dds_pair_stats(ctx, &c1, &l1);
   dds_pair_timing(ctx, &b1, &g1, &mx);
   const double nl = l1 > l0 ? (double)(l1 - l0) : 1.0;
@@ -98,12 +110,13 @@ int main(int argc, char** argv) {
          "\"p50_ms\": %.4f, \"p99_ms\": %.4f, \"max_ms\": %.4f, \"errors\": %d, \"modulus_digits\": %zu, "
          "\"cached_moduli\": %zu, \"pair_queues_after\": %zu, \"hw_threads\": %u, "
          "\"batch_us_per_launch\": %.2f, \"gpu_round_trip_us_per_launch\": %.2f, \"wall_us_per_launch\": %.2f, "
-         "\"mean_batches_in_flight\": %.3f, \"max_batch_ms\": %.3f, \"samples\": [",
+         "\"mean_batches_in_flight\": %.3f, \"max_batch_ms\": %.3f, \"cpu_cores_busy\": %.2f, "
+         "\"involuntary_switches\": %ld, \"voluntary_switches\": %ld, \"samples\": [",
          T, (unsigned long long)(c1 - c0), (unsigned long long)(l1 - l0),
          (l1 > l0) ? (double)(c1 - c0) / (double)(l1 - l0) : 0.0, (double)all.size() / secs, pct(0.5), pct(0.99),
          all.empty() ? 0.0 : all.back(), errors.load(), mod.size(), moduli, queues, std::thread::hardware_concurrency(),
          (double)(b1 - b0) / nl * 1e-3, (double)(g1 - g0) / nl * 1e-3, secs / nl * 1e6, (double)(b1 - b0) * 1e-9 / secs,
-         (double)mx * 1e-6);
+         (double)mx * 1e-6, cpu_s / secs, ru1.ru_nivcsw - ru0.ru_nivcsw, ru1.ru_nvcsw - ru0.ru_nvcsw);
   bool first = true;
   for (int t = 0; t < std::min(T, 4); ++t)
     for (size_t i = 0; i < R[t].size(); ++i) {
