@@ -246,7 +246,7 @@ struct dds_ctx {
   std::atomic<uint64_t> pair_calls{0}, pair_launches{0};
   // where a batch's time goes (dds_pair_timing): leader time per batch (gather, codec, GPU round trip,
   // hand-back), its GPU round trip alone (H2D + k_pairs + D2H + sync), the longest batch
-  std::atomic<uint64_t> pair_batch_ns{0}, pair_gpu_ns{0}, pair_max_batch_ns{0};
+  std::atomic<uint64_t> pair_batch_ns{0}, pair_gpu_ns{0}, pair_max_batch_ns{0}, pair_max_gpu_ns{0};
   // caller output buffers registered with dds_host_register (page-locked): base -> bytes. Results
   // bound for them are DMA'd straight in, with no pinned staging buffer and no second host copy.
   std::mutex regmu;

@@ -32,6 +32,12 @@ namespace {
 
 constexpr size_t kTailPairs = 256;
 
+void atomic_max(std::atomic<uint64_t>& m, uint64_t v) {
+  uint64_t cur = m.load();
+  while (v > cur && !m.compare_exchange_weak(cur, v)) {
+  }
+}
+
 uint64_t since_ns(std::chrono::steady_clock::time_point t0) {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -84,7 +90,9 @@ int tail_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& ba
     HIP_TRY(hipMemcpyAsync(h + 2 * words, d + 2 * words, words * 4, hipMemcpyDeviceToHost, wl.st));
   }
   HIP_TRY(hipStreamSynchronize(wl.st));
-  ctx->pair_gpu_ns.fetch_add(since_ns(g0));
+  const uint64_t gns = since_ns(g0);
+  ctx->pair_gpu_ns.fetch_add(gns);
+  atomic_max(ctx->pair_max_gpu_ns, gns);
   for (size_t i = 0; i < n; ++i) batch[i]->r = bn::from_rw(h + 2 * words + i * S3, S3, mc.W3);
   return DDS_OK;
 }
@@ -117,9 +125,7 @@ void run_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& ba
   run_batch_(ctx, M, batch);
   const uint64_t ns = since_ns(t0);
   ctx->pair_batch_ns.fetch_add(ns);
-  uint64_t mx = ctx->pair_max_batch_ns.load();
-  while (ns > mx && !ctx->pair_max_batch_ns.compare_exchange_weak(mx, ns)) {
-  }
+  atomic_max(ctx->pair_max_batch_ns, ns);
 }
 
 // DDSHE_PAIR_SPIN_US (default 0: sleep at once): how long a caller in another leader's batch yields
@@ -262,11 +268,13 @@ int dds_pair_stats(dds_ctx* ctx, uint64_t* calls, uint64_t* launches) {
   return DDS_OK;
 }
 
-int dds_pair_timing(dds_ctx* ctx, uint64_t* batch_ns, uint64_t* gpu_ns, uint64_t* max_batch_ns) {
+int dds_pair_timing(dds_ctx* ctx, uint64_t* batch_ns, uint64_t* gpu_ns, uint64_t* max_batch_ns,
+                    uint64_t* max_gpu_ns) {
   if (!ctx) return fail(DDS_E_ARG, "bad arguments");
   if (batch_ns) *batch_ns = ctx->pair_batch_ns.load();
   if (gpu_ns) *gpu_ns = ctx->pair_gpu_ns.load();
   if (max_batch_ns) *max_batch_ns = ctx->pair_max_batch_ns.exchange(0);  // window: since the last read
+  if (max_gpu_ns) *max_gpu_ns = ctx->pair_max_gpu_ns.exchange(0);
   return DDS_OK;
 }
 

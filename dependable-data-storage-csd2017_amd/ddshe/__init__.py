@@ -137,7 +137,7 @@ for _n in ("dds_sum_all_dec", "dds_mult_all_dec"):
 _u64p = C.POINTER(C.c_uint64)
 _sig("dds_pair_modmul_dec", C.c_int, C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, _sz, _szp)
 _sig("dds_pair_stats", C.c_int, C.c_void_p, _u64p, _u64p)
-_sig("dds_pair_timing", C.c_int, C.c_void_p, _u64p, _u64p, _u64p)
+_sig("dds_pair_timing", C.c_int, C.c_void_p, _u64p, _u64p, _u64p, _u64p)
 _sig("dds_ctx_cache_stats", C.c_int, C.c_void_p, _szp, _szp)
 _sig("dds_col_fold_rows", C.c_int, C.c_void_p, _u64p, _sz, _u8p, _sz, _szp)
 _sig("dds_col_fold_dec", C.c_int, C.c_void_p, _u64p, _sz, C.c_char_p, _sz, _szp)
@@ -393,11 +393,11 @@ class Engine:
         return calls.value, launches.value
 
     def pair_timing(self):
-        """(leader ns over all batches, GPU round-trip ns, longest batch ns since the last call) of
-        pair_modmul_dec"""
-        b, g, m = C.c_uint64(), C.c_uint64(), C.c_uint64()
-        _check(_lib.dds_pair_timing(self._h, C.byref(b), C.byref(g), C.byref(m)), "dds_pair_timing")
-        return b.value, g.value, m.value
+        """(leader ns over all batches, GPU round-trip ns, longest batch ns and longest round trip ns
+        since the last call) of pair_modmul_dec"""
+        b, g, m, mg = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(_lib.dds_pair_timing(self._h, C.byref(b), C.byref(g), C.byref(m), C.byref(mg)), "dds_pair_timing")
+        return b.value, g.value, m.value, mg.value
 
     def cache_stats(self):
         """(cached modulus constants, live pairwise queues) of this engine"""

@@ -107,11 +107,12 @@ int dds_pair_modmul_dec(dds_ctx* ctx, const char* op1_dec, const char* op2_dec, 
 int dds_pair_stats(dds_ctx* ctx, uint64_t* calls, uint64_t* launches);
 /* Where the pairwise batches' time went, cumulative ns on this context: the leaders' time per batch
  * (operand repacking, GPU round trip, results), the GPU round trip alone (H2D + k_pairs + D2H +
- * synchronisation; batches of up to 256 pairs), and the longest batch since the previous call that
- * asked for it (each such read starts a new window). Against the wall clock of a
+ * synchronisation; batches of up to 256 pairs), and the longest batch and the longest GPU round trip
+ * since the previous call that asked for them (each such read starts a new window). Against the wall clock of a
  * run, batch_ns / wall is the mean number of batches in flight: near the in-flight limit the engine
  * bounds the rate, well below it the callers' own scheduling does. */
-int dds_pair_timing(dds_ctx* ctx, uint64_t* batch_ns, uint64_t* gpu_ns, uint64_t* max_batch_ns);
+int dds_pair_timing(dds_ctx* ctx, uint64_t* batch_ns, uint64_t* gpu_ns, uint64_t* max_batch_ns,
+                    uint64_t* max_gpu_ns);
 /* Sizes of the per-request caches: modulus constants (LRU, at most DDSHE_MAX_MODULI, default 64) and
  * pairwise queues (one per modulus with calls in flight; dropped when idle). */
 int dds_ctx_cache_stats(dds_ctx* ctx, size_t* moduli, size_t* pair_queues);

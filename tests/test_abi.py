@@ -55,7 +55,7 @@ def test_null_arguments_rejected():
     assert lib.dds_modmul_fold(None, None, 0, None, 0, 0, None, 0, None) == ddshe.DDS_E_ARG
     assert lib.dds_ctx_create(0, None) == ddshe.DDS_E_ARG
     assert lib.dds_col_count(None) == 0
-    assert lib.dds_pair_timing(None, None, None, None) == ddshe.DDS_E_ARG
+    assert lib.dds_pair_timing(None, None, None, None, None) == ddshe.DDS_E_ARG
 
 
 def test_synth_plaintexts_match_kernel_formula():

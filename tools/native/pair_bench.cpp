@@ -57,7 +57,7 @@ int main(int argc, char** argv) {
       return 1;
     }
   }
-  uint64_t c0 = 0, l0 = 0, c1 = 0, l1 = 0, b0 = 0, g0 = 0, b1 = 0, g1 = 0, mx = 0;
+  uint64_t c0 = 0, l0 = 0, c1 = 0, l1 = 0, b0 = 0, g0 = 0, b1 = 0, g1 = 0, mx = 0, mg = 0;
   std::vector<std::vector<double>> lat(T);
   std::atomic<int> ready{0}, errors{0};
   std::atomic<bool> go{false};
@@ -87,7 +87,7 @@ int main(int argc, char** argv) {
     });
   while (ready.load() < T) std::this_thread::yield();
   dds_pair_stats(ctx, &c0, &l0);
-  dds_pair_timing(ctx, &b0, &g0, &mx);  // also restarts the longest-batch window
+  dds_pair_timing(ctx, &b0, &g0, &mx, &mg);  // also restarts the longest-batch windows
   struct rusage ru0, ru1;
   getrusage(RUSAGE_SELF, &ru0);
   const auto t0 = std::chrono::steady_clock::now();
@@ -98,7 +98,7 @@ int main(int argc, char** argv) {
   auto tv = [](const timeval& a, const timeval& b) { return (double)(b.tv_sec - a.tv_sec) + 1e-6 * (double)(b.tv_usec - a.tv_usec); };
   const double cpu_s = tv(ru0.ru_utime, ru1.ru_utime) + tv(ru0.ru_stime, ru1.ru_stime);
   dds_pair_stats(ctx, &c1, &l1);
-  dds_pair_timing(ctx, &b1, &g1, &mx);
+  dds_pair_timing(ctx, &b1, &g1, &mx, &mg);
   const double nl = l1 > l0 ? (double)(l1 - l0) : 1.0;
   std::vector<double> all;
   for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
@@ -110,13 +110,13 @@ int main(int argc, char** argv) {
          "\"p50_ms\": %.4f, \"p99_ms\": %.4f, \"max_ms\": %.4f, \"errors\": %d, \"modulus_digits\": %zu, "
          "\"cached_moduli\": %zu, \"pair_queues_after\": %zu, \"hw_threads\": %u, "
          "\"batch_us_per_launch\": %.2f, \"gpu_round_trip_us_per_launch\": %.2f, \"wall_us_per_launch\": %.2f, "
-         "\"mean_batches_in_flight\": %.3f, \"max_batch_ms\": %.3f, \"cpu_cores_busy\": %.2f, "
+         "\"mean_batches_in_flight\": %.3f, \"max_batch_ms\": %.3f, \"max_gpu_round_trip_ms\": %.3f, \"cpu_cores_busy\": %.2f, "
          "\"involuntary_switches\": %ld, \"voluntary_switches\": %ld, \"samples\": [",
          T, (unsigned long long)(c1 - c0), (unsigned long long)(l1 - l0),
          (l1 > l0) ? (double)(c1 - c0) / (double)(l1 - l0) : 0.0, (double)all.size() / secs, pct(0.5), pct(0.99),
          all.empty() ? 0.0 : all.back(), errors.load(), mod.size(), moduli, queues, std::thread::hardware_concurrency(),
          (double)(b1 - b0) / nl * 1e-3, (double)(g1 - g0) / nl * 1e-3, secs / nl * 1e6, (double)(b1 - b0) * 1e-9 / secs,
-         (double)mx * 1e-6, cpu_s / secs, ru1.ru_nivcsw - ru0.ru_nivcsw, ru1.ru_nvcsw - ru0.ru_nvcsw);
+         (double)mx * 1e-6, (double)mg * 1e-6, cpu_s / secs, ru1.ru_nivcsw - ru0.ru_nivcsw, ru1.ru_nvcsw - ru0.ru_nvcsw);
   bool first = true;
   for (int t = 0; t < std::min(T, 4); ++t)
     for (size_t i = 0; i < R[t].size(); ++i) {
