@@ -836,33 +836,45 @@ class ProductFilterWorkload(_Workload):
         res_ms.sort()
         filt["resident_opecol_search"] = {"median_ms": res_ms[len(res_ms) // 2], "matches": res_ok,
                                           "path": "dds_opecol_search (device filter + D2H of the matching row ids)"}
-        # the route-shaped answer as a row bitmask (dds_opecol_search_mask): 1 bit per row crosses PCIe
-        mk_ms, mk_ok = [], True
-        # the caller's reusable mask buffer, page-locked and device-mapped once (dds_host_register): the
-        # count kernel writes the mask into it
-        mbuf = np.zeros(max(1, (self.mine + 63) // 64), dtype=np.uint64)
-        self.eng.host_register(mbuf)
-        for op, f in (("gt", np.greater), ("ge", np.greater_equal), ("lt", np.less), ("le", np.less_equal)):
-            for _ in range(5):
-                t = time.perf_counter()
-                words, cnt = self.opecol.search_mask(str(self.bound), op, out=mbuf)
-                mk_ms.append((time.perf_counter() - t) * 1e3)
-            if self.world == 1:
-                bits = np.unpackbits(words.view(np.uint8), bitorder="little")[: self.mine].astype(bool)
-                mk_ok = mk_ok and cnt == counts[op] and bool(np.array_equal(bits, f(self.ope_host, self.bound)))
-        mk_ms.sort()
-        med = mk_ms[len(mk_ms) // 2]
+        # the route-shaped answer as a row bitmask (dds_opecol_search_mask): 1 bit per row crosses PCIe,
+        # written by the count kernel straight into a device-mapped reply buffer the caller reuses:
+        # an engine-allocated one (dds_host_alloc, placed by the HIP runtime for the device) and a caller
+        # array page-locked once (dds_host_register)
+        nwords = max(1, (self.mine + 63) // 64)
         route_bytes = 9 * self.mine  # what the route reads per call (int64 + class byte per row)
+
+        def mask_route(mbuf):
+            ms, ok = [], True
+            for op, f in (("gt", np.greater), ("ge", np.greater_equal), ("lt", np.less), ("le", np.less_equal)):
+                for _ in range(5):
+                    t = time.perf_counter()
+                    words, cnt = self.opecol.search_mask(str(self.bound), op, out=mbuf)
+                    ms.append((time.perf_counter() - t) * 1e3)
+                if self.world == 1:
+                    bits = np.unpackbits(words.view(np.uint8), bitorder="little")[: self.mine].astype(bool)
+                    ok = ok and cnt == counts[op] and bool(np.array_equal(bits, f(self.ope_host, self.bound)))
+            ms.sort()
+            return ms[len(ms) // 2], ok
+
+        abuf = self.eng.host_alloc(nwords, np.uint64)
+        med, mk_ok = mask_route(abuf)
+        self.eng.host_free(abuf)
+        rbuf = np.zeros(nwords, dtype=np.uint64)
+        self.eng.host_register(rbuf)
+        reg_med, reg_ok = mask_route(rbuf)
+        self.eng.host_unregister(rbuf)
+        zc = os.environ.get("DDSHE_MASK_ZEROCOPY", "1") != "0"
         filt["resident_opecol_search_mask"] = {
-            "median_ms": med, "matches": mk_ok, "rows": self.mine,
+            "median_ms": med, "matches": mk_ok and reg_ok, "rows": self.mine,
+            "registered_caller_array_ms": reg_med,
             "route_roofline": {"bound": "hbm", "achieved": route_bytes / (med / 1e3) / 1e9, "peak": 8000.0,
                                "unit": "GB/s", "frac": route_bytes / (med / 1e3) / 1e9 / 8000.0,
                                "note": "column bytes / whole call time (host clock), mask read-back included"},
-            "path": "dds_opecol_search_mask (one k_ope_count launch stores the mask words through the device "
-                    "mapping of the caller's registered buffer and the per-tile counts into a mapped host array "
-                    "the host adds up: no copies" + (")" if os.environ.get("DDSHE_MASK_ZEROCOPY", "1") != "0"
-                                                     else "; DDSHE_MASK_ZEROCOPY=0: one D2H of n/8 bytes + the count)")}
-        self.eng.host_unregister(mbuf)
+            "path": "dds_opecol_search_mask into a dds_host_alloc reply buffer (median_ms) and into a "
+                    "dds_host_register'ed caller array (registered_caller_array_ms): one k_ope_count launch "
+                    "stores the mask words through the buffer's device mapping and the per-tile counts into a "
+                    "mapped host array the host adds up" + (": no copies" if zc else
+                                                              "; DDSHE_MASK_ZEROCOPY=0: one D2H of n/8 bytes + the count")}
         out.update(data="synthetic (seeded RSA ciphertexts of U[1,10^4) plaintexts, seeded OPE map)",
                    roofline=roof, filter_roofline=filt, cpu_baseline=cpu, verified=ok,
                    fold_ms_per_step=self.fold_ms / a.steps, filter_ms_per_step=self.filter_ms / a.steps,

@@ -1073,7 +1073,13 @@ int col_set_live(dds_col* col, const uint64_t* ids, size_t n, const uint8_t* liv
 
 // =============================================================================
 dds_ctx::~dds_ctx() {
-  for (auto& kv : host_regs) (void)hipHostUnregister(reinterpret_cast<void*>(kv.first));
+  for (auto& kv : host_regs) {
+    void* p = reinterpret_cast<void*>(kv.first);
+    if (kv.second.owned)
+      (void)hipHostFree(p);
+    else
+      (void)hipHostUnregister(p);
+  }
 }
 
 extern "C" {
@@ -1146,7 +1152,7 @@ int dds_host_register(dds_ctx* ctx, void* ptr, size_t bytes) {
   void* dptr = nullptr;
   if (hipHostGetDevicePointer(&dptr, ptr, 0) != hipSuccess) dptr = nullptr;  // DMA copies still work
   (void)hipGetLastError();
-  ctx->host_regs[b] = dds_ctx::HostReg{bytes, dptr};
+  ctx->host_regs[b] = dds_ctx::HostReg{bytes, dptr, false};
   return DDS_OK;
 }
 
@@ -1155,11 +1161,42 @@ int dds_host_unregister(dds_ctx* ctx, void* ptr) {
   std::lock_guard<std::mutex> lk(ctx->regmu);
   auto it = ctx->host_regs.find((uintptr_t)ptr);
   if (it == ctx->host_regs.end()) return fail(DDS_E_ARG, "not a registered buffer");
+  if (it->second.owned) return fail(DDS_E_ARG, "allocated by dds_host_alloc: release it with dds_host_free");
   (void)hipSetDevice(ctx->device);
   (void)hipDeviceSynchronize();  // no copy into it is still in flight
   hipError_t e = hipHostUnregister(ptr);
   ctx->host_regs.erase(it);
   return e == hipSuccess ? DDS_OK : fail(DDS_E_HIP, "hipHostUnregister");
+}
+
+int dds_host_alloc(dds_ctx* ctx, size_t bytes, void** out) {
+  if (!ctx || !bytes || !out) return fail(DDS_E_ARG, "bad arguments");
+  *out = nullptr;
+  std::lock_guard<std::mutex> lk(ctx->regmu);
+  HIP_TRY(hipSetDevice(ctx->device));
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocMapped) != hipSuccess || !p) {
+    (void)hipGetLastError();
+    return fail(DDS_E_NOMEM, "hipHostMalloc");
+  }
+  void* dptr = nullptr;
+  if (hipHostGetDevicePointer(&dptr, p, 0) != hipSuccess) dptr = nullptr;
+  (void)hipGetLastError();
+  ctx->host_regs[(uintptr_t)p] = dds_ctx::HostReg{bytes, dptr, true};
+  *out = p;
+  return DDS_OK;
+}
+
+int dds_host_free(dds_ctx* ctx, void* ptr) {
+  if (!ctx || !ptr) return fail(DDS_E_ARG, "bad arguments");
+  std::lock_guard<std::mutex> lk(ctx->regmu);
+  auto it = ctx->host_regs.find((uintptr_t)ptr);
+  if (it == ctx->host_regs.end() || !it->second.owned) return fail(DDS_E_ARG, "not a dds_host_alloc buffer");
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();  // nothing still writes into it
+  hipError_t e = hipHostFree(ptr);
+  ctx->host_regs.erase(it);
+  return e == hipSuccess ? DDS_OK : fail(DDS_E_HIP, "hipHostFree");
 }
 
 int dds_ctx_set_stream(dds_ctx* ctx, void* stream) {

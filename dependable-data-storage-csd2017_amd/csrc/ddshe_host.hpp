@@ -252,7 +252,8 @@ struct dds_ctx {
   std::mutex regmu;
   struct HostReg {
     size_t bytes;
-    void* dptr;  // the range's device address (mapped), or null
+    void* dptr;          // the range's device address (mapped), or null
+    bool owned = false;  // allocated by dds_host_alloc (hipHostFree), else registered caller memory
   };
   std::map<uintptr_t, HostReg> host_regs;
   ~dds_ctx();

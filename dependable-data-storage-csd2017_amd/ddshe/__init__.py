@@ -60,7 +60,8 @@ EXPORTS = [
     "dds_opecol_write_rows", "dds_opecol_write_rows_dec", "dds_opecol_set_live", "dds_opecol_live_count",
     "dds_opecol_search_mask", "dds_ctx_cache_stats",
     "dds_strtab_append", "dds_strtab_write_rows", "dds_strtab_set_live", "dds_strtab_rows", "dds_strtab_live_count",
-    "dds_strtab_stats", "dds_strtab_truncate", "dds_host_register", "dds_host_unregister",
+    "dds_strtab_stats", "dds_strtab_truncate", "dds_host_register", "dds_host_unregister", "dds_host_alloc",
+    "dds_host_free",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -119,6 +120,8 @@ _sig("dds_strtab_stats", C.c_int, C.c_void_p, C.c_void_p, _sz)
 _sig("dds_strtab_truncate", C.c_int, C.c_void_p, _sz)
 _sig("dds_host_register", C.c_int, C.c_void_p, C.c_void_p, _sz)
 _sig("dds_host_unregister", C.c_int, C.c_void_p, C.c_void_p)
+_sig("dds_host_alloc", C.c_int, C.c_void_p, _sz, C.POINTER(C.c_void_p))
+_sig("dds_host_free", C.c_int, C.c_void_p, C.c_void_p)
 _sig("dds_search_eq", C.c_int, C.c_void_p, _sz, C.c_char_p, _sz, C.c_int, C.c_void_p, _szp)
 _sig("dds_search_entry", C.c_int, C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), _sz, C.c_int, C.c_void_p,
      _szp)
@@ -479,6 +482,18 @@ class Engine:
 
     def host_unregister(self, arr: np.ndarray):
         _check(_lib.dds_host_unregister(self._h, arr.ctypes.data_as(C.c_void_p)), "dds_host_unregister")
+
+    def host_alloc(self, count: int, dtype=np.uint64) -> np.ndarray:
+        """dds_host_alloc: an engine-allocated reply array (page-locked, device-mapped, registered).
+        Release it with host_free before dropping the engine (the array must not be used after)."""
+        dt = np.dtype(dtype)
+        p = C.c_void_p()
+        _check(_lib.dds_host_alloc(self._h, max(1, count) * dt.itemsize, C.byref(p)), "dds_host_alloc")
+        buf = (C.c_uint8 * (max(1, count) * dt.itemsize)).from_address(p.value)
+        return np.frombuffer(buf, dtype=dt, count=max(1, count))
+
+    def host_free(self, arr: np.ndarray):
+        _check(_lib.dds_host_free(self._h, arr.ctypes.data_as(C.c_void_p)), "dds_host_free")
 
     def strtab(self, rows) -> "StrTable":
         """Device-resident string table of the rows' contents (lists of values, str()-ed)."""

@@ -117,12 +117,18 @@ int dds_pair_timing(dds_ctx* ctx, uint64_t* batch_ns, uint64_t* gpu_ns, uint64_t
  * pairwise queues (one per modulus with calls in flight; dropped when idle). */
 int dds_ctx_cache_stats(dds_ctx* ctx, size_t* moduli, size_t* pair_queues);
 /* Page-lock a caller output buffer the caller reuses across requests (a JNA Memory, a direct
- * ByteBuffer): results bound for it (dds_opecol_search_mask's bitmask, row-id lists of the searches
- * and orders) are then DMA'd straight in, without a pinned staging buffer and a second host copy.
+ * ByteBuffer) and map it into the device: results bound for it are then written straight in, without
+ * a pinned staging buffer and a second host copy (dds_opecol_search_mask's bitmask by the count kernel
+ * itself through the mapping; row-id lists of the searches and orders by one DMA).
  * Registered ranges must not overlap; the buffer must stay allocated until dds_host_unregister (or
  * dds_ctx_destroy, which unregisters every buffer). */
 int dds_host_register(dds_ctx* ctx, void* ptr, size_t bytes);
 int dds_host_unregister(dds_ctx* ctx, void* ptr);
+/* A reply buffer allocated by the engine: page-locked, mapped into the device and placed by the HIP
+ * runtime for the context's device (hipHostMalloc), registered as dds_host_register would. Free it
+ * with dds_host_free (dds_ctx_destroy frees any left); dds_host_unregister refuses it. */
+int dds_host_alloc(dds_ctx* ctx, size_t bytes, void** out);
+int dds_host_free(dds_ctx* ctx, void* ptr);
 /* SumAll without nsqr (plain BigInteger add, DDSRestServer.scala:425): sum of count
  * operands; result big-endian in out (min(out_cap) = width + 8 is always enough). */
 int dds_bigint_sum(dds_ctx* ctx, const uint8_t* operands_be, size_t width, size_t count, uint8_t* out,

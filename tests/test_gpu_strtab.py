@@ -294,3 +294,32 @@ def test_search_mask_registered_buffer(eng):
     finally:
         eng.host_unregister(buf)
         col.close()
+
+
+def test_search_mask_engine_allocated_buffer(eng):
+    """dds_host_alloc: an engine-allocated, device-mapped reply buffer takes the Search bitmask like a
+    registered one; dds_host_unregister refuses it and dds_host_free releases it once."""
+    from ddshe import DDSError
+    rng = np.random.default_rng(13)
+    n = 300_017
+    vals = rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)
+    col = eng.opecol(n)
+    col.append(vals)
+    buf = eng.host_alloc((n + 63) // 64, np.uint64)
+    try:
+        with pytest.raises(DDSError):
+            eng.host_unregister(buf)
+        for it, (op, f) in enumerate((("gt", np.greater), ("le", np.less_equal), ("ge", np.greater_equal),
+                                      ("lt", np.less)) * 3):
+            bound = int(rng.integers(-(1 << 40), 1 << 40))
+            buf[:] = np.uint64(0xFFFFFFFFFFFFFFFF) if it % 2 else np.uint64(0)
+            words, cnt = col.search_mask(str(bound), op, out=buf)
+            bits = np.unpackbits(buf.view(np.uint8), bitorder="little")
+            want = f(vals, bound)
+            assert np.array_equal(bits[:n].astype(bool), want) and not bits[n:].any(), (it, op, bound)
+            assert cnt == int(want.sum())
+    finally:
+        eng.host_free(buf)
+        col.close()
+    with pytest.raises(DDSError):
+        eng.host_free(buf)
