@@ -1053,8 +1053,8 @@ class OrderWorkload(_Workload):
         oc = self.eng.opecol(max(1, self.mine))
         try:
             oc.append(self.col, np.where(self.valid != 0, 2, 0).astype(np.uint8))
-            out_buf = np.empty(max(1, self.mine), dtype=np.uint32)
-            self.eng.host_register(out_buf)  # the reply buffer a caller reuses: the ids are DMA'd into it
+            # the reply buffer a caller reuses, engine-allocated (dds_host_alloc): the ids are DMA'd into it
+            out_buf = self.eng.host_alloc(max(1, self.mine), np.uint32)
             ts = []
             self.eng.set_timing(True)
             self.eng.reset_timing()
@@ -1064,16 +1064,17 @@ class OrderWorkload(_Workload):
                 ts.append((time.perf_counter() - t) * 1e3)
             _, _, dev_ms, _ = self.eng.timing()
             self.eng.set_timing(False)
-            self.eng.host_unregister(out_buf)
             ts.sort()
             ok = bool(np.array_equal(perm, self.d_out.cpu().numpy().view(np.uint32))) if self.args.verify else None
+            del perm
+            self.eng.host_free(out_buf)
             med = ts[len(ts) // 2]
             return {"median_ms": med, "device_ms": dev_ms / 7, "matches_raw_array_order": ok,
                     "route_roofline": {"bound": "hbm", "achieved": 13 * self.mine / (med / 1e3) / 1e9, "peak": 8000.0,
                                        "unit": "GB/s", "frac": 13 * self.mine / (med / 1e3) / 1e9 / 8000.0,
                                        "note": "13 B/row / whole call time (host clock), the 40 MB id read-back included"},
                     "path": "dds_opecol_order (no k_rs_prep: bounds kept on writes; device_ms = HIP events around "
-                            "the ordering) + D2H of the permutation into a registered reply buffer"}
+                            "the ordering) + D2H of the permutation into a dds_host_alloc reply buffer"}
         finally:
             oc.close()
 

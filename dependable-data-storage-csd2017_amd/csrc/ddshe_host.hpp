@@ -65,7 +65,8 @@ struct DevBuf {
 struct HostBuf {  // pinned staging (truly asynchronous H2D)
   void* p = nullptr;
   size_t cap = 0;
-  unsigned flags = 0;  // hipHostMalloc flags (set before the first ensure)
+  unsigned flags = 0;     // hipHostMalloc flags (set before the first ensure)
+  void* dptr = nullptr;  // device address when flags map the buffer (hipHostMallocMapped)
   ~HostBuf() {
     if (p) (void)hipHostFree(p);
   }
@@ -76,8 +77,10 @@ struct HostBuf {  // pinned staging (truly asynchronous H2D)
       p = nullptr;
       cap = 0;
     }
+    dptr = nullptr;
     hipError_t e = hipHostMalloc(&p, bytes, flags);
     if (e == hipSuccess) cap = bytes;
+    if (e == hipSuccess && (flags & hipHostMallocMapped)) e = hipHostGetDevicePointer(&dptr, p, 0);
     return e;
   }
 };
@@ -355,13 +358,16 @@ struct WorkerLease {
     // caller's current device is restored when the lease ends)
     if (hipGetDevice(&prev_device) != hipSuccess) prev_device = -1;
     if (prev_device != ctx->device && hipSetDevice(ctx->device) != hipSuccess) return fail(DDS_E_HIP, "hipSetDevice");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    if (!ctx->idle.empty()) {
-      w = ctx->idle.back();
-      ctx->idle.pop_back();
-    } else {
+    {
+      std::lock_guard<std::mutex> lk(ctx->mu);
+      if (!ctx->idle.empty()) {
+        w = ctx->idle.back();
+        ctx->idle.pop_back();
+      }
+    }
+    if (!w) {  // a new worker: its streams and events are created outside the context lock, so callers
+               // that find an idle worker (and get_mod lookups) do not wait behind the creation
       auto nw = std::make_unique<Worker>();
-      if (hipSetDevice(ctx->device) != hipSuccess) return fail(DDS_E_HIP, "hipSetDevice");
       if (hipStreamCreateWithFlags(&nw->stream, hipStreamNonBlocking) != hipSuccess)
         return fail(DDS_E_HIP, "hipStreamCreate");
       for (auto& e : nw->ev)
@@ -371,6 +377,7 @@ struct WorkerLease {
       if (hipEventCreateWithFlags(&nw->ev_peer, hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&nw->ev_done, hipEventDisableTiming) != hipSuccess)
         return fail(DDS_E_HIP, "hipEventCreate");
+      std::lock_guard<std::mutex> lk(ctx->mu);
       w = nw.get();
       ctx->workers.push_back(std::move(nw));
     }

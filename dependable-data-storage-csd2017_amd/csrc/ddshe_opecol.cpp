@@ -551,8 +551,7 @@ int dds_opecol_search_mask(dds_opecol* col, const char* bound_dec, int op, uint6
       const size_t nb = ope_blocks(n);
       w->hcnt.flags = hipHostMallocCoherent | hipHostMallocMapped;
       HIP_TRY(w->hcnt.ensure(std::max<size_t>(nb * 4, 64)));
-      void* dp = nullptr;
-      HIP_TRY(hipHostGetDevicePointer(&dp, w->hcnt.p, 0));
+      void* dp = w->hcnt.dptr;
       record_time(ctx, w, wl.st, true, 2);
       HIP_TRY(launch_ope_mask(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, nullptr, wl.st, kSearch, kWide,
                               false, hm, 2 * words, (uint32_t*)dp));

@@ -78,9 +78,7 @@ int tail_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& ba
   }
   const auto g0 = std::chrono::steady_clock::now();
   if (zc) {
-    void* dp = nullptr;
-    HIP_TRY(hipHostGetDevicePointer(&dp, h, 0));
-    uint32_t* d = (uint32_t*)dp;
+    uint32_t* d = (uint32_t*)hb.dptr;
     HIP_TRY(launch_pairs_sos(S3, d, d + words, n, mc.d3, mc.d3 + 5 * (size_t)S3, d + 2 * words, wl.st));
   } else {
     HIP_TRY(w->x2.ensure(cap_bytes));
