@@ -191,3 +191,87 @@ def test_resident_opecol_order_msd_with_dead_rows(eng):
         want = idx[np.argsort(key, kind="stable")]
         assert np.array_equal(oc.order(desc), want.astype(np.uint32)), desc
     oc.close()
+
+
+@pytest.mark.parametrize("kind", ["at_limit", "over_limit", "extremes_mixed", "ope_map_1e4", "all_lacking_but_two"])
+def test_order_dense_ranks(eng, kind):
+    """Columns with few distinct keys (OPE ciphertexts of < 10^4 plaintexts) take the dense-rank path:
+    one pass collects the distinct keys in a hash set, their ranks come from a compare-count, and two
+    8-bit passes over the u16 ranks order the rows stably. 65,534 distinct keys is the most it takes
+    (the ranks and the lacking rows' rank must fit 16 bits); one more and the engine sorts by the key
+    bits instead. INT64_MAX (ascending) / INT64_MIN (descending) map to the set's empty marker and are
+    ranked through a flag."""
+    rng = np.random.default_rng(53)
+    n = 300_007
+    if kind in ("at_limit", "over_limit"):
+        d = 65_534 if kind == "at_limit" else 65_535
+        vals = rng.choice(np.arange(-(1 << 40), 1 << 40, 7919, dtype=np.int64), size=d, replace=False)
+        col = np.concatenate([vals, vals[rng.integers(0, d, size=n - d)]])
+        rng.shuffle(col)
+    elif kind == "extremes_mixed":
+        vals = np.array([-2**63, 2**63 - 1, -2**63 + 1, 2**63 - 2, 0, -1, 1, 12345], dtype=np.int64)
+        col = vals[rng.integers(0, len(vals), size=n)]
+    elif kind == "ope_map_1e4":
+        ope_map = np.cumsum(rng.integers(1, 1 << 40, size=10001, dtype=np.int64)) - (1 << 52)
+        col = ope_map[rng.integers(1, 10001, size=n)]
+    else:
+        col = rng.integers(-5, 5, size=n, dtype=np.int64)
+    valid = (rng.random(n) > 0.1).astype(np.uint8)
+    if kind == "all_lacking_but_two":
+        valid[:] = 0
+        valid[[17, n - 3]] = 1
+    for desc in (True, False):
+        assert np.array_equal(eng.ope_order(col, valid, desc), expected(col, valid, desc)), (kind, desc)
+        assert np.array_equal(eng.ope_order(col, None, desc), expected(col, np.ones(n, np.uint8), desc)), (kind, desc)
+
+
+def test_resident_opecol_order_dense_with_dead_rows(eng):
+    """dds_opecol_order on a resident column of few distinct keys (the dense-rank path), rows lacking
+    the position and removed sets mixed in."""
+    import ddshe
+    rng = np.random.default_rng(59)
+    n = 200_003
+    ope_map = np.cumsum(rng.integers(1, 1 << 30, size=5000, dtype=np.int64))
+    col = ope_map[rng.integers(0, 5000, size=n)]
+    cls = np.where(rng.random(n) > 0.1, 2, 0).astype(np.uint8)  # 2: holds a Long string, 0: lacks it
+    oc = ddshe.OpeColumn(eng, n)
+    oc.append(col, cls)
+    dead = rng.choice(n, size=n // 9, replace=False)
+    oc.set_live(dead, 0)
+    live = np.ones(n, dtype=bool)
+    live[dead] = False
+    for desc in (True, False):
+        want = expected(col, (cls != 0).astype(np.uint8), desc)
+        want = want[live[want]].astype(np.uint32)
+        assert np.array_equal(oc.order(desc), want), desc
+    oc.close()
+
+
+def test_order_key_bit_path_on_few_keys():
+    """DDSHE_ORDER_DENSE=0 (a fresh process): the same few-key columns through the key-bit passes
+    (LSD for narrow spans, the MSD split for wide ones), so both orderings stay covered."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r'''
+import sys
+import numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[1] + "/dependable-data-storage-csd2017_amd"]
+import ddshe
+from tests.test_gpu_order import expected
+eng = ddshe.Engine(0)
+rng = np.random.default_rng(61)
+n = 300_007
+ope_map = np.cumsum(rng.integers(1, 1 << 40, size=10001, dtype=np.int64)) - (1 << 52)
+for col in (ope_map[rng.integers(1, 10001, size=n)], rng.integers(0, 50, size=n, dtype=np.int64) - 25):
+    valid = (rng.random(n) > 0.1).astype(np.uint8)
+    for desc in (True, False):
+        assert np.array_equal(eng.ope_order(col, valid, desc), expected(col, valid, desc)), desc
+eng.close()
+print("ok")
+'''
+    env = dict(os.environ, DDSHE_ORDER_DENSE="0")
+    pr = subprocess.run([sys.executable, "-c", code, root], env=env, capture_output=True, text=True, timeout=300,
+                        cwd=root)
+    assert pr.returncode == 0 and pr.stdout.strip().endswith("ok"), pr.stderr[-2000:]
