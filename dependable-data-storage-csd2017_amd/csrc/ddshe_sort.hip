@@ -21,10 +21,6 @@
 #include <stdint.h>
 #include <stdlib.h>
 
-#include <algorithm>
-#include <map>
-#include <mutex>
-
 #include "ddshe_launch.hpp"
 
 namespace ddshe {
@@ -659,421 +655,14 @@ __global__ void __launch_bounds__(1024) k_msd_big(const uint64_t* __restrict__ k
   }
 }
 
-// ---- Dense-rank path (OPE columns with few distinct keys) ---------------------------------------
-// OPE columns hold the ciphertexts of few plaintexts (the generator draws them from [0, 10^4),
-// DDSDataGenerator.scala:274), so an ordering is a stable counting sort by the RANK of each row's key
-// among the distinct keys:
-//   k_dr_insert   one pass over the column (one 1024-thread block per CU, looping over tiles): every
-//                 holder's key into a global open-addressing set (2^17 slots, CAS-inserted; the
-//                 inserting thread appends the key to a dense list). Each block first checks an LDS set
-//                 of the keys it has already put there (2^14 slots), so the global set sees each key
-//                 about once per CU instead of once per row;
-//   k_dr_rank     rank of every distinct key = how many distinct keys are smaller (compare-count over
-//                 LDS chunks of the dense list, no sort);
-//   k_dr_assign   second pass over the column (one block per CU): the block loads (fingerprint, rank)
-//                 of every distinct key into an LDS table, then gives each row its final rank R (holders
-//                 by key, rows lacking the position after them for OrderLS / before them for OrderSL) as
-//                 u16 and counts R's low byte per tile. Two distinct keys with equal 32-bit fingerprints
-//                 on one probe path are detected while the table is built; the blocks then look the
-//                 rows up in the global set instead;
-//   two stable 8-bit LSD passes over R (the k_rs_* tile scans; k_dr_scatter moves 2 B of rank + 4 B of
-//   id per row, the last pass only the ids).
-// Rows with equal keys have equal ranks, so input order is kept (the reference's stable sortWith).
-// Tiles are 8192 rows (1024 threads x 8): digit runs of ~32 rows per tile. Per row: 9 B read twice
-// (key + class byte), 2 B rank written, then 2 + 6 + 2 + 6 B read and 6 + 4 B written by the passes
-// (~44 B/row against ~98 B/row for the MSD split over the key bits).
-// More than kDrMaxKeys distinct keys (or a probe run of kDrProbes) sets the overflow word: every later
-// kernel returns at once and the host runs the key-bit path instead.
-constexpr uint32_t kDrMaxKeys = 65534;  // distinct holder keys: ranks 0..D (+1 for the lacking rows) in u16
-constexpr int kDrSlotBits = 17;
-constexpr uint32_t kDrSlots = 1u << kDrSlotBits;
-constexpr int kDrProbes = 64;
-constexpr uint64_t kDrEmpty = ~0ull;   // an empty slot; the key ~0 itself is tracked by a flag
-constexpr int kDrRankChunk = 2048;     // dense keys compared per block of k_dr_rank
-constexpr int kDrBlock = 1024;
-constexpr int kDrWaves = kDrBlock / 64;
-constexpr int kDrItems = 8;
-constexpr size_t kDrTile = (size_t)kDrBlock * kDrItems;
-constexpr int kDrLdsBits = 14;         // LDS sets / tables of k_dr_insert and k_dr_assign
-constexpr uint32_t kDrLds = 1u << kDrLdsBits;
-constexpr uint32_t kDrLdsMaxKeys = kDrLds * 3 / 4;  // k_dr_assign's LDS table up to this many keys
-enum { kDrCtlCount = 0, kDrCtlOverflow = 1, kDrCtlMaxKey = 2 };
-
-__device__ __forceinline__ uint32_t dr_hash(uint64_t u) {
-  return (uint32_t)((u * 0x9E3779B97F4A7C15ull) >> (64 - kDrSlotBits));
-}
-__device__ __forceinline__ uint32_t dr_lhash(uint64_t u) {  // LDS slot (independent bits of the same product)
-  return (uint32_t)((u * 0x9E3779B97F4A7C15ull) >> 20) & (kDrLds - 1);
-}
-__device__ __forceinline__ uint32_t dr_fp(uint64_t u) {  // 32-bit fingerprint, never 0 (0 = empty)
-  const uint32_t f = (uint32_t)(((u ^ (u >> 31)) * 0xBF58476D1CE4E5B9ull) >> 32);
-  return f ? f : 1u;
-}
-// row of item k of a lane: each wave owns a contiguous 512-row sixteenth of the tile
-__device__ __forceinline__ size_t dr_row(size_t tile, int wid, int k, int lane) {
-  return tile * kDrTile + (size_t)wid * (kDrTile / kDrWaves) + (size_t)k * 64 + lane;
-}
-
-__device__ __noinline__ void dr_global_insert(uint64_t u, uint64_t* __restrict__ T, uint64_t* __restrict__ dkeys,
-                                              uint32_t* __restrict__ dslot, uint32_t* __restrict__ ctl) {
-  uint32_t h = dr_hash(u);
-  for (int p = 0; p < kDrProbes; ++p) {
-    // a plain load first; it may be a stale empty line of this XCD's L2, so an empty reading is
-    // settled by the CAS, which answers from the coherent copy at the memory side
-    const uint64_t v = T[h];
-    if (v == u) return;
-    if (v == kDrEmpty) {
-      const uint64_t old = atomicCAS((unsigned long long*)&T[h], (unsigned long long)kDrEmpty, (unsigned long long)u);
-      if (old == kDrEmpty) {
-        const uint32_t idx = atomicAdd(&ctl[kDrCtlCount], 1u);
-        if (idx < kDrMaxKeys) {
-          dkeys[idx] = u;
-          dslot[idx] = h;
-        } else {
-          atomicOr(&ctl[kDrCtlOverflow], 1u);
-        }
-        return;
-      }
-      if (old == u) return;
-    }
-    h = (h + 1) & (kDrSlots - 1);
-  }
-  atomicOr(&ctl[kDrCtlOverflow], 1u);
-}
-
-__global__ void __launch_bounds__(kDrBlock) k_dr_insert(const int64_t* __restrict__ col, const uint8_t* __restrict__ valid,
-                                                        size_t n, int desc, uint64_t* __restrict__ T,
-                                                        uint64_t* __restrict__ dkeys, uint32_t* __restrict__ dslot,
-                                                        uint32_t* __restrict__ ctl) {
-  __shared__ unsigned long long seen[kDrLds];  // keys this block has put in the global set
-  for (uint32_t j = threadIdx.x; j < kDrLds; j += kDrBlock) seen[j] = kDrEmpty;
-  __syncthreads();
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const size_t ntiles = (n + kDrTile - 1) / kDrTile;
-  bool saw_max = false;
-  for (size_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    uint64_t u[kDrItems];
-    uint8_t hold[kDrItems];
-#pragma unroll
-    for (int k = 0; k < kDrItems; ++k) {  // all loads first (index clamped), masked below
-      const size_t i = min(dr_row(tile, wid, k, lane), n - 1);
-      u[k] = rs_ukey((uint64_t)col[i], desc);
-      hold[k] = valid ? valid[i] : 1;
-    }
-#pragma unroll
-    for (int k = 0; k < kDrItems; ++k) {
-      if (dr_row(tile, wid, k, lane) >= n || !hold[k]) continue;
-      if (u[k] == kDrEmpty) {
-        saw_max = true;
-        continue;
-      }
-      uint32_t h = dr_lhash(u[k]);
-      int p = 0;
-      for (; p < 32; ++p) {  // LDS probe: found -> done; empty -> claim it, then the global set
-        const unsigned long long v = seen[h];
-        if (v == u[k]) break;
-        if (v == kDrEmpty) {
-          const unsigned long long old = atomicCAS(&seen[h], (unsigned long long)kDrEmpty, (unsigned long long)u[k]);
-          if (old == kDrEmpty) {
-            dr_global_insert(u[k], T, dkeys, dslot, ctl);
-            break;
-          }
-          if (old == u[k]) break;
-        }
-        h = (h + 1) & (kDrLds - 1);
-      }
-      if (p == 32) dr_global_insert(u[k], T, dkeys, dslot, ctl);  // LDS set crowded: straight to the global one
-    }
-  }
-  if (__any(saw_max) && lane == 0) atomicOr(&ctl[kDrCtlMaxKey], 1u);
-}
-
-// rank[i] += |{ j in chunk : dkeys[j] < dkeys[i] }| (rank zeroed by the caller); grid x over the keys,
-// y over chunks of the dense list; blocks past the distinct count return at once
-__global__ void __launch_bounds__(256) k_dr_rank(const uint64_t* __restrict__ dkeys, const uint32_t* __restrict__ ctl,
-                                                 uint32_t* __restrict__ rank) {
-  __shared__ ulonglong2 sk[kDrRankChunk / 2];
-  if (ctl[kDrCtlOverflow]) return;
-  const uint32_t D = min(ctl[kDrCtlCount], kDrMaxKeys);
-  const uint32_t i0 = blockIdx.x * 256, c0 = blockIdx.y * kDrRankChunk;
-  if (i0 >= D || c0 >= D) return;
-  const uint32_t m = min((uint32_t)kDrRankChunk, D - c0);
-  uint64_t* skw = reinterpret_cast<uint64_t*>(sk);
-  for (uint32_t j = threadIdx.x; j < kDrRankChunk; j += 256) skw[j] = j < m ? dkeys[c0 + j] : kDrEmpty;  // pad: never <
-  __syncthreads();
-  const uint32_t i = i0 + threadIdx.x;
-  const uint64_t my = i < D ? dkeys[i] : 0ull;
-  uint32_t c0s = 0, c1s = 0, c2s = 0, c3s = 0;  // independent sums: 4 LDS reads in flight
-  const uint32_t mp = (m + 3) & ~3u;
-#pragma unroll 4
-  for (uint32_t j = 0; j < mp / 2; j += 2) {  // every lane reads the same 16 B: broadcast
-    const ulonglong2 a = sk[j], b = sk[j + 1];
-    c0s += a.x < my ? 1u : 0u;
-    c1s += a.y < my ? 1u : 0u;
-    c2s += b.x < my ? 1u : 0u;
-    c3s += b.y < my ? 1u : 0u;
-  }
-  const uint32_t c = c0s + c1s + c2s + c3s;
-  if (i < D && c) atomicAdd(&rank[i], c);
-}
-
-// rank per global-set slot (the rows' lookup when k_dr_assign cannot hold the keys in LDS)
-__global__ void __launch_bounds__(256) k_dr_slotrank(const uint32_t* __restrict__ dslot, const uint32_t* __restrict__ rank,
-                                                     const uint32_t* __restrict__ ctl, uint16_t* __restrict__ srank) {
-  if (ctl[kDrCtlOverflow]) return;
-  const uint32_t D = min(ctl[kDrCtlCount], kDrMaxKeys);
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < D; i += gridDim.x * 256) srank[dslot[i]] = (uint16_t)rank[i];
-}
-
-// lanes of the wave with the same digit d (< 512): AND of 9 bit-ballots
-__device__ __forceinline__ uint64_t dr_peers(uint32_t d) {
-  uint64_t peers = ~0ull;
-#pragma unroll
-  for (int b = 0; b < 9; ++b) {
-    const uint64_t bal = __ballot((d >> b) & 1u);
-    peers &= ((d >> b) & 1u) ? bal : ~bal;
-  }
-  return peers;
-}
-
-// per-tile counts of one digit into hist[tile][*] (tile-major, kRsDigits columns, the last one unused);
-// cnt: kRsDigits words of LDS
-__device__ __forceinline__ void dr_tile_hist(const uint32_t (&d)[kDrItems], uint32_t* cnt, size_t tile,
-                                             uint32_t* __restrict__ hist) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  for (int j = threadIdx.x; j < kRsDigits; j += kDrBlock) cnt[j] = 0;
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kDrItems; ++k) {
-    const uint64_t peers = dr_peers(d[k]);
-    if (d[k] != kRsNone && (peers & lt) == 0) atomicAdd(&cnt[d[k]], (uint32_t)__popcll(peers));
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < kRsDigits; j += kDrBlock) hist[tile * kRsDigits + j] = cnt[j];
-}
-
-// final rank of every row (u16) + the tile counts of its low byte; one block per CU over the tiles
-__global__ void __launch_bounds__(kDrBlock) k_dr_assign(const int64_t* __restrict__ col, const uint8_t* __restrict__ valid,
-                                                        size_t n, int desc, const uint64_t* __restrict__ T,
-                                                        const uint64_t* __restrict__ dkeys,
-                                                        const uint32_t* __restrict__ rank,
-                                                        const uint16_t* __restrict__ srank,
-                                                        const uint32_t* __restrict__ ctl, uint16_t* __restrict__ rk,
-                                                        uint32_t* __restrict__ hist) {
-  __shared__ uint32_t tfp[kDrLds];
-  __shared__ uint16_t trk[kDrLds];
-  __shared__ uint32_t cnt[kRsDigits];
-  __shared__ uint32_t clash;
-  if (ctl[kDrCtlOverflow]) return;
-  const uint32_t Dt = min(ctl[kDrCtlCount], kDrMaxKeys);  // keys in the set; the key ~0 ranks after them
-  const uint32_t lack = Dt + (ctl[kDrCtlMaxKey] ? 1u : 0u);
-  // (fingerprint, rank) of every distinct key into the LDS table; equal fingerprints met on a probe
-  // path -> clash: this block (and every other one: the build is the same) looks rows up globally
-  for (uint32_t j = threadIdx.x; j < kDrLds; j += kDrBlock) tfp[j] = 0;
-  if (threadIdx.x == 0) clash = Dt > kDrLdsMaxKeys ? 1u : 0u;
-  __syncthreads();
-  if (!clash) {
-    for (uint32_t q = threadIdx.x; q < Dt; q += kDrBlock) {
-      const uint64_t u = dkeys[q];
-      const uint32_t f = dr_fp(u);
-      uint32_t h = dr_lhash(u);
-      for (;;) {
-        const uint32_t old = atomicCAS(&tfp[h], 0u, f);
-        if (old == 0u) {
-          trk[h] = (uint16_t)rank[q];
-          break;
-        }
-        if (old == f) {
-          clash = 1u;
-          break;
-        }
-        h = (h + 1) & (kDrLds - 1);
-      }
-    }
-    __syncthreads();
-    // a key inserted before a clashing one never walked past it: check that every key's lookup stops
-    // at its own slot
-    if (!clash) {
-      for (uint32_t q = threadIdx.x; q < Dt; q += kDrBlock) {
-        const uint64_t u = dkeys[q];
-        const uint32_t f = dr_fp(u);
-        uint32_t h = dr_lhash(u);
-        while (tfp[h] != f) h = (h + 1) & (kDrLds - 1);
-        if (trk[h] != (uint16_t)rank[q]) clash = 1u;
-      }
-    }
-  }
-  __syncthreads();
-  const bool lds = clash == 0u;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const size_t ntiles = (n + kDrTile - 1) / kDrTile;
-  for (size_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    uint64_t u[kDrItems];
-    uint8_t hold[kDrItems];
-#pragma unroll
-    for (int k = 0; k < kDrItems; ++k) {
-      const size_t i = min(dr_row(tile, wid, k, lane), n - 1);
-      u[k] = rs_ukey((uint64_t)col[i], desc);
-      hold[k] = valid ? valid[i] : 1;
-    }
-    uint32_t d[kDrItems];
-#pragma unroll
-    for (int k = 0; k < kDrItems; ++k) {
-      const size_t i = dr_row(tile, wid, k, lane);
-      uint32_t r = 0;
-      if (hold[k] && i < n) {
-        if (u[k] == kDrEmpty) {
-          r = Dt;
-        } else if (lds) {
-          const uint32_t f = dr_fp(u[k]);
-          uint32_t h = dr_lhash(u[k]);
-          for (int p = 0; p < (int)kDrLds && tfp[h] != f; ++p) h = (h + 1) & (kDrLds - 1);
-          r = trk[h];
-        } else {
-          uint32_t h = dr_hash(u[k]);
-          for (int p = 0; p < kDrProbes && T[h] != u[k]; ++p) h = (h + 1) & (kDrSlots - 1);
-          r = srank[h];
-        }
-      }
-      // OrderLS (desc): holders by rank, then the rows lacking the position; OrderSL: those first
-      const uint32_t R = desc ? (hold[k] ? r : lack) : (hold[k] ? r + 1u : 0u);
-      if (i < n) rk[i] = (uint16_t)R;
-      d[k] = i < n ? (R & 0xFFu) : kRsNone;
-    }
-    dr_tile_hist(d, cnt, tile, hist);
-    __syncthreads();  // cnt is reused by the next tile
-  }
-}
-
-__global__ void __launch_bounds__(kDrBlock) k_dr_hist(const uint16_t* __restrict__ rk, size_t n, int shift,
-                                                      const uint32_t* __restrict__ ctl, uint32_t* __restrict__ hist) {
-  __shared__ uint32_t cnt[kRsDigits];
-  if (ctl[kDrCtlOverflow]) return;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t d[kDrItems];
-#pragma unroll
-  for (int k = 0; k < kDrItems; ++k) d[k] = rk[min(dr_row(blockIdx.x, wid, k, lane), n - 1)];
-#pragma unroll
-  for (int k = 0; k < kDrItems; ++k) d[k] = dr_row(blockIdx.x, wid, k, lane) < n ? (d[k] >> shift) & 0xFFu : kRsNone;
-  dr_tile_hist(d, cnt, blockIdx.x, hist);
-}
-
-// exclusive scan of kRsDigits values v(d) into out[0..kRsDigits] by one wave (5 digits per lane)
-template <class F>
-__device__ __forceinline__ void dr_wave_scan(F v_of, uint32_t* out, int lane) {
-  uint32_t v[5], s = 0;
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    const int d = lane * 5 + q;
-    v[q] = d < kRsDigits ? v_of(d) : 0u;
-    s += v[q];
-  }
-  uint32_t inc = s;
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)inc, off);
-    if (lane >= off) inc += y;
-  }
-  uint32_t run = inc - s;
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    const int d = lane * 5 + q;
-    if (d <= kRsDigits) out[d] = run;
-    run += v[q];
-  }
-}
-
-// One stable LSD pass over the u16 ranks (digit (R >> shift) & 0xFF), as k_rs_scatter: per-wave ranks
-// from bit-ballots, rows staged in LDS in tile-local digit order, written out by consecutive threads.
-// ids == nullptr: identity (first pass); rk_out == nullptr: the ranks are not needed after (last pass)
-__global__ void __launch_bounds__(kDrBlock) k_dr_scatter(const uint16_t* __restrict__ rk, const uint32_t* __restrict__ ids,
-                                                         size_t n, int shift, const uint32_t* __restrict__ hist,
-                                                         const uint32_t* __restrict__ ctot,
-                                                         const uint32_t* __restrict__ dtot,
-                                                         const uint32_t* __restrict__ ctl, uint16_t* __restrict__ rk_out,
-                                                         uint32_t* __restrict__ ids_out) {
-  __shared__ uint32_t cnt[kDrWaves][kRsDigits];
-  __shared__ uint32_t dbase[kRsDigits + 1];
-  __shared__ uint32_t lstart[kRsDigits + 1];
-  __shared__ uint16_t srk[kDrTile];
-  __shared__ uint32_t sid[kDrTile];
-  __shared__ uint16_t sdig[kDrTile];
-  if (ctl[kDrCtlOverflow]) return;
-  for (int j = threadIdx.x; j < kDrWaves * kRsDigits; j += kDrBlock) (&cnt[0][0])[j] = 0;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  if (wid == 0) dr_wave_scan([&](int j) { return dtot[j]; }, dbase, lane);
-  __syncthreads();
-  uint16_t r[kDrItems];
-  uint32_t id[kDrItems], dr[kDrItems];
-#pragma unroll
-  for (int k = 0; k < kDrItems; ++k) {
-    const size_t i = min(dr_row(blockIdx.x, wid, k, lane), n - 1);
-    r[k] = rk[i];
-    id[k] = ids ? ids[i] : (uint32_t)dr_row(blockIdx.x, wid, k, lane);
-  }
-#pragma unroll
-  for (int k = 0; k < kDrItems; ++k) {
-    const uint32_t d = dr_row(blockIdx.x, wid, k, lane) < n ? ((uint32_t)r[k] >> shift) & 0xFFu : kRsNone;
-    const uint64_t peers = dr_peers(d);
-    uint32_t rank = 0;
-    if (d != kRsNone) {
-      const uint32_t before = cnt[wid][d];  // every peer reads before the leader writes (wave order)
-      rank = before + (uint32_t)__popcll(peers & lt);
-      if ((peers & lt) == 0) cnt[wid][d] = before + (uint32_t)__popcll(peers);
-    }
-    dr[k] = d | (rank << 9);
-  }
-  __syncthreads();
-  if (wid == 0)
-    dr_wave_scan([&](int j) {
-      uint32_t t = 0;
-      for (int w = 0; w < kDrWaves; ++w) t += cnt[w][j];
-      return t;
-    }, lstart, lane);
-  __syncthreads();
-  for (int j = threadIdx.x; j < kRsDigits; j += kDrBlock) {
-    uint32_t run = lstart[j];
-    for (int w = 0; w < kDrWaves; ++w) {
-      const uint32_t c = cnt[w][j];
-      cnt[w][j] = run;
-      run += c;
-    }
-    dbase[j] += ctot[(size_t)(blockIdx.x / kScanTiles) * kRsDigits + j] + hist[(size_t)blockIdx.x * kRsDigits + j];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kDrItems; ++k) {
-    const uint32_t d = dr[k] & 511u;
-    if (d == kRsNone) continue;
-    const uint32_t lp = cnt[wid][d] + (dr[k] >> 9);
-    srk[lp] = r[k];
-    sid[lp] = id[k];
-    sdig[lp] = (uint16_t)d;
-  }
-  __syncthreads();
-  const size_t t0 = (size_t)blockIdx.x * kDrTile;
-  const uint32_t rows = (uint32_t)min(kDrTile, n - t0);
-  for (uint32_t q = threadIdx.x; q < rows; q += kDrBlock) {
-    const uint32_t d = sdig[q];
-    const uint32_t dst = dbase[d] + (q - lstart[d]);
-    if (rk_out) rk_out[dst] = srk[q];
-    ids_out[dst] = sid[q];
-  }
-}
-
 size_t rs_blocks(size_t n) { return (n + kRsTile - 1) / kRsTile; }
-static size_t rs_scratch_base(size_t n) {
+size_t rs_scratch_bytes(size_t n) {
   // keys x2 (8 B), ids x1 extra (4 B; the other id buffer is the caller's output), histogram, OR/AND,
   // MSD bucket starts + control words + big-bucket list
-  const size_t b = 2 * n * 8 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 1024 +
-                   (size_t)kRsDigits * ((rs_blocks(n) + kScanTiles - 1) / kScanTiles) * 4 + 256 +
-                   16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows)) + 768 + (4 * (size_t)kMsdBuckets + 8) * 4;
-  return (b + 255) & ~(size_t)255;
+  return 2 * n * 8 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 1024 +
+         (size_t)kRsDigits * ((rs_blocks(n) + kScanTiles - 1) / kScanTiles) * 4 + 256 +
+         16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows)) + 768 + (4 * (size_t)kMsdBuckets + 8) * 4;
 }
-// dense-rank path: the set (8 B per slot), dense keys + their slots, ranks + control words, slot ranks
-constexpr size_t kDrBytes = (size_t)kDrSlots * 8 + 65536 * 8 + 65536 * 4 + (65536 * 4 + 256) + (size_t)kDrSlots * 2;
-size_t rs_scratch_bytes(size_t n) { return rs_scratch_base(n) + kDrBytes; }
 
 // the MSD path pays off from 4 LSD passes on (a span of > 24 bits) and enough rows to fill the buckets
 static bool msd_enabled(size_t n, int sb) {
@@ -1084,85 +673,9 @@ static bool msd_enabled(size_t n, int sb) {
   return mode != 0 && n >= ((size_t)1 << 16) && sb > 24;
 }
 
-// compute units of the current device (the persistent dense-rank passes run one block per CU)
-static int dr_cus() {
-  static std::mutex mu;
-  static std::map<int, int> known;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 256;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = known.find(dev);
-  if (it != known.end()) return it->second;
-  int c = 0;
-  if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
-  known[dev] = c;
-  return c;
-}
-
-// DDSHE_ORDER_DENSE=0 turns the dense-rank path off (A/B)
-static bool dr_enabled(size_t n) {
-  static const int mode = [] {
-    const char* s = getenv("DDSHE_ORDER_DENSE");
-    return s ? atoi(s) : 1;
-  }();
-  return mode != 0 && n >= ((size_t)1 << 16) && n < ((size_t)1 << 31);
-}
-
-// The dense-rank ordering (see k_dr_insert); *done = false when the column has too many distinct keys
-// (nothing written to out_ids that matters: the caller sorts by the key bits instead)
-static hipError_t dr_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
-                           uint32_t* out_ids, hipStream_t st, bool* done) {
-  *done = false;
-  const size_t nb = rs_blocks(n);
-  uint16_t* rka = (uint16_t*)scratch;                  // in the key buffers of the bit path
-  uint16_t* rkb = rka + ((n + 127) & ~(size_t)127);
-  uint32_t* ib = (uint32_t*)((uint64_t*)scratch + 2 * n);
-  uint32_t* hist = (uint32_t*)(((uintptr_t)(ib + n) + 255) & ~(uintptr_t)255);
-  uint32_t* dtot = hist + (size_t)kRsDigits * nb;
-  uint32_t* ctot = (uint32_t*)(((uintptr_t)(dtot + kRsDigits) + 255) & ~(uintptr_t)255);
-  char* dr = (char*)scratch + rs_scratch_base(n);
-  uint64_t* T = (uint64_t*)dr;
-  uint64_t* dkeys = T + kDrSlots;
-  uint32_t* dslot = (uint32_t*)(dkeys + 65536);
-  uint32_t* rank = dslot + 65536;
-  uint32_t* ctl = rank + 65536;  // right after the ranks: one memset clears both
-  uint16_t* srank = (uint16_t*)(ctl + 64);
-  hipError_t e;
-  if ((e = hipMemsetAsync(T, 0xFF, (size_t)kDrSlots * 8, st)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(rank, 0, 65536 * 4 + 256, st)) != hipSuccess) return e;
-  const size_t ntd = (n + kDrTile - 1) / kDrTile, nchd = (ntd + kScanTiles - 1) / kScanTiles;
-  const unsigned gp = (unsigned)std::min<size_t>(ntd, (size_t)dr_cus());  // persistent passes: one block per CU
-  hipLaunchKernelGGL(k_dr_insert, dim3(gp), dim3(kDrBlock), 0, st, col, valid, n, desc, T, dkeys, dslot, ctl);
-  hipLaunchKernelGGL(k_dr_rank, dim3((kDrMaxKeys + 255) / 256, (kDrMaxKeys + kDrRankChunk - 1) / kDrRankChunk), dim3(256),
-                     0, st, dkeys, ctl, rank);
-  hipLaunchKernelGGL(k_dr_slotrank, dim3(256), dim3(256), 0, st, dslot, rank, ctl, srank);
-  hipLaunchKernelGGL(k_dr_assign, dim3(gp), dim3(kDrBlock), 0, st, col, valid, n, desc, T, dkeys, rank, srank, ctl,
-                     rka, hist);
-  hipLaunchKernelGGL(k_rs_scan_tiles, dim3((unsigned)nchd), dim3(kScanThreads), 0, st, hist, ntd, ctot);
-  hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nchd, dtot);
-  hipLaunchKernelGGL(k_dr_scatter, dim3((unsigned)ntd), dim3(kDrBlock), 0, st, rka, nullptr, n, 0, hist, ctot, dtot, ctl,
-                     rkb, ib);
-  hipLaunchKernelGGL(k_dr_hist, dim3((unsigned)ntd), dim3(kDrBlock), 0, st, rkb, n, 8, ctl, hist);
-  hipLaunchKernelGGL(k_rs_scan_tiles, dim3((unsigned)nchd), dim3(kScanThreads), 0, st, hist, ntd, ctot);
-  hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nchd, dtot);
-  hipLaunchKernelGGL(k_dr_scatter, dim3((unsigned)ntd), dim3(kDrBlock), 0, st, rkb, ib, n, 8, hist, ctot, dtot, ctl,
-                     nullptr, out_ids);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  uint32_t ov = 1;
-  if ((e = hipMemcpyAsync(&ov, ctl + kDrCtlOverflow, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-  if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-  *done = ov == 0;
-  return hipSuccess;
-}
-
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
                             uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds) {
   if (n == 0) return hipSuccess;
-  if (dr_enabled(n)) {
-    bool done = false;
-    hipError_t e = dr_order(col, valid, n, desc, scratch, out_ids, st, &done);
-    if (e != hipSuccess || done) return e;
-  }
   const size_t nb = rs_blocks(n);
   uint64_t* ka = (uint64_t*)scratch;
   uint64_t* kb = ka + n;
