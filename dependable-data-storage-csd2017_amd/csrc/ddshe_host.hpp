@@ -250,6 +250,13 @@ struct dds_ctx {
   // where a batch's time goes (dds_pair_timing): leader time per batch (gather, codec, GPU round trip,
   // hand-back), its GPU round trip alone (H2D + k_pairs + D2H + sync), the longest batch
   std::atomic<uint64_t> pair_batch_ns{0}, pair_gpu_ns{0}, pair_max_batch_ns{0}, pair_max_gpu_ns{0};
+  // pairwise batches lease their own workers, at most pair_inflight() of them, made on demand and kept:
+  // once a burst has run, no leader creates a stream or pins a buffer again (a queue dropped and
+  // recreated under load could otherwise have more leaders than that, each making a worker)
+  std::mutex pwmu;
+  std::condition_variable pwcv;
+  std::vector<ddshe::host::Worker*> pair_free;
+  int pair_made = 0;
   // caller output buffers registered with dds_host_register (page-locked): base -> bytes. Results
   // bound for them are DMA'd straight in, with no pinned staging buffer and no second host copy.
   std::mutex regmu;
@@ -347,6 +354,25 @@ inline hipError_t read_sync(Worker* w, hipStream_t st, const void* dsrc, void* d
   return hipSuccess;
 }
 
+// a new worker (stream, events) owned by ctx->workers and not in ctx->idle; the caller's device must be
+// the context's. The HIP calls run outside the context lock, so callers that find an idle worker (and
+// get_mod lookups) do not wait behind a creation
+inline int new_worker(dds_ctx* ctx, Worker** out) {
+  auto nw = std::make_unique<Worker>();
+  if (hipStreamCreateWithFlags(&nw->stream, hipStreamNonBlocking) != hipSuccess) return fail(DDS_E_HIP, "hipStreamCreate");
+  for (auto& e : nw->ev)
+    if (hipEventCreate(&e) != hipSuccess) return fail(DDS_E_HIP, "hipEventCreate");
+  for (auto& e : nw->ev_dec)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(DDS_E_HIP, "hipEventCreate");
+  if (hipEventCreateWithFlags(&nw->ev_peer, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&nw->ev_done, hipEventDisableTiming) != hipSuccess)
+    return fail(DDS_E_HIP, "hipEventCreate");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  *out = nw.get();
+  ctx->workers.push_back(std::move(nw));
+  return DDS_OK;
+}
+
 struct WorkerLease {
   dds_ctx* ctx;
   Worker* w = nullptr;
@@ -365,21 +391,9 @@ struct WorkerLease {
         ctx->idle.pop_back();
       }
     }
-    if (!w) {  // a new worker: its streams and events are created outside the context lock, so callers
-               // that find an idle worker (and get_mod lookups) do not wait behind the creation
-      auto nw = std::make_unique<Worker>();
-      if (hipStreamCreateWithFlags(&nw->stream, hipStreamNonBlocking) != hipSuccess)
-        return fail(DDS_E_HIP, "hipStreamCreate");
-      for (auto& e : nw->ev)
-        if (hipEventCreate(&e) != hipSuccess) return fail(DDS_E_HIP, "hipEventCreate");
-      for (auto& e : nw->ev_dec)
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(DDS_E_HIP, "hipEventCreate");
-      if (hipEventCreateWithFlags(&nw->ev_peer, hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&nw->ev_done, hipEventDisableTiming) != hipSuccess)
-        return fail(DDS_E_HIP, "hipEventCreate");
-      std::lock_guard<std::mutex> lk(ctx->mu);
-      w = nw.get();
-      ctx->workers.push_back(std::move(nw));
+    if (!w) {
+      const int rc = new_worker(ctx, &w);
+      if (rc) return rc;
     }
     st = ctx->ext_stream ? ctx->ext_stream : w->stream;
     return DDS_OK;

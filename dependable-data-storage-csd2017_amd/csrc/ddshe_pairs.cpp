@@ -42,6 +42,47 @@ uint64_t since_ns(std::chrono::steady_clock::time_point t0) {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// a worker of the context's pairwise pool (dds_ctx::pair_free): at most pair_inflight() exist; a leader
+// that finds none free waits for one (a batch takes tens of µs) instead of making another
+struct PairLease {
+  dds_ctx* ctx;
+  Worker* w = nullptr;
+  hipStream_t st = nullptr;
+  int prev_device = -1;
+  explicit PairLease(dds_ctx* c) : ctx(c) {}
+  int acquire() {
+    if (hipGetDevice(&prev_device) != hipSuccess) prev_device = -1;
+    if (prev_device != ctx->device && hipSetDevice(ctx->device) != hipSuccess) return fail(DDS_E_HIP, "hipSetDevice");
+    std::unique_lock<std::mutex> lk(ctx->pwmu);
+    while (ctx->pair_free.empty() && ctx->pair_made >= pair_inflight()) ctx->pwcv.wait(lk);
+    if (!ctx->pair_free.empty()) {
+      w = ctx->pair_free.back();
+      ctx->pair_free.pop_back();
+    } else {
+      ++ctx->pair_made;
+      lk.unlock();
+      const int rc = new_worker(ctx, &w);
+      if (rc) {
+        std::lock_guard<std::mutex> g(ctx->pwmu);
+        --ctx->pair_made;
+        ctx->pwcv.notify_one();
+        w = nullptr;
+        return rc;
+      }
+    }
+    st = ctx->ext_stream ? ctx->ext_stream : w->stream;
+    return DDS_OK;
+  }
+  ~PairLease() {
+    if (w) {
+      std::lock_guard<std::mutex> lk(ctx->pwmu);
+      ctx->pair_free.push_back(w);
+      ctx->pwcv.notify_one();
+    }
+    if (prev_device >= 0 && prev_device != ctx->device) (void)hipSetDevice(prev_device);
+  }
+};
+
 // the batch in the tree (latency) shape from limbs already < M: one workgroup product per pair
 int tail_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& batch) {
   const size_t mb = bn::byte_length(M), n = batch.size();
@@ -51,7 +92,7 @@ int tail_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& ba
   int rc = get_mod(ctx, mbe.data(), mb, &mcp);
   if (rc) return rc;
   ModConsts& mc = *mcp;
-  WorkerLease wl(ctx);
+  PairLease wl(ctx);
   if ((rc = wl.acquire())) return rc;
   Worker* w = wl.w;
   const int S3 = mc.S3;  // one workgroup per pair in the tree shape (k_pairs_sos)
