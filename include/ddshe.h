@@ -121,7 +121,8 @@ int dds_ctx_cache_stats(dds_ctx* ctx, size_t* moduli, size_t* pair_queues);
  * a pinned staging buffer and a second host copy (dds_opecol_search_mask's bitmask by the count kernel
  * itself through the mapping; row-id lists of the searches and orders by one DMA).
  * Registered ranges must not overlap; the buffer must stay allocated until dds_host_unregister (or
- * dds_ctx_destroy, which unregisters every buffer). */
+ * dds_ctx_destroy, which unregisters every buffer). Like any output buffer, one serves one call at a
+ * time (concurrent calls into the same bytes race). */
 int dds_host_register(dds_ctx* ctx, void* ptr, size_t bytes);
 int dds_host_unregister(dds_ctx* ctx, void* ptr);
 /* A reply buffer allocated by the engine: page-locked, mapped into the device and placed by the HIP
