@@ -619,7 +619,7 @@ __device__ __forceinline__ uint32_t ope_thread_mask(const int64_t* __restrict__ 
 // past the buffer's end (the last tile's) are dropped
 __device__ __forceinline__ void ope_store_mask(uint32_t m, uint32_t* __restrict__ masks, uint32_t* __restrict__ counts,
                                                size_t tile, unsigned long long* __restrict__ total = nullptr,
-                                               size_t hlimit = 0) {
+                                               size_t hlimit = 0, int hwide = 0) {
   __shared__ uint8_t nib[kOpeGroups * kOpeBlock];
   __shared__ uint32_t wsum[kOpeBlock / 64];
   const int tid = threadIdx.x;
@@ -634,10 +634,40 @@ __device__ __forceinline__ void ope_store_mask(uint32_t m, uint32_t* __restrict_
 #pragma unroll
   for (int i = 0; i < 8; ++i) word |= (uint32_t)((eight >> (8 * i)) & 0xFu) << (4 * i);
   const size_t wi = tile * kOpeBlock + tid;
-  if (hlimit == 0)
+  if (hlimit == 0) {
     masks[wi] = word;
-  else if (wi < hlimit)
+  } else if (hwide) {
+    // over PCIe: the tile's 1 KiB as wider stores (A/B: hwide 1 = 8-byte system-scope stores by the first
+    // two waves, 2 = 16-byte non-temporal stores by the first wave); the buffer is 16-byte aligned (the
+    // launcher checks), words past its end dropped
+    __shared__ __attribute__((aligned(16))) uint32_t wbuf[kOpeBlock];
+    wbuf[tid] = word;
+    __syncthreads();
+    if (hwide == 1) {
+      if (tid < kOpeBlock / 2) {
+        const size_t w0 = tile * kOpeBlock + 2 * (size_t)tid;
+        const uint64_t v = reinterpret_cast<const uint64_t*>(wbuf)[tid];
+        if (w0 + 1 < hlimit)
+          __hip_atomic_store(reinterpret_cast<uint64_t*>(masks + w0), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else if (w0 < hlimit)
+          __hip_atomic_store(masks + w0, (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    } else if (tid < kOpeBlock / 4) {
+      const size_t w0 = tile * kOpeBlock + 4 * (size_t)tid;
+      const uint4 v = reinterpret_cast<const uint4*>(wbuf)[tid];
+      if (w0 + 3 < hlimit) {
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        const v4u q = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(q, reinterpret_cast<v4u*>(masks + w0));
+      } else {
+        const uint32_t e[4] = {v.x, v.y, v.z, v.w};
+        for (int j = 0; j < 4; ++j)
+          if (w0 + j < hlimit) __hip_atomic_store(masks + w0 + j, e[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  } else if (wi < hlimit) {
     __hip_atomic_store(masks + wi, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   if (tid == 0) {
     uint32_t c = 0;
     for (int w = 0; w < kOpeBlock / 64; ++w) c += wsum[w];
@@ -663,10 +693,11 @@ __global__ void __launch_bounds__(kOpeBlock) k_ope_count(const int64_t* __restri
                                                          const uint8_t* __restrict__ valid, size_t n, int64_t bound,
                                                          int op, uint32_t vmask, uint32_t vbad,
                                                          uint32_t* __restrict__ masks, uint32_t* __restrict__ counts,
-                                                         unsigned long long* __restrict__ total, size_t hlimit) {
+                                                         unsigned long long* __restrict__ total, size_t hlimit,
+                                                         int hwide) {
   const bool vec = ((uintptr_t)col % 16 == 0) && (!HasValid || (uintptr_t)valid % 4 == 0);
   const uint32_t m = ope_thread_mask<HasValid>(col, valid, n, bound, op, blockIdx.x, vec, vmask, vbad);
-  ope_store_mask(m, masks, counts, blockIdx.x, total, hlimit);
+  ope_store_mask(m, masks, counts, blockIdx.x, total, hlimit, hwide);
 }
 
 // SearchEq/NEq front end (ddshe_strscan.hip's position index): same tile layout and masks as
@@ -1377,16 +1408,27 @@ void ope_code(int64_t bound, int op, int64_t* t, int* code) {
 void ope_count(const int64_t* col, const uint8_t* valid, size_t n, int64_t bound, int op, uint32_t* masks,
                uint32_t* counts, hipStream_t st, uint32_t vmask, uint32_t vbad,
                unsigned long long* total = nullptr, size_t hlimit = 0) {
+  // zero-copy mask store width (DDSHE_MASK_STORE, A/B: 16 = 16-byte non-temporal stores by the tile's
+  // first wave (default: 0.0445-0.0457 ms per 10M-row Search route against 0.046-0.055 for one word per
+  // lane on the same box); 8 = 8-byte system-scope stores; 4 = one word per lane, system-scope; plain
+  // 16-byte stores were slower, 0.058 ms: the lines sit in L2 until the kernel's end-of-kernel write-back).
+  // The wider forms need a 16-byte aligned buffer, else one word per lane
+  static const int wide_mode = [] {
+    const char* e = getenv("DDSHE_MASK_STORE");
+    const int v = e ? atoi(e) : 16;
+    return v == 8 ? 1 : v == 16 ? 2 : 0;
+  }();
+  const int hwide = (hlimit && ((uintptr_t)masks & 15) == 0) ? wide_mode : 0;
   const size_t nb = ope_blocks(n);
   int64_t t;
   int code;
   ope_code(bound, op, &t, &code);
   if (valid)
     hipLaunchKernelGGL(k_ope_count<true>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, t, code, vmask,
-                       vbad, masks, counts, total, hlimit);
+                       vbad, masks, counts, total, hlimit, hwide);
   else
     hipLaunchKernelGGL(k_ope_count<false>, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, col, valid, n, t, code, vmask,
-                       vbad, masks, counts, total, hlimit);
+                       vbad, masks, counts, total, hlimit, hwide);
 }
 }  // namespace
 
