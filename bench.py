@@ -864,12 +864,14 @@ class ProductFilterWorkload(_Workload):
         reg_med, reg_ok = mask_route(rbuf)
         self.eng.host_unregister(rbuf)
         zc = os.environ.get("DDSHE_MASK_ZEROCOPY", "1") != "0"
+        native = self.native_search() if self.world == 1 else None
         filt["resident_opecol_search_mask"] = {
             "median_ms": med, "matches": mk_ok and reg_ok, "rows": self.mine,
             "registered_caller_array_ms": reg_med,
             "route_roofline": {"bound": "hbm", "achieved": route_bytes / (med / 1e3) / 1e9, "peak": 8000.0,
                                "unit": "GB/s", "frac": route_bytes / (med / 1e3) / 1e9 / 8000.0,
                                "note": "column bytes / whole call time (host clock), mask read-back included"},
+            "native_call": native,
             "path": "dds_opecol_search_mask into a dds_host_alloc reply buffer (median_ms) and into a "
                     "dds_host_register'ed caller array (registered_caller_array_ms): one k_ope_count launch "
                     "stores the mask words through the buffer's device mapping and the per-tile counts into a "
@@ -880,6 +882,19 @@ class ProductFilterWorkload(_Workload):
                    fold_ms_per_step=self.fold_ms / a.steps, filter_ms_per_step=self.filter_ms / a.steps,
                    homomult_per_s=(self.total - 1) * a.steps / elapsed, matches=counts)
         return out
+
+    def native_search(self):
+        """The same route from C++ (tools/native/search_bench: the call a JNA binding makes, without the
+        Python binding's marshalling) over its own seeded 10M-row OPE column, every reply checked in the
+        child against a host count of the predicate."""
+        exe = os.path.join(ROOT, "tools", "native", "search_bench")
+        if not os.path.exists(exe):
+            return {"skipped": "tools/native/search_bench not built"}
+        import subprocess
+        pr = subprocess.run([exe, str(self.mine)], capture_output=True, text=True, timeout=300)
+        if pr.returncode != 0:
+            return {"error": pr.stderr[-400:]}
+        return json.loads(pr.stdout.strip().splitlines()[-1])
 
     def close(self):
         self.col.close()
