@@ -243,3 +243,25 @@ def test_resident_opecol_order_few_keys_with_dead_rows(eng):
         want = want[live[want]].astype(np.uint32)
         assert np.array_equal(oc.order(desc), want), desc
     oc.close()
+
+
+def test_resident_order_into_engine_allocated_buffer(eng):
+    """dds_opecol_order's permutation DMA'd straight into a dds_host_alloc reply buffer (the form the
+    bench times) equals the one copied through the engine's staging buffer."""
+    import ddshe
+    rng = np.random.default_rng(67)
+    n = 250_003
+    col = rng.integers(-(1 << 45), 1 << 45, size=n, dtype=np.int64)
+    cls = np.where(rng.random(n) > 0.05, 2, 0).astype(np.uint8)
+    oc = ddshe.OpeColumn(eng, n)
+    oc.append(col, cls)
+    buf = eng.host_alloc(n, np.uint32)
+    try:
+        for desc in (True, False):
+            buf[:] = 0xFFFFFFFF
+            got = oc.order(desc, out=buf)
+            assert np.array_equal(got, oc.order(desc)), desc
+            assert np.array_equal(got, expected(col, (cls != 0).astype(np.uint8), desc).astype(np.uint32)), desc
+    finally:
+        eng.host_free(buf)
+        oc.close()
