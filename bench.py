@@ -443,10 +443,21 @@ class SumWorkload(_Workload):
         eng.set_stream(None)  # latency of the engine's own streams (no torch stream sync in the call)
         col.fold()
         gpu, fold_ms, fold_p99 = med(col.fold, 50)
+        # the same call at the C-ABI with its arguments built once (what a JNA binding does per request)
+        import ctypes as C
+        fout = (C.c_uint8 * (col.mb + 4096))()
+        flen = C.c_size_t()
+        fold_c = self.ddshe._lib.dds_col_fold
+
+        def c_fold():
+            st = fold_c(col._h, 0, 10000, fout, len(fout), C.byref(flen))
+            assert st == 0, st
+            return flen.value
+        _, fold_c_ms, fold_c_p99 = med(c_fold, 50)
+        assert int.from_bytes(bytes(fout[: flen.value]), "big") == gpu
         rows = [str(x) for x in col.read(0, 10000)]
         # the C entry point a JNA binding calls with its String[] (marshalling of the Python strings done once,
         # outside the timed call: the JVM hands over its strings as they are)
-        import ctypes as C
         arr = (C.c_char_p * len(rows))(*[r.encode() for r in rows])
         cap = sum(len(r) for r in rows) * 2 + 64
         obuf, olen, modb = C.create_string_buffer(cap), C.c_size_t(), str(nsq1).encode()
@@ -496,7 +507,9 @@ class SumWorkload(_Workload):
         del rng
         eng.set_stream(self.torch.cuda.current_stream().cuda_stream)
         return {"config1_sumall_10k_1024bit": {
-                    "resident_fold_ms": fold_ms, "resident_fold_p99_ms": fold_p99, "decimal_route_ms": dec_ms,
+                    "resident_fold_ms": fold_ms, "resident_fold_p99_ms": fold_p99,
+                    "resident_fold_c_abi_ms": fold_c_ms, "resident_fold_c_abi_p99_ms": fold_c_p99,
+                    "decimal_route_ms": dec_ms,
                     "decimal_route_path": "dds_sum_all_dec (String[] of 10k BigInteger.toString rows -> decimal reply)",
                     "decimal_route_with_python_marshalling_ms": dec_py_ms,
                     "cpu_reference_ms": cpu_ms, "cpu_kind": "OpenSSL BN_mod_mul fold, 1 core (oracle/csrc/bn_baseline.c)",
