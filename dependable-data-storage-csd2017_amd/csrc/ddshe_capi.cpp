@@ -396,14 +396,43 @@ int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const 
     }
   }
   // finalize: the root block writes the result straight into the pinned stage (no copy launch after it)
+  // and then a sequence number the host spins on (the stream's own completion is noticed later by its
+  // next user; DDSHE_FOLD_SPIN=0 or timing: hipStreamSynchronize)
+  static const bool spin_ok = [] {
+    const char* e = getenv("DDSHE_FOLD_SPIN");
+    return !(e && e[0] == '0');
+  }();
+  const bool spin = finalize && spin_ok && !ctx->timing.load();
+  volatile uint32_t* dflag = nullptr;
+  uint32_t seq = 0;
+  if (spin) {
+    dflag = reinterpret_cast<volatile uint32_t*>(w->hstage.p) + kStageDoneWord;
+    if (++w->done_seq == 0) ++w->done_seq;
+    seq = w->done_seq;
+    *dflag = 0u;  // whatever the word held, the root's store is the only way it becomes seq (never 0)
+  }
   HIP_TRY(launch_tree(S3, lt.X, lt.xs, lt.Sin, lt.Win, lt.n, lt.ids, mc.d3, finalize ? dY : nullptr,
-                      nodes, tflags, finalize ? hy + S3 : w->out.as<uint32_t>(), S2, mc.W, st, lt.gs));
+                      nodes, tflags, finalize ? hy + S3 : w->out.as<uint32_t>(), S2, mc.W, st, lt.gs,
+                      const_cast<uint32_t*>(dflag), seq));
   if (!finalize) {
     *part = w->out.as<uint32_t>();
     *Eout = E;
     return DDS_OK;
   }
-  HIP_TRY(hipStreamSynchronize(st));
+  if (spin) {
+    // bounded: past 50 ms (a loaded GPU, a fault) the stream synchronisation decides
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*dflag != seq) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+        HIP_TRY(hipStreamSynchronize(st));
+        break;
+      }
+      __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  } else {
+    HIP_TRY(hipStreamSynchronize(st));
+  }
   account_fold(ctx, w);
   *value = bn::from_rw(hy + S3, S3, mc.W3);
   return DDS_OK;

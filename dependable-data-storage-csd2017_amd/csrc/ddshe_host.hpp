@@ -103,6 +103,7 @@ struct Worker {
   // per-row status bytes, and the event after each slot's last use
   HostBuf hch[2], hoff[2];
   HostBuf hstage;  // fold finalize: Y in, result out (pinned: no staging copies on the latency path)
+  uint32_t done_seq = 0;  // fold finalize: the last sequence number the root stored at kStageDoneWord
   HostBuf hcnt;    // coherent + mapped: the Search bitmask's per-tile match counts, stored by the device
   HostBuf hpair;   // pairwise batches: operands and results, coherent + mapped (k_pairs_sos reads and writes it)
   HostBuf hbig;    // large read-backs (Search ids / match masks, Order permutations) before the caller's copy
@@ -337,6 +338,7 @@ struct PairQueue {
 // pinned staging of a worker (fixed 16 KiB, allocated once: pointers into it stay valid across a call):
 // bytes [0, 64) small readbacks (read_sync), words [16, 4096) the finalize Y and result
 constexpr size_t kStageBytes = 16384, kStageWord0 = 16;
+constexpr size_t kStageDoneWord = kStageBytes / 4 - 1;  // the finalize's completion word (past Y + result)
 inline hipError_t stage_ptr(Worker* w, uint32_t** p) {
   hipError_t e = w->hstage.ensure(kStageBytes);
   *p = e == hipSuccess ? (uint32_t*)w->hstage.p : nullptr;

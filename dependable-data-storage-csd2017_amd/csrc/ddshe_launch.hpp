@@ -66,10 +66,13 @@ bool tail_qp(int S);
 // leaf g is row ids[g] when ids != nullptr) to the canonical result (Y != nullptr: S limbs of W bits,
 // times Y R^-1) or a canonical partial (Sout limbs of Wout bits). consts: N | n' | N | 2N | 3N.
 // nodes: 4 nleaves + 2 rows of S words (nodes + level buffers), flags: 2 nleaves + 2 words (zeroed here).
+// done (nullable; out in host memory): after the root has written out, *done = seq (system scope), so a
+// caller can spin on it instead of synchronising the stream.
 Shape tree_shape(size_t mod_bits);
 hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Win, size_t nleaves, const uint32_t* ids,
                        const uint32_t* consts, const uint32_t* Y, uint32_t* nodes, uint32_t* flags, uint32_t* out,
-                       int Sout, int Wout, hipStream_t st, size_t gstride = 1);
+                       int Sout, int Wout, hipStream_t st, size_t gstride = 1, uint32_t* done = nullptr,
+                       uint32_t seq = 0);
 // out[i] = A[i] * B[i] mod N in the tree shape (S limbs of W bits, row-major, operands < N, canonical
 // results): one workgroup per pair (k_pairs_sos). consts as launch_tree, R2 = R^2 mod N (R = 2^(W S)).
 hipError_t launch_pairs_sos(int S, const uint32_t* A, const uint32_t* B, size_t n, const uint32_t* consts,

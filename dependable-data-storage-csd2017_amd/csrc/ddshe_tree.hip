@@ -269,7 +269,8 @@ __global__ void __launch_bounds__(NT) k_tree(const uint32_t* __restrict__ X, siz
                                                        uint32_t* __restrict__ flags, uint32_t* __restrict__ out, int Sout,
                                                        int Wout, int max_levels, uint32_t* __restrict__ lvl_out,
                                                        int fence_mode, uint64_t* __restrict__ stamps,
-                                                       uint32_t* __restrict__ clear, size_t nclear, int yleaf) {
+                                                       uint32_t* __restrict__ clear, size_t nclear, int yleaf,
+                                                       uint32_t* __restrict__ done, uint32_t seq) {
   using O = Sos<S, W>;
   // the next launch's hand-off counters, zeroed here instead of by a separate memset launch
   for (size_t j = (size_t)blockIdx.x * NT + threadIdx.x; j < nclear; j += (size_t)gridDim.x * NT) clear[j] = 0u;
@@ -417,6 +418,12 @@ __global__ void __launch_bounds__(NT) k_tree(const uint32_t* __restrict__ X, siz
     for (int j = tid; j < S; j += NT) out[j] = sa[j];
   } else {
     for (int j = tid; j < Sout; j += NT) out[j] = repack_limb(sa, S, W, Wout, j);
+  }
+  if (done) {  // out is host memory a caller spins on: every storing thread's writes reach the system first,
+               // then one system-scope release store of the call's sequence number
+    __threadfence_system();
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (stamped) {
     if (threadIdx.x == 0) s_stamps[1] = __builtin_amdgcn_s_memrealtime() | ((uint64_t)sp.k << 56);
@@ -573,7 +580,7 @@ static bool handoff_fits(const void* fn) {
 
 hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Win, size_t nleaves, const uint32_t* ids,
                        const uint32_t* consts, const uint32_t* Y, uint32_t* nodes, uint32_t* flags, uint32_t* out,
-                       int Sout, int Wout, hipStream_t st, size_t gstride) {
+                       int Sout, int Wout, hipStream_t st, size_t gstride, uint32_t* done, uint32_t seq) {
   static const int levels_env = tree_env("DDSHE_TREE_LEVELS", 0), fence = tree_env("DDSHE_TREE_FENCE", 2);
   static const size_t wide = (size_t)tree_env("DDSHE_TREE_WIDE", 256);
   static uint64_t* d_st = nullptr;
@@ -614,13 +621,14 @@ hipError_t launch_tree(int S, const uint32_t* X, size_t xstride, int Sin, int Wi
       DDSHE_TREE_SWITCH(S, hipLaunchKernelGGL((k_tree<S, W, kTreeWideThreads>), dim3((unsigned)blocks),
                                               dim3(kTreeWideThreads), 0, st, X, xstride, gstride, Sin, Win, nleaves,
                                               ids, consts, Y, nodes, flags, out, Sout, Wout, last ? 0 : 1, lvl[flip],
-                                              fence, stamping ? d_st : nullptr, flags, nclear, 0));
+                                              fence, stamping ? d_st : nullptr, flags, nclear, 0, done, seq));
     } else {
       const size_t dyn = handoff ? kOneWgPerCuLds : 0;
       DDSHE_TREE_SWITCH(S, {
         hipLaunchKernelGGL((k_tree<S, W, kTreeThreads>), dim3((unsigned)((nl + 1) / 2)), dim3(kTreeThreads), dyn, st,
                            X, xstride, gstride, Sin, Win, nl, ids, consts, Y, nodes, flags, out, Sout, Wout,
-                           last ? 0 : lv, lvl[flip], fence, stamping ? d_st : nullptr, nullptr, (size_t)0, yleaf);
+                           last ? 0 : lv, lvl[flip], fence, stamping ? d_st : nullptr, nullptr, (size_t)0, yleaf,
+                           done, seq);
       });
     }
     hipError_t e = hipGetLastError();
