@@ -455,6 +455,24 @@ class SumWorkload(_Workload):
             return flen.value
         _, fold_c_ms, fold_c_p99 = med(c_fold, 50)
         assert int.from_bytes(bytes(fout[: flen.value]), "big") == gpu
+
+        def cpu_per_fold(c, count, reps):
+            """host CPU of the calling thread (thread clock) and wall time per dds_col_fold, timing off"""
+            out, ln = (C.c_uint8 * (c.mb + 4096))(), C.c_size_t()
+            assert fold_c(c._h, 0, count, out, len(out), C.byref(ln)) == 0
+            cs, ws = [], []
+            for _ in range(reps):
+                c0, w0 = time.thread_time(), time.perf_counter()
+                assert fold_c(c._h, 0, count, out, len(out), C.byref(ln)) == 0
+                cs.append(time.thread_time() - c0)
+                ws.append(time.perf_counter() - w0)
+            cs.sort()
+            ws.sort()
+            return {"rows": count, "host_cpu_ms": cs[len(cs) // 2] * 1e3, "wall_ms": ws[len(ws) // 2] * 1e3}
+        host_cpu = [cpu_per_fold(col, 10000, 50)]
+        for cnt, reps in ((1_000_000, 10), (10_000_000, 5)):
+            if self.mine >= cnt:
+                host_cpu.append(cpu_per_fold(self.col, cnt, reps))
         rows = [str(x) for x in col.read(0, 10000)]
         # the C entry point a JNA binding calls with its String[] (marshalling of the Python strings done once,
         # outside the timed call: the JVM hands over its strings as they are)
@@ -515,6 +533,11 @@ class SumWorkload(_Workload):
                     "cpu_reference_ms": cpu_ms, "cpu_kind": "OpenSSL BN_mod_mul fold, 1 core (oracle/csrc/bn_baseline.c)",
                     "speedup_resident_vs_cpu": cpu_ms / fold_ms,
                     "matches": gpu == ref and dec == str(ref)},
+                "host_cpu_per_fold": {
+                    "folds": host_cpu,
+                    "how": "time.thread_time of the calling thread around dds_col_fold (timing off): the finalize "
+                           "spins on the root's sequence word up to DDSHE_FOLD_SPIN_ROWS (100k) rows and sleeps on a "
+                           "blocking-sync event above; 10k rows on the config-1 column, 1M / 10M on the headline column"},
                 "pair_sum_route_2048bit": {"median_ms": pair_ms, "p99_ms": pair_p99,
                                            "path": "dds_pair_modmul_dec, one caller (the /Sum route body)",
                                            "matches": pair == str(int(a) * int(b) % k2["nsquare"])},
@@ -679,7 +702,7 @@ def run_extra_configs(main_wl):
     return out
 
 
-# tools/profile_all.sh passes, summarised by tools/pmc_summary.py (newest round first)
+# tools/gpurun/profile_all.sh passes, summarised by tools/pmc_summary.py (newest round first)
 PMC_FILE = next((f for f in ("r04_pmc.json", "r03_pmc.json", "r02_pmc_filter_order.json")
                  if os.path.exists(os.path.join(ROOT, "profiles", f))), "r02_pmc_filter_order.json")
 

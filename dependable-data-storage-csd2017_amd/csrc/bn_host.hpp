@@ -114,12 +114,17 @@ inline uint32_t divmod_small(Limbs& a, uint32_t d) {
   return (uint32_t)rem;
 }
 
-// Knuth algorithm D: returns a mod m (m non-zero).
-inline Limbs mod(const Limbs& a, const Limbs& m) {
-  if (cmp(a, m) < 0) return a;
+// Knuth algorithm D: returns a mod m (m non-zero); the quotient into *quot when given.
+inline Limbs mod(const Limbs& a, const Limbs& m, Limbs* quot = nullptr) {
+  if (cmp(a, m) < 0) {
+    if (quot) quot->clear();
+    return a;
+  }
   if (m.size() == 1) {
     Limbs t = a;
-    return from_u64(divmod_small(t, m[0]));
+    const Limbs r = from_u64(divmod_small(t, m[0]));
+    if (quot) quot->swap(t);
+    return r;
   }
   const int s = __builtin_clz(m.back());
   const size_t n = m.size(), mm = a.size() - n;
@@ -127,6 +132,7 @@ inline Limbs mod(const Limbs& a, const Limbs& m) {
   for (size_t i = n; i-- > 0;) v[i] = (m[i] << s) | (s && i ? (uint32_t)((uint64_t)m[i - 1] >> (32 - s)) : 0);
   u[a.size()] = s ? (uint32_t)((uint64_t)a.back() >> (32 - s)) : 0;
   for (size_t i = a.size(); i-- > 0;) u[i] = (a[i] << s) | (s && i ? (uint32_t)((uint64_t)a[i - 1] >> (32 - s)) : 0);
+  if (quot) quot->assign(mm + 1, 0);
   for (size_t j = mm + 1; j-- > 0;) {
     uint64_t num = ((uint64_t)u[j + n] << 32) | u[j + n - 1];
     uint64_t qhat = num / v[n - 1], rhat = num % v[n - 1];
@@ -154,8 +160,11 @@ inline Limbs mod(const Limbs& a, const Limbs& m) {
         c >>= 32;
       }
       u[j + n] += (uint32_t)c;
+      --qhat;
     }
+    if (quot) (*quot)[j] = (uint32_t)qhat;
   }
+  if (quot) trim(*quot);
   Limbs r(n);
   for (size_t i = 0; i < n; ++i) r[i] = (u[i] >> s) | (s && i + 1 < u.size() ? (uint32_t)((uint64_t)u[i + 1] << (32 - s)) : 0);
   trim(r);
@@ -386,6 +395,111 @@ inline uint32_t mont_n0(uint32_t n_low, int W) {
   uint32_t inv = n_low;  // Newton: inv = inv*(2 - n*inv), 5 iterations for 32 bits
   for (int i = 0; i < 5; ++i) inv *= 2u - n_low * inv;
   return (0u - inv) & ((1u << W) - 1);
+}
+
+// ---- host modular product (the pairwise routes' lone requests) -----------------------------------
+// /Sum and /Mult (DDSRestServer.scala:385,479) are ONE modular product per request: a request with no
+// batch partner queued is served here rather than by a GPU round trip (ddshe_pairs.cpp). 64-bit limbs,
+// base B = 2^64, N of k limbs: the product by column sums (Comba: a 3-word accumulator per column, no
+// carry chain through memory), then Barrett (HAC 14.42) with mu = floor(B^(2k) / N) precomputed per
+// modulus: q = floor(floor(x / B^(k-1)) * mu / B^(k+1)), r = x - q N (mod B^(k+1)), at most two
+// subtractions of N. About 2.5 k^2 multiplies (k = 64 at the committed 4096-bit n^2).
+struct Barrett64 {
+  size_t k = 0;
+  std::vector<uint64_t> n;   // N, k limbs
+  std::vector<uint64_t> mu;  // floor(B^(2k) / N), k + 1 limbs
+};
+
+inline std::vector<uint64_t> to_u64(const Limbs& a, size_t k) {
+  std::vector<uint64_t> r(k, 0);
+  for (size_t i = 0; i < a.size() && i / 2 < k; ++i) r[i / 2] |= (uint64_t)a[i] << (32 * (i & 1));
+  return r;
+}
+
+inline Limbs from_u64v(const uint64_t* a, size_t k) {
+  Limbs r(2 * k);
+  for (size_t i = 0; i < k; ++i) {
+    r[2 * i] = (uint32_t)a[i];
+    r[2 * i + 1] = (uint32_t)(a[i] >> 32);
+  }
+  trim(r);
+  return r;
+}
+
+inline Barrett64 barrett64_make(const Limbs& N) {
+  Barrett64 m;
+  m.k = (bit_length(N) + 63) / 64;
+  m.n = to_u64(N, m.k);
+  Limbs mu;
+  (void)mod(pow2(128 * m.k), N, &mu);
+  m.mu = to_u64(mu, m.k + 1);
+  return m;
+}
+
+// column sums: out[c] = column c of a * b for c in [c0, c1) (out must not alias; c1 <= na + nb). c0 > 0
+// drops the carries of the lower columns (Barrett's truncated product: the quotient estimate is then at
+// most a few units low); c1 < na + nb gives the product mod B^c1.
+inline void mul_u64(const uint64_t* a, size_t na, const uint64_t* b, size_t nb, uint64_t* out, size_t c0 = 0,
+                    size_t c1 = ~(size_t)0) {
+  typedef unsigned __int128 u128;
+  u128 acc = 0;
+  uint64_t top = 0;
+  c1 = std::min(c1, na + nb);
+  for (size_t c = c0; c < c1 && c + 1 < na + nb; ++c) {
+    const size_t i0 = c >= nb ? c - nb + 1 : 0, i1 = std::min(c, na - 1);
+    for (size_t i = i0; i <= i1; ++i) {
+      const u128 p = (u128)a[i] * b[c - i];
+      acc += p;
+      top += acc < p;
+    }
+    out[c] = (uint64_t)acc;
+    acc = (acc >> 64) | ((u128)top << 64);
+    top = 0;
+  }
+  if (c1 == na + nb) out[na + nb - 1] = (uint64_t)acc;
+}
+
+// a * b mod N for a, b < N (reduced operands), as a trimmed value
+inline Limbs barrett64_modmul(const Barrett64& m, const Limbs& a, const Limbs& b) {
+  typedef unsigned __int128 u128;
+  const size_t k = m.k;
+  std::vector<uint64_t> buf(2 * k + 2 * (k + 2) + (2 * k + 2) + (k + 1) + (k + 1) + 2 * (k + 1), 0);
+  uint64_t* x = buf.data();         // 2k: a b
+  uint64_t* q2 = x + 2 * k;         // 2k + 2: q1 mu
+  uint64_t* r2 = q2 + 2 * k + 2;    // 2k + 1: q3 N
+  const std::vector<uint64_t> av = to_u64(a, k), bv = to_u64(b, k);
+  mul_u64(av.data(), k, bv.data(), k, x);
+  // q1 = x / B^(k-1): k + 1 limbs; q3 = q1 mu / B^(k+1) from the columns >= k - 1 only
+  mul_u64(x + k - 1, k + 1, m.mu.data(), k + 1, q2, k - 1);
+  const uint64_t* q3 = q2 + k + 1;  // k + 1 limbs
+  mul_u64(q3, k + 1, m.n.data(), k, r2, 0, k + 1);  // q3 N mod B^(k+1)
+  // r = x - q3 N mod B^(k+1)
+  std::vector<uint64_t> r(k + 1);
+  uint64_t br = 0;
+  for (size_t j = 0; j <= k; ++j) {
+    const u128 d = (u128)x[j] - r2[j] - br;
+    r[j] = (uint64_t)d;
+    br = (uint64_t)(d >> 64) & 1u;
+  }
+  for (int it = 0; it < 8; ++it) {  // r < 5N: Barrett's 2 plus the truncated product's few
+    bool ge = r[k] != 0;
+    if (!ge) {
+      ge = true;
+      for (size_t j = k; j-- > 0;)
+        if (r[j] != m.n[j]) {
+          ge = r[j] > m.n[j];
+          break;
+        }
+    }
+    if (!ge) break;
+    br = 0;
+    for (size_t j = 0; j <= k; ++j) {
+      const u128 d = (u128)r[j] - (j < k ? m.n[j] : 0) - br;
+      r[j] = (uint64_t)d;
+      br = (uint64_t)(d >> 64) & 1u;
+    }
+  }
+  return from_u64v(r.data(), k);
 }
 
 }  // namespace bn

@@ -397,12 +397,16 @@ int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const 
   }
   // finalize: the root block writes the result straight into the pinned stage (no copy launch after it)
   // and then a sequence number the host spins on (the stream's own completion is noticed later by its
-  // next user; DDSHE_FOLD_SPIN=0 or timing: hipStreamSynchronize)
-  static const bool spin_ok = [] {
-    const char* e = getenv("DDSHE_FOLD_SPIN");
-    return !(e && e[0] == '0');
+  // next user). Only short folds spin (DDSHE_FOLD_SPIN_ROWS, default 100k rows: ~0.2 ms of device time
+  // at 2048-bit keys): a long fold's caller sleeps on a blocking-sync event instead of holding a core of
+  // the ForkJoin pool the proxy shares between routes (DDSRestServer.scala:21). Timing on:
+  // hipStreamSynchronize.
+  static const size_t spin_rows = [] {
+    const char* e = getenv("DDSHE_FOLD_SPIN_ROWS");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)100000;
   }();
-  const bool spin = finalize && spin_ok && !ctx->timing.load();
+  const bool timing = ctx->timing.load();
+  const bool spin = finalize && !timing && lv.rows <= spin_rows;
   volatile uint32_t* dflag = nullptr;
   uint32_t seq = 0;
   if (spin) {
@@ -430,6 +434,9 @@ int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const 
       __builtin_ia32_pause();
     }
     std::atomic_thread_fence(std::memory_order_acquire);
+  } else if (!timing) {
+    HIP_TRY(hipEventRecord(w->ev_block, st));
+    HIP_TRY(hipEventSynchronize(w->ev_block));
   } else {
     HIP_TRY(hipStreamSynchronize(st));
   }
@@ -452,6 +459,7 @@ int fold_value_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, co
   Leaves lv;
   int rc = fold_level1(ctx, w, st, mc, X, xstride, count, d_ids, &lv);
   if (rc) return rc;
+  lv.rows = count;
   return reduce_leaves(ctx, w, st, mc, lv, true, value, nullptr, nullptr);
 }
 
@@ -2366,7 +2374,9 @@ int dds_ope_order_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_va
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
     HIP_TRY(w->tab.ensure(rs_scratch_bytes(n)));
-    HIP_TRY(launch_ope_order(d_col, d_valid, n, descending ? 1 : 0, w->tab.p, d_out_idx, wl.st));
+    HIP_TRY(ensure_zeroed(w->rstick, rs_tick_words(n) * 4, wl.st));
+    HIP_TRY(launch_ope_order(d_col, d_valid, n, descending ? 1 : 0, w->tab.p, w->rstick.as<uint32_t>(), d_out_idx,
+                             wl.st));
     HIP_TRY(hipStreamSynchronize(wl.st));
     return DDS_OK;
   } catch (const std::bad_alloc&) {
@@ -2389,8 +2399,9 @@ int dds_ope_order(dds_ctx* ctx, const int64_t* col, const uint8_t* valid, size_t
     HIP_TRY(hipMemcpyAsync(w->in.p, col, n * 8, hipMemcpyHostToDevice, wl.st));
     if (valid) HIP_TRY(hipMemcpyAsync(w->in2.p, valid, n, hipMemcpyHostToDevice, wl.st));
     HIP_TRY(w->tab.ensure(rs_scratch_bytes(n)));
+    HIP_TRY(ensure_zeroed(w->rstick, rs_tick_words(n) * 4, wl.st));
     HIP_TRY(launch_ope_order(w->in.as<int64_t>(), valid ? w->in2.as<uint8_t>() : nullptr, n, descending ? 1 : 0,
-                             w->tab.p, w->out.as<uint32_t>(), wl.st));
+                             w->tab.p, w->rstick.as<uint32_t>(), w->out.as<uint32_t>(), wl.st));
     HIP_TRY(hipMemcpyAsync(out_idx, w->out.p, n * 4, hipMemcpyDeviceToHost, wl.st));
     HIP_TRY(hipStreamSynchronize(wl.st));
     return DDS_OK;

@@ -62,6 +62,15 @@ struct DevBuf {
   }
 };
 
+// a device buffer kept at zero between uses (the kernels that count into it reset it themselves):
+// zeroed on the stream when (re)allocated
+inline hipError_t ensure_zeroed(DevBuf& b, size_t bytes, hipStream_t st) {
+  if (bytes <= b.cap) return hipSuccess;
+  hipError_t e = b.ensure(bytes);
+  if (e == hipSuccess) e = hipMemsetAsync(b.p, 0, b.cap, st);
+  return e;
+}
+
 struct HostBuf {  // pinned staging (truly asynchronous H2D)
   void* p = nullptr;
   size_t cap = 0;
@@ -96,7 +105,9 @@ struct Worker {
   // tiles add into it, it is read, then re-zeroed on the stream after the read); ev_done marks the read
   DevBuf ctr;
   bool ctr_zero = false;
+  DevBuf rstick;  // the OPE sort's scan tickets (ensure_zeroed; left at zero by the sort)
   hipEvent_t ev_done = {};
+  hipEvent_t ev_block = {};  // hipEventBlockingSync: the host sleeps on long folds instead of spinning
   DevBuf crt[7];  // CRT encryption scratch (see encrypt_crt_device)
   hipEvent_t ev[4] = {};
   // decimal codec: double-buffered pinned chunks (chars, offsets), their device copies,
@@ -122,6 +133,7 @@ struct Worker {
       if (e) (void)hipEventDestroy(e);
     if (ev_peer) (void)hipEventDestroy(ev_peer);
     if (ev_done) (void)hipEventDestroy(ev_done);
+    if (ev_block) (void)hipEventDestroy(ev_block);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -251,6 +263,12 @@ struct dds_ctx {
   // where a batch's time goes (dds_pair_timing): leader time per batch (gather, codec, GPU round trip,
   // hand-back), its GPU round trip alone (H2D + k_pairs + D2H + sync), the longest batch
   std::atomic<uint64_t> pair_batch_ns{0}, pair_gpu_ns{0}, pair_max_batch_ns{0}, pair_max_gpu_ns{0};
+  // host CPU of the pairwise route by phase (dds_pair_cpu), thread CPU clock ns: decimal codec, limb
+  // packing of the batches, queue / condition-variable time of the callers, the leaders' wait for the GPU
+  // round trip, the host products (and how many requests they served)
+  std::atomic<uint64_t> pair_cpu_ns[5] = {}, pair_host_calls{0};
+  std::atomic<int> pair_policy{-1};  // dds_pair_set_policy; -1: DDSHE_PAIR_POLICY / the default
+  std::map<ddshe::bn::Limbs, std::shared_ptr<const ddshe::bn::Barrett64>> pair_bar;  // under pmu
   // pairwise batches lease their own workers, at most pair_inflight() of them, made on demand and kept:
   // once a burst has run, no leader creates a stream or pins a buffer again (a queue dropped and
   // recreated under load could otherwise have more leaders than that, each making a worker)
@@ -333,6 +351,7 @@ struct PairQueue {
   std::mutex mu;
   std::vector<PairReq*> pending;
   int inflight = 0;
+  int host_busy = 0;  // lone requests being served by the host product (policy DDS_PAIR_LONE)
 };
 
 // pinned staging of a worker (fixed 16 KiB, allocated once: pointers into it stay valid across a call):
@@ -367,7 +386,8 @@ inline int new_worker(dds_ctx* ctx, Worker** out) {
   for (auto& e : nw->ev_dec)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(DDS_E_HIP, "hipEventCreate");
   if (hipEventCreateWithFlags(&nw->ev_peer, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&nw->ev_done, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&nw->ev_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&nw->ev_block, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess)
     return fail(DDS_E_HIP, "hipEventCreate");
   std::lock_guard<std::mutex> lk(ctx->mu);
   *out = nw.get();
@@ -545,6 +565,7 @@ struct Leaves {
   int64_t E;
   const uint32_t* ids;
   size_t gs = 1;
+  size_t rows = 0;  // rows folded into these leaves (finalize: how the host waits for the root)
 };
 int fold_level1(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
                 size_t count, const uint32_t* d_ids, Leaves* lv);

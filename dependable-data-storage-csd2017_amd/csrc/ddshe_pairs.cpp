@@ -12,8 +12,13 @@
 // one D2H, one synchronisation); larger ones take the batched dds_modmul_pairs path. A queue lives
 // while it has work: the last caller out of an idle queue drops it, so moduli sent once by clients
 // leave nothing behind.
+// Policy (dds_pair_set_policy): DDS_PAIR_GPU queues every request; DDS_PAIR_LONE serves a request that
+// finds its modulus' queue empty, no batch in flight and no other host product running with the
+// engine's host product (bn::barrett64_modmul: one 4096-bit product costs less host CPU than a GPU
+// round trip's wait), the others queue; DDS_PAIR_HOST serves every request that way.
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <chrono>
 #include <condition_variable>
@@ -40,6 +45,46 @@ void atomic_max(std::atomic<uint64_t>& m, uint64_t v) {
 
 uint64_t since_ns(std::chrono::steady_clock::time_point t0) {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// thread CPU clock (dds_pair_cpu's phases)
+uint64_t cpu_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+enum { kCpuCodec = 0, kCpuPack = 1, kCpuQueue = 2, kCpuWait = 3, kCpuHost = 4 };
+
+int pair_policy(dds_ctx* ctx) {
+  const int p = ctx->pair_policy.load(std::memory_order_relaxed);
+  if (p >= 0) return p;
+  static const int dflt = [] {
+    const char* e = getenv("DDSHE_PAIR_POLICY");
+    return e ? atoi(e) : DDS_PAIR_LONE;
+  }();
+  return dflt;
+}
+
+// the host product's constants of M (built once per context and modulus; a few dozen moduli at most
+// are kept: a client that sends a new modulus per request rebuilds them)
+std::shared_ptr<const bn::Barrett64> barrett_of(dds_ctx* ctx, const bn::Limbs& M) {
+  {
+    std::lock_guard<std::mutex> lk(ctx->pmu);
+    auto it = ctx->pair_bar.find(M);
+    if (it != ctx->pair_bar.end()) return it->second;
+  }
+  auto b = std::make_shared<const bn::Barrett64>(bn::barrett64_make(M));
+  std::lock_guard<std::mutex> lk(ctx->pmu);
+  if (ctx->pair_bar.size() >= 64) ctx->pair_bar.clear();
+  ctx->pair_bar.emplace(M, b);
+  return b;
+}
+
+void host_product(dds_ctx* ctx, const bn::Barrett64& bar, PairReq* req) {
+  const uint64_t c0 = cpu_ns();
+  req->r = bn::barrett64_modmul(bar, req->a, req->b);
+  ctx->pair_cpu_ns[kCpuHost].fetch_add(cpu_ns() - c0);
+  ctx->pair_host_calls.fetch_add(1);
 }
 
 // a worker of the context's pairwise pool (dds_ctx::pair_free): at most pair_inflight() exist; a leader
@@ -112,11 +157,13 @@ int tail_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& ba
   const size_t cap_bytes = 3 * (size_t)S3 * std::max(n, kTailPairs) * 4;
   HIP_TRY(hb.ensure(cap_bytes));
   uint32_t* h = (uint32_t*)hb.p;
+  uint64_t c0 = cpu_ns();
   for (size_t i = 0; i < n; ++i) {
     const std::vector<uint32_t> ra = bn::to_rw(batch[i]->a, S3, mc.W3), rb = bn::to_rw(batch[i]->b, S3, mc.W3);
     std::copy(ra.begin(), ra.end(), h + i * S3);
     std::copy(rb.begin(), rb.end(), h + words + i * S3);
   }
+  ctx->pair_cpu_ns[kCpuPack].fetch_add(cpu_ns() - c0);
   const auto g0 = std::chrono::steady_clock::now();
   if (zc) {
     uint32_t* d = (uint32_t*)hb.dptr;
@@ -128,11 +175,15 @@ int tail_batch(dds_ctx* ctx, const bn::Limbs& M, const std::vector<PairReq*>& ba
     HIP_TRY(launch_pairs_sos(S3, d, d + words, n, mc.d3, mc.d3 + 5 * (size_t)S3, d + 2 * words, wl.st));
     HIP_TRY(hipMemcpyAsync(h + 2 * words, d + 2 * words, words * 4, hipMemcpyDeviceToHost, wl.st));
   }
+  c0 = cpu_ns();
   HIP_TRY(hipStreamSynchronize(wl.st));
+  const uint64_t c1 = cpu_ns();
+  ctx->pair_cpu_ns[kCpuWait].fetch_add(c1 - c0);
   const uint64_t gns = since_ns(g0);
   ctx->pair_gpu_ns.fetch_add(gns);
   atomic_max(ctx->pair_max_gpu_ns, gns);
   for (size_t i = 0; i < n; ++i) batch[i]->r = bn::from_rw(h + 2 * words + i * S3, S3, mc.W3);
+  ctx->pair_cpu_ns[kCpuPack].fetch_add(cpu_ns() - c1);
   return DDS_OK;
 }
 
@@ -180,7 +231,15 @@ int pair_spin_us() {
   return us;
 }
 
-int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req) {
+int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req,
+                     const std::shared_ptr<const bn::Barrett64>& bar) {
+  const int policy = pair_policy(ctx);
+  if (policy == DDS_PAIR_HOST) {
+    host_product(ctx, *bar, req);
+    return DDS_OK;
+  }
+  const uint64_t c_in = cpu_ns();
+  uint64_t c_batch = 0;  // CPU of the batches this caller led (counted in their own phases)
   std::shared_ptr<PairQueue> q;
   {
     std::lock_guard<std::mutex> lk(ctx->pmu);
@@ -189,7 +248,17 @@ int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req) {
     q = slot;
   }
   std::unique_lock<std::mutex> lk(q->mu);
-  q->pending.push_back(req);
+  if (policy == DDS_PAIR_LONE && q->pending.empty() && q->inflight == 0 && q->host_busy == 0) {
+    ++q->host_busy;  // lone: the host product, while later callers queue for a GPU batch
+    lk.unlock();
+    host_product(ctx, *bar, req);
+    lk.lock();
+    --q->host_busy;
+    if (!q->pending.empty() && q->pending.front()->sleeping) q->pending.front()->cv.notify_one();  // a leader
+    req->done.store(true, std::memory_order_release);
+  } else {
+    q->pending.push_back(req);
+  }
   while (!req->done.load(std::memory_order_acquire)) {
     if (req->taken) {
       // in another leader's batch: spin briefly without the lock (a batch takes tens of µs), then sleep
@@ -216,11 +285,13 @@ int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req) {
     batch.swap(q->pending);
     for (PairReq* r : batch) r->taken = true;
     lk.unlock();
+    const uint64_t b0 = cpu_ns();
     try {
       run_batch(ctx, M, batch);
     } catch (...) {
       for (PairReq* r : batch) r->rc = DDS_E_NOMEM;
     }
+    c_batch += cpu_ns() - b0;
     lk.lock();
     --q->inflight;
     if (!q->pending.empty() && q->pending.front()->sleeping) q->pending.front()->cv.notify_one();  // next leader
@@ -234,16 +305,18 @@ int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req) {
     }
     req->done.store(true, std::memory_order_release);
   }
-  const bool idle = q->inflight == 0 && q->pending.empty();
+  const bool idle = q->inflight == 0 && q->pending.empty() && q->host_busy == 0;
   lk.unlock();
   if (idle) {  // drop the idle queue (a caller that still holds it just runs as its own leader)
     std::lock_guard<std::mutex> g(ctx->pmu);
     auto it = ctx->pair_queues.find(M);
     if (it != ctx->pair_queues.end() && it->second == q) {
       std::lock_guard<std::mutex> ql(q->mu);
-      if (q->inflight == 0 && q->pending.empty()) ctx->pair_queues.erase(it);
+      if (q->inflight == 0 && q->pending.empty() && q->host_busy == 0) ctx->pair_queues.erase(it);
     }
   }
+  const uint64_t c_all = cpu_ns() - c_in;
+  ctx->pair_cpu_ns[kCpuQueue].fetch_add(c_all > c_batch ? c_all - c_batch : 0);
   return req->rc;
 }
 
@@ -256,8 +329,10 @@ int dds_pair_modmul_dec(dds_ctx* ctx, const char* a_dec, const char* b_dec, cons
   try {
     if (!ctx || !a_dec || !b_dec || !mod_dec) return fail(DDS_E_ARG, "bad arguments");
     ctx->pair_calls.fetch_add(1);
+    uint64_t c0 = cpu_ns();
     // operands first, then the modulus (:380-383): any of them malformed -> NumberFormatException -> 500
     bn::Limbs a, b, M;
+    std::shared_ptr<const bn::Barrett64> bar;
     bool an = false, bneg = false, mneg = false;
     if (!bn::from_dec(a_dec, strlen(a_dec), a, &an)) return fail(DDS_E_FORMAT, "NumberFormatException: operand1");
     if (!bn::from_dec(b_dec, strlen(b_dec), b, &bneg)) return fail(DDS_E_FORMAT, "NumberFormatException: operand2");
@@ -265,14 +340,22 @@ int dds_pair_modmul_dec(dds_ctx* ctx, const char* a_dec, const char* b_dec, cons
       thread_local std::string last_text;
       thread_local bn::Limbs last_mod;
       thread_local bool last_neg = false, last_ok = false;
+      thread_local std::shared_ptr<const bn::Barrett64> last_bar;
+      thread_local const dds_ctx* last_ctx = nullptr;
       const size_t ml = strlen(mod_dec);
       if (!(last_text.size() == ml && memcmp(last_text.data(), mod_dec, ml) == 0)) {
         last_text.assign(mod_dec, ml);
         last_ok = bn::from_dec(mod_dec, ml, last_mod, &last_neg);
+        last_bar.reset();
       }
       if (!last_ok) return fail(DDS_E_FORMAT, "NumberFormatException: modulus");
       M = last_mod;
       mneg = last_neg;
+      if (!mneg && !M.empty() && (M[0] & 1u) && bn::bit_length(M) >= 2) {
+        if (!last_bar || last_ctx != ctx) last_bar = barrett_of(ctx, M);
+        last_ctx = ctx;
+        bar = last_bar;
+      }
     }
     if (mneg || M.empty()) return fail(DDS_E_FORMAT, "ArithmeticException: BigInteger: modulus not positive");
     if (!(M[0] & 1u) || bn::bit_length(M) < 2) {  // even modulus or 1: the fold's CRT path, uncoalesced
@@ -283,17 +366,20 @@ int dds_pair_modmul_dec(dds_ctx* ctx, const char* a_dec, const char* b_dec, cons
     if (bn::cmp(a, M) >= 0) a = bn::mod(a, M);
     if (bn::cmp(b, M) >= 0) b = bn::mod(b, M);
     PairReq req;
-    req.a = a;
-    req.b = b;
-    int rc = modmul_coalesced(ctx, M, &req);
+    req.a = std::move(a);
+    req.b = std::move(b);
+    ctx->pair_cpu_ns[kCpuCodec].fetch_add(cpu_ns() - c0);
+    int rc = modmul_coalesced(ctx, M, &req, bar);
     if (rc) return rc;
-    bn::Limbs r = req.r;
+    c0 = cpu_ns();
+    bn::Limbs r = std::move(req.r);
     bn::trim(r);
     if ((an != bneg) && !r.empty()) r = bn::sub(M, r);
     const std::string s = bn::to_dec(r);
     if (out_len) *out_len = s.size();
     if (!out || out_cap < s.size() + 1) return fail(DDS_E_BUFSIZE, "output buffer too small");
     memcpy(out, s.c_str(), s.size() + 1);
+    ctx->pair_cpu_ns[kCpuCodec].fetch_add(cpu_ns() - c0);
     return DDS_OK;
   } catch (const std::bad_alloc&) {
     return fail(DDS_E_NOMEM, "host allocation");
@@ -314,6 +400,23 @@ int dds_pair_timing(dds_ctx* ctx, uint64_t* batch_ns, uint64_t* gpu_ns, uint64_t
   if (gpu_ns) *gpu_ns = ctx->pair_gpu_ns.load();
   if (max_batch_ns) *max_batch_ns = ctx->pair_max_batch_ns.exchange(0);  // window: since the last read
   if (max_gpu_ns) *max_gpu_ns = ctx->pair_max_gpu_ns.exchange(0);
+  return DDS_OK;
+}
+
+int dds_pair_set_policy(dds_ctx* ctx, int policy, int* previous) {
+  if (!ctx || policy > DDS_PAIR_HOST) return fail(DDS_E_ARG, "bad arguments");
+  if (previous) *previous = pair_policy(ctx);
+  if (policy >= 0) ctx->pair_policy.store(policy);
+  return DDS_OK;
+}
+
+int dds_pair_cpu(dds_ctx* ctx, uint64_t* codec_ns, uint64_t* pack_ns, uint64_t* queue_ns, uint64_t* wait_ns,
+                 uint64_t* host_ns, uint64_t* host_calls) {
+  if (!ctx) return fail(DDS_E_ARG, "bad arguments");
+  uint64_t* outs[5] = {codec_ns, pack_ns, queue_ns, wait_ns, host_ns};
+  for (int i = 0; i < 5; ++i)
+    if (outs[i]) *outs[i] = ctx->pair_cpu_ns[i].load();
+  if (host_calls) *host_calls = ctx->pair_host_calls.load();
   return DDS_OK;
 }
 

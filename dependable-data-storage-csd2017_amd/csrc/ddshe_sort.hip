@@ -26,12 +26,14 @@
 namespace ddshe {
 
 constexpr int kRsBlock = 256;
-constexpr int kRsWaves = kRsBlock / 64;
 constexpr int kRsItems = 8;                       // rows per lane
 constexpr size_t kRsTile = (size_t)kRsBlock * kRsItems;
 constexpr int kRsDigits = 257;                    // 256 + the validity bucket of the last pass
 constexpr uint32_t kRsNone = 511;                 // digit of a lane past the end (never counted)
 constexpr uint64_t kSign = 0x8000000000000000ull;
+constexpr int kScanTiles = 64;                    // tiles per chunk of the scan over tiles (k_rs_hist)
+constexpr int kMsdBits = 16;                      // MSD split: buckets of the top 16 bits of the key span
+constexpr uint32_t kMsdBuckets = 1u << kMsdBits;
 
 // Sort key of a holder: its value in unsigned order (descending: complemented), minus the smallest
 // such key (kmin). Rows lacking the position get key 0 so that earlier passes keep them in input
@@ -41,9 +43,13 @@ __device__ __forceinline__ uint64_t rs_ukey(uint64_t raw, int desc) {
   const uint64_t u = raw ^ kSign;  // signed order -> unsigned order
   return desc ? ~u : u;
 }
+// kbit (span < 2^56): a row lacking the position gets key 2^63 instead of 0. Its digit is still 0 in
+// every pass but the last (whose shift is <= 48), and the last pass reads its validity from that bit: no
+// id (vbit) or valid[] read there.
+constexpr uint64_t kRsNoHold = 1ull << 63;
 __device__ __forceinline__ uint64_t rs_key_of(uint64_t raw, const uint8_t* __restrict__ valid, size_t i, int desc,
-                                              uint64_t kmin) {
-  return (valid && !valid[i]) ? 0ull : rs_ukey(raw, desc) - kmin;
+                                              uint64_t kmin, bool kbit) {
+  return (valid && !valid[i]) ? (kbit ? kRsNoHold : 0ull) : rs_ukey(raw, desc) - kmin;
 }
 
 // min / max of the holders' keys (per block, then k_rs_red): only the bytes of max - min are sorted.
@@ -162,44 +168,69 @@ __device__ __forceinline__ uint32_t rs_load_id(const uint32_t* __restrict__ ids,
 }
 
 __device__ __forceinline__ uint32_t rs_digit(uint64_t k, uint32_t id, const uint8_t* __restrict__ valid, int shift,
-                                             bool last, int desc, bool vbit) {
+                                             bool last, int desc, bool vbit, bool kbit) {
   uint32_t d = (uint32_t)(k >> shift) & 0xFFu;
   if (last && valid) {
-    const bool v = vbit ? (id & kRsLack) == 0 : valid[id] != 0;
+    const bool v = kbit ? (k >> 63) == 0 : vbit ? (id & kRsLack) == 0 : valid[id] != 0;
     d = desc ? (v ? d : 256u) : (v ? d + 1u : 0u);
   }
   return d;
 }
 
-// row of item k of a lane: each wave owns a contiguous quarter of the tile
-__device__ __forceinline__ size_t rs_row(size_t tile, int wid, int k, int lane) {
-  return tile * kRsTile + (size_t)wid * (kRsTile / kRsWaves) + (size_t)k * 64 + lane;
+// Tile of a block. xcd != 0: blocks are dealt round-robin over the 8 XCDs (observed; speed only, never
+// correctness), so block b works on tile (b % 8)-th eighth + b / 8: each XCD walks a contiguous range of
+// tiles and neighbouring tiles' writes to one digit run meet in the same L2.
+__device__ __forceinline__ size_t rs_tile(size_t nblocks, int xcd) {
+  const size_t b = blockIdx.x;
+  if (!xcd) return b;
+  const size_t q = nblocks >> 3, r = nblocks & 7, x = b & 7;
+  return x * q + (x < r ? x : r) + (b >> 3);
 }
 
-__global__ void __launch_bounds__(kRsBlock) k_rs_hist(const uint64_t* __restrict__ keys,
+// Tile geometry of a pass: BLK threads x kRsItems rows. Bigger tiles give longer digit runs in the
+// scatter's write-out (2048-row tiles: ~8 rows per digit on random digits, the first pass's case).
+template <int BLK>
+struct RsTile {
+  static constexpr int kWaves = BLK / 64;
+  static constexpr size_t kRows = (size_t)BLK * kRsItems;
+  // row of item k of a lane: each wave owns a contiguous 1/kWaves of the tile
+  static __device__ __forceinline__ size_t row(size_t tile, int wid, int k, int lane) {
+    return tile * kRows + (size_t)wid * (kRows / kWaves) + (size_t)k * 64 + lane;
+  }
+};
+
+template <int BLK>
+__global__ void __launch_bounds__(BLK) k_rs_hist(const uint64_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ ids,
                                                       const uint8_t* __restrict__ valid, size_t n, int shift,
-                                                      bool last, int desc, bool vbit, uint64_t kmin,
-                                                      uint32_t* __restrict__ hist, size_t nblocks) {
+                                                      bool last, int desc, bool vbit, bool kbit, uint64_t kmin,
+                                                      uint32_t* __restrict__ hist, size_t nblocks,
+                                                      uint32_t* __restrict__ clr, uint32_t nclr) {
+  using T = RsTile<BLK>;
   __shared__ uint32_t cnt[kRsDigits];
-  for (int d = threadIdx.x; d < kRsDigits; d += kRsBlock) cnt[d] = 0;
+  for (int d = threadIdx.x; d < kRsDigits; d += BLK) cnt[d] = 0;
+  if (clr) {  // first pass of the MSD path: the bucket tables of the last scatter start at their identities
+    const size_t g = (size_t)blockIdx.x * BLK + threadIdx.x;
+    for (size_t g2 = g; g2 < nclr; g2 += (size_t)gridDim.x * BLK)
+      clr[g2] = g2 < 3 * (size_t)kMsdBuckets ? ~0u : 0u;  // first[], kmin[] (2 words each): ~0; the rest 0
+  }
   __syncthreads();
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t lt = (1ull << lane) - 1ull;
-  const bool need_id = last && valid;
+  const bool need_id = last && valid && !kbit;
   // all loads first (independent, in flight together), then the LDS counting
   uint64_t key[kRsItems];
   uint32_t id[kRsItems];
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {  // unconditional loads (index clamped), masked below
-    const size_t i = min(rs_row(blockIdx.x, wid, k, lane), n - 1);
-    key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc, kmin);  // first pass: keys = the column
+    const size_t i = min(T::row(blockIdx.x, wid, k, lane), n - 1);
+    key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc, kmin, kbit);  // first pass: keys = the column
     id[k] = need_id ? rs_load_id(ids, i, valid, vbit) : 0u;
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
-    const size_t i = rs_row(blockIdx.x, wid, k, lane);
-    const uint32_t d = i < n ? rs_digit(key[k], id[k], valid, shift, last, desc, vbit) : kRsNone;
+    const size_t i = T::row(blockIdx.x, wid, k, lane);
+    const uint32_t d = i < n ? rs_digit(key[k], id[k], valid, shift, last, desc, vbit, kbit) : kRsNone;
     // one LDS atomic per distinct digit of the wave (OPE columns repeat digits a lot; measured
     // faster than per-wave histograms with one atomic per row)
     uint64_t peers = ~0ull;
@@ -211,74 +242,102 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_hist(const uint64_t* __restrict
     if (d != kRsNone && (peers & lt) == 0) atomicAdd(&cnt[d], (uint32_t)__popcll(peers));
   }
   __syncthreads();
-  for (int d = threadIdx.x; d < kRsDigits; d += kRsBlock) hist[(size_t)blockIdx.x * kRsDigits + d] = cnt[d];  // 1 KiB, coalesced
+  for (int d = threadIdx.x; d < kRsDigits; d += BLK) hist[(size_t)blockIdx.x * kRsDigits + d] = cnt[d];  // 1 KiB, coalesced
 }
 
-// Tile counts are tile-major (hist[tile][digit]: each histogram block writes 1 KiB in one go; the
-// digit-major layout cost one 32-byte sector per 4-byte count, 8x the bytes, PMC round 2). The
-// exclusive scan over tiles per digit then runs in two steps:
-//   k_rs_scan_tiles: one block per chunk of kScanTiles tiles, one thread per digit: the chunk's
-//     counts of that digit (coalesced rows across the digit threads) are replaced in place by their
-//     exclusive prefix within the chunk, and the chunk total goes to ctot[chunk][digit];
-//   k_rs_scan_chunks: one block, one thread per digit: exclusive prefix of the chunk totals in place,
-//     digit total -> dtot[digit].
-// A tile's offset for digit d is then dbase[d] + ctot[chunk][d] + hist[tile][d] (k_rs_scatter).
-constexpr int kScanTiles = 64;
+// Exclusive scan over tiles per digit: one block per chunk of kScanTiles tiles, one thread per digit
+// (coalesced rows across the digit threads): the chunk's counts are replaced in place by their
+// exclusive prefix within the chunk and the chunk total goes out write-through (sc1) to
+// ctot[chunk][digit]; the last chunk to finish (ticket) then replaces the chunk totals by their
+// exclusive prefix and stores the digit totals to dtot (k_tree's in-kernel hand-off: sc1 stores ->
+// s_waitcnt vmcnt(0) -> barrier -> agent atomic; sc1 loads after the ticket) and puts the ticket back
+// to zero. A tile's offset for digit d is then dbase[d] + ctot[chunk][d] + hist[tile][d].
+// (Round 4 ran the chunk-total scan as a second launch, 6 us per pass; doing both scans inside the
+// histogram kernel's last blocks instead made it 2x slower: every block then waits for its
+// write-through row before its ticket.)
 constexpr int kScanThreads = 320;  // >= kRsDigits
-__global__ void __launch_bounds__(kScanThreads) k_rs_scan_tiles(uint32_t* __restrict__ hist, size_t nblocks,
-                                                                uint32_t* __restrict__ ctot) {
+__global__ void __launch_bounds__(kScanThreads) k_rs_scan(uint32_t* __restrict__ hist, size_t nblocks,
+                                                          uint32_t* __restrict__ ctot, uint32_t* __restrict__ dtot,
+                                                          uint32_t* __restrict__ tick) {
+  __shared__ int s_go;
   const int d = threadIdx.x;
-  if (d >= kRsDigits) return;
-  const size_t t0 = (size_t)blockIdx.x * kScanTiles;
-  uint32_t v[kScanTiles];
+  const size_t t0 = (size_t)blockIdx.x * kScanTiles, nch = gridDim.x;
+  if (d < kRsDigits) {
+    uint32_t v[kScanTiles];
 #pragma unroll
-  for (int r = 0; r < kScanTiles; ++r) v[r] = t0 + r < nblocks ? hist[(t0 + r) * kRsDigits + d] : 0u;
-  uint32_t run = 0;
+    for (int r = 0; r < kScanTiles; ++r) v[r] = t0 + r < nblocks ? hist[(t0 + r) * kRsDigits + d] : 0u;
+    uint32_t run = 0;
 #pragma unroll
-  for (int r = 0; r < kScanTiles; ++r) {
-    if (t0 + r < nblocks) hist[(t0 + r) * kRsDigits + d] = run;
-    run += v[r];
+    for (int r = 0; r < kScanTiles; ++r) {
+      if (t0 + r < nblocks) hist[(t0 + r) * kRsDigits + d] = run;
+      run += v[r];
+    }
+    __hip_atomic_store(ctot + (size_t)blockIdx.x * kRsDigits + d, run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  ctot[(size_t)blockIdx.x * kRsDigits + d] = run;
-}
-
-__global__ void __launch_bounds__(kScanThreads) k_rs_scan_chunks(uint32_t* __restrict__ ctot, size_t nchunks,
-                                                                 uint32_t* __restrict__ dtot) {
-  const int d = threadIdx.x;
-  if (d >= kRsDigits) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (d == 0) s_go = __hip_atomic_fetch_add(tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nch - 1;
+  __syncthreads();
+  if (!s_go || d >= kRsDigits) return;
   uint32_t run = 0;
-  for (size_t c0 = 0; c0 < nchunks; c0 += 16) {
+  for (size_t c0 = 0; c0 < nch; c0 += 16) {
     uint32_t v[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = c0 + q < nchunks ? ctot[(c0 + q) * kRsDigits + d] : 0u;
+    for (int q = 0; q < 16; ++q)
+      v[q] = c0 + q < nch ? __hip_atomic_load(ctot + (c0 + q) * kRsDigits + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : 0u;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      if (c0 + q < nchunks) ctot[(c0 + q) * kRsDigits + d] = run;
+      if (c0 + q < nch) ctot[(c0 + q) * kRsDigits + d] = run;  // read by the scatter (next launch)
       run += v[q];
     }
   }
   dtot[d] = run;
+  if (d == 0) *tick = 0u;  // every chunk has taken its ticket
 }
+
+// Tile counts are tile-major (hist[tile][digit]: each histogram block writes 1 KiB in one go; the
+// digit-major layout cost one 32-byte sector per 4-byte count, 8x the bytes, PMC round 2); k_rs_scan
+// (above) turns them into per-tile offsets.
 
 // The ranked rows are first placed in tile-local digit order in LDS, then written out by
 // consecutive threads: lanes of a store instruction hit consecutive addresses of a digit run
 // (runs average kRsTile/256 = 16 rows), instead of 64 different buckets per store.
-__global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restrict__ keys,
+// Bucket table of the MSD split, filled by the last LSD pass's scatter (k_rs_scatter with runs.first set):
+// rows of one top-16-bit bucket form one run in each tile's digit run, so per (tile, bucket) run the
+// scatter takes first[b] = min(run start), end[b] = max(run end), kmin/kmax[b] = min/max(run's first key),
+// and stores multi[b] = 1 where two adjacent rows of a run differ. A bucket holds two distinct keys iff
+// multi[b] or kmin[b] != kmax[b]. Layout (one clear): first | kmin (~0) | end | kmax | multi | ctl (0).
+struct MsdRuns {
+  uint32_t* first;
+  unsigned long long* kmin;
+  uint32_t* end;
+  unsigned long long* kmax;
+  uint32_t* multi;
+  int s1;  // bucket = key >> s1
+};
+constexpr uint32_t kMsdTableWords = 7 * kMsdBuckets + 8;
+
+template <int BLK>
+__global__ void __launch_bounds__(BLK) k_rs_scatter(const uint64_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ ids,
                                                          const uint8_t* __restrict__ valid, size_t n, int shift,
-                                                         int desc, bool vbit, bool last, uint64_t kmin,
+                                                         int desc, bool vbit, bool kbit, bool last, uint64_t kmin,
                                                          const uint32_t* __restrict__ hist,
                                                          const uint32_t* __restrict__ ctot,
                                                          const uint32_t* __restrict__ dtot, size_t nblocks,
                                                          uint64_t* __restrict__ keys_out,
-                                                         uint32_t* __restrict__ ids_out) {
-  __shared__ uint32_t cnt[kRsWaves][kRsDigits];
+                                                         uint32_t* __restrict__ ids_out, int xcd, MsdRuns runs) {
+  const size_t tile = rs_tile(nblocks, xcd);
+  using T = RsTile<BLK>;
+  constexpr int W = T::kWaves;
+  __shared__ uint32_t cnt[W][kRsDigits];
   __shared__ uint32_t dbase[kRsDigits + 1];   // global start of digit d, then of this tile's run of d
   __shared__ uint32_t lstart[kRsDigits + 1];  // tile-local start of digit d
-  __shared__ uint64_t skey[kRsTile];
-  __shared__ uint32_t sid[kRsTile];
-  __shared__ uint16_t sdig[kRsTile];
-  for (int d = threadIdx.x; d < kRsWaves * kRsDigits; d += kRsBlock) (&cnt[0][0])[d] = 0;
+  __shared__ uint64_t skey[T::kRows];
+  __shared__ uint32_t sid[T::kRows];
+  __shared__ uint16_t sdig[T::kRows];
+  for (int d = threadIdx.x; d < W * kRsDigits; d += BLK) (&cnt[0][0])[d] = 0;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t lt = (1ull << lane) - 1ull;
   // exclusive scan of kRsDigits values v(d) into out[] by one wave (5 digits per lane)
@@ -309,14 +368,14 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
   uint32_t id[kRsItems], dr[kRsItems];  // dr = digit | rank << 9
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {  // all loads first, unconditional (index clamped), masked below
-    const size_t i = min(rs_row(blockIdx.x, wid, k, lane), n - 1);
-    key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc, kmin);  // first pass: keys = the column
+    const size_t i = min(T::row(tile, wid, k, lane), n - 1);
+    key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc, kmin, kbit);  // first pass: keys = the column
     id[k] = rs_load_id(ids, i, valid, vbit);  // ids == nullptr: first executed pass, identity
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
-    const size_t i = rs_row(blockIdx.x, wid, k, lane);
-    dr[k] = i < n ? rs_digit(key[k], id[k], valid, shift, last, desc, vbit) : kRsNone;
+    const size_t i = T::row(tile, wid, k, lane);
+    dr[k] = i < n ? rs_digit(key[k], id[k], valid, shift, last, desc, vbit, kbit) : kRsNone;
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
@@ -337,17 +396,25 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
     dr[k] = d | (rank << 9);
   }
   __syncthreads();
-  if (wid == 0) wave_scan([&](int d) { return cnt[0][d] + cnt[1][d] + cnt[2][d] + cnt[3][d]; }, lstart);
+  if (wid == 0)
+    wave_scan(
+        [&](int d) {
+          uint32_t c = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) c += cnt[w][d];
+          return c;
+        },
+        lstart);
   __syncthreads();
   // cnt[w][d] <- tile-local start of wave w's rows of digit d; dbase[d] <- global start of the tile's run
-  for (int d = threadIdx.x; d < kRsDigits; d += kRsBlock) {
+  for (int d = threadIdx.x; d < kRsDigits; d += BLK) {
     uint32_t run = lstart[d];
-    for (int w = 0; w < kRsWaves; ++w) {
+    for (int w = 0; w < W; ++w) {
       const uint32_t c = cnt[w][d];
       cnt[w][d] = run;
       run += c;
     }
-    dbase[d] += ctot[(size_t)(blockIdx.x / kScanTiles) * kRsDigits + d] + hist[(size_t)blockIdx.x * kRsDigits + d];
+    dbase[d] += ctot[(tile / kScanTiles) * kRsDigits + d] + hist[tile * kRsDigits + d];
   }
   __syncthreads();
 #pragma unroll
@@ -355,18 +422,33 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
     const uint32_t d = dr[k] & 511u;
     if (d == kRsNone) continue;
     const uint32_t lp = cnt[wid][d] + (dr[k] >> 9);
-    if (keys_out) skey[lp] = key[k];
+    if (keys_out || runs.first) skey[lp] = key[k];
     sid[lp] = (last && vbit) ? (id[k] & ~kRsLack) : id[k];
     sdig[lp] = (uint16_t)d;
   }
   __syncthreads();
-  const size_t t0 = (size_t)blockIdx.x * kRsTile;
-  const uint32_t rows = (uint32_t)min(kRsTile, n - t0);
-  for (uint32_t q = threadIdx.x; q < rows; q += kRsBlock) {
+  const size_t t0 = tile * T::kRows;
+  const uint32_t rows = (uint32_t)min(T::kRows, n - t0);
+  for (uint32_t q = threadIdx.x; q < rows; q += BLK) {
     const uint32_t d = sdig[q];
     const uint32_t dst = dbase[d] + (q - lstart[d]);
     if (keys_out) keys_out[dst] = skey[q];
     ids_out[dst] = sid[q];
+    // bucket runs (last pass of the MSD path; rows lacking the position sit in digit 256 / 0: skipped)
+    if (runs.first && !(valid && d == (desc ? 256u : 0u))) {
+      const uint64_t k = skey[q];
+      const uint32_t b = (uint32_t)(k >> runs.s1);
+      const bool head = q == lstart[d] || (uint32_t)(skey[q - 1] >> runs.s1) != b;
+      const bool tail = q + 1 == lstart[d + 1] || (uint32_t)(skey[q + 1] >> runs.s1) != b;
+      if (head) {
+        atomicMin(&runs.first[b], dst);
+        atomicMin(&runs.kmin[b], (unsigned long long)k);
+        atomicMax(&runs.kmax[b], (unsigned long long)k);
+      } else if (skey[q - 1] != k) {
+        runs.multi[b] = 1u;
+      }
+      if (tail) atomicMax(&runs.end[b], dst + 1);
+    }
   }
 }
 
@@ -393,8 +475,6 @@ __global__ void __launch_bounds__(kRsBlock) k_rs_scatter(const uint64_t* __restr
 // Per row: 2 LSD passes + 8 B of bounds read, and for rows of multi-key buckets a 4 B id copy plus
 // (8 B key + 4 B id read, 4 B id written) per partition round or sort, against
 // ceil(bits(span) / 8) LSD passes (7 for a 2^54 span).
-constexpr int kMsdBits = 16;
-constexpr uint32_t kMsdBuckets = 1u << kMsdBits;
 constexpr uint32_t kMsdWaveMax = 512;
 constexpr uint32_t kMsdBlockMax = 8192;
 constexpr int kMsdBigBlocks = 256;  // grid of the block path (grid-stride over the big buckets; one per CU:
@@ -450,51 +530,6 @@ __device__ __forceinline__ void bitonic(uint64_t (&v)[E], int t, uint64_t* xch) 
         }
       }
     }
-  }
-}
-
-__device__ __forceinline__ uint32_t msd_bucket_of(uint64_t key, int s1) { return (uint32_t)(key >> s1); }
-
-// Holder range of the sorted rows: the last (validity) pass put the rows lacking the position in
-// bucket 256 (descending: at the end) or 0 (ascending: in front).
-__device__ __forceinline__ void msd_holders(const uint32_t* __restrict__ dtot, size_t n, int desc, bool has_valid,
-                                            size_t* h0, size_t* h1) {
-  *h0 = 0;
-  *h1 = n;
-  if (has_valid) {
-    if (desc) *h1 = n - dtot[256];
-    else *h0 = dtot[0];
-  }
-}
-
-// first[b] / end[b]: first row / one past the last row of non-empty bucket b (read only where multi[b]);
-// multi[b] = 1 when bucket b holds two distinct keys (preset to 0). Neighbouring keys come from the
-// adjacent lanes; 4 rows per thread (loads in flight together); block 0 also clears the control words.
-constexpr int kMsdBoundsRows = 4;
-__global__ void __launch_bounds__(256) k_msd_bounds(const uint64_t* __restrict__ keys, size_t n, int s1,
-                                                    const uint32_t* __restrict__ dtot, int desc, bool has_valid,
-                                                    uint32_t* __restrict__ first, uint32_t* __restrict__ end,
-                                                    uint32_t* __restrict__ multi) {
-  size_t h0, h1;
-  msd_holders(dtot, n, desc, has_valid, &h0, &h1);
-  const int lane = threadIdx.x & 63;
-  const size_t base = h0 + (size_t)blockIdx.x * 256 * kMsdBoundsRows + threadIdx.x;
-  uint64_t k[kMsdBoundsRows];
-#pragma unroll
-  for (int r = 0; r < kMsdBoundsRows; ++r) k[r] = keys[min(base + (size_t)r * 256, h1 - 1)];
-#pragma unroll
-  for (int r = 0; r < kMsdBoundsRows; ++r) {
-    const size_t i = base + (size_t)r * 256;
-    const bool in = i < h1;
-    uint64_t kp = (uint64_t)__shfl_up((long long)k[r], 1), kn = (uint64_t)__shfl_down((long long)k[r], 1);
-    if (!in) continue;
-    if (lane == 0 && i > h0) kp = keys[i - 1];
-    if (lane == 63 && i + 1 < h1) kn = keys[i + 1];
-    const uint32_t b = msd_bucket_of(k[r], s1);
-    const bool head = i == h0 || msd_bucket_of(kp, s1) != b;
-    if (head) first[b] = (uint32_t)i;
-    else if (kp != k[r]) multi[b] = 1u;
-    if (i == h1 - 1 || msd_bucket_of(kn, s1) != b) end[b] = (uint32_t)(i + 1);
   }
 }
 
@@ -574,29 +609,39 @@ __device__ __forceinline__ void msd_wave_sort(const uint64_t* __restrict__ keys,
   }
 }
 
-__global__ void __launch_bounds__(256) k_msd_local(const uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
-                                                   uint32_t* __restrict__ ids, const uint32_t* __restrict__ first,
-                                                   const uint32_t* __restrict__ end,
-                                                   const uint32_t* __restrict__ multi, int s1,
+__global__ void __launch_bounds__(256) k_msd_local(const int64_t* __restrict__ col, int desc, uint64_t kmin,
+                                                   uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
+                                                   uint32_t* __restrict__ ids, MsdRuns runs,
                                                    uint32_t* __restrict__ ctl, uint32_t* __restrict__ big) {
   const int lane = threadIdx.x & 63;
   {  // one wave per bucket (a grid-stride loop over the buckets measured 34 -> 56 us: the multi-key
      // buckets' rounds serialise within a wave)
     const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (!multi[b]) return;  // empty, or one key: the last pass already put its rows in their place
-    const uint32_t lo = first[b], m = end[b] - lo;
-    // this bucket's grouped ids to the side buffer (free after the last pass), read from there below
+    const uint32_t lo = runs.first[b];
+    if (lo == ~0u) return;  // empty
+    if (!runs.multi[b] && runs.kmin[b] == runs.kmax[b]) return;  // one key: the last pass put its rows in place
+    const uint32_t m = runs.end[b] - lo;
+    // this bucket's grouped ids to the side buffer (free after the last pass), and their keys gathered
+    // from the column by id (the last pass does not write the keys out), read from there below
     for (uint32_t p0 = 0; p0 < m; p0 += 512) {  // 8 loads in flight per lane, then their stores
       uint32_t v[8];
+      int64_t c[8];
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         const uint32_t p = p0 + (uint32_t)(r * 64 + lane);
-        v[r] = p < m ? ids[lo + p] : 0u;
+        v[r] = ids[lo + min(p, m - 1)];
+      }
+      if (col) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) c[r] = col[v[r]];
       }
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         const uint32_t p = p0 + (uint32_t)(r * 64 + lane);
-        if (p < m) src[lo + p] = v[r];
+        if (p < m) {
+          src[lo + p] = v[r];
+          if (col) keys[lo + p] = rs_ukey((uint64_t)c[r], desc) - kmin;
+        }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's copies land before its lanes read them
@@ -605,7 +650,7 @@ __global__ void __launch_bounds__(256) k_msd_local(const uint64_t* __restrict__ 
       if (lane == 0) big[atomicAdd(&ctl[kMsdCtlBig], 1u)] = b;
       return;
     }
-    const uint64_t rmask = (1ull << s1) - 1ull;
+    const uint64_t rmask = (1ull << runs.s1) - 1ull;
     if (m <= 64) msd_wave_sort<1, 6>(keys, src, ids, lo, m, rmask, lane);
     else if (m <= 128) msd_wave_sort<2, 7>(keys, src, ids, lo, m, rmask, lane);
     else if (m <= 256) msd_wave_sort<4, 8>(keys, src, ids, lo, m, rmask, lane);
@@ -635,15 +680,14 @@ __device__ __forceinline__ void msd_block_sort(const uint64_t* __restrict__ keys
 // buckets of 513..8192 rows with more distinct keys than k_msd_local's partition rounds: one
 // workgroup each (grid-stride over the list); larger ones: overflow flag (host falls back to LSD)
 __global__ void __launch_bounds__(1024) k_msd_big(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ src,
-                                                  uint32_t* __restrict__ ids, const uint32_t* __restrict__ first,
-                                                  const uint32_t* __restrict__ end, int s1, uint32_t* __restrict__ ctl,
+                                                  uint32_t* __restrict__ ids, MsdRuns runs, uint32_t* __restrict__ ctl,
                                                   const uint32_t* __restrict__ big) {
   __shared__ uint64_t xch[kMsdBlockMax];
   const uint32_t nbig = ctl[kMsdCtlBig];
-  const uint64_t rmask = (1ull << s1) - 1ull;
+  const uint64_t rmask = (1ull << runs.s1) - 1ull;
   for (uint32_t q = blockIdx.x; q < nbig; q += gridDim.x) {
     const uint32_t b = big[q];
-    const uint32_t lo = first[b], m = end[b] - lo;
+    const uint32_t lo = runs.first[b], m = runs.end[b] - lo;
     if (m > kMsdBlockMax) {
       if (threadIdx.x == 0) atomicOr(&ctl[kMsdCtlOverflow], 1u);
       continue;
@@ -661,7 +705,7 @@ size_t rs_scratch_bytes(size_t n) {
   // MSD bucket starts + control words + big-bucket list
   return 2 * n * 8 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 1024 +
          (size_t)kRsDigits * ((rs_blocks(n) + kScanTiles - 1) / kScanTiles) * 4 + 256 +
-         16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows)) + 768 + (4 * (size_t)kMsdBuckets + 8) * 4;
+         16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows)) + 768 + (8 * (size_t)kMsdBuckets + 8) * 4;
 }
 
 // the MSD path pays off from 4 LSD passes on (a span of > 24 bits) and enough rows to fill the buckets
@@ -673,8 +717,39 @@ static bool msd_enabled(size_t n, int sb) {
   return mode != 0 && n >= ((size_t)1 << 16) && sb > 24;
 }
 
+static int order_env(const char* name, int dflt) {
+  const char* s = getenv(name);
+  return s ? atoi(s) : dflt;
+}
+static int order_xcd() {
+  static const int mode = [] {
+    const char* s = getenv("DDSHE_ORDER_XCD");  // 0: tile = block (A/B)
+    return s ? atoi(s) : 1;
+  }();
+  return mode;
+}
+
+// one LSD pass: per-tile digit counts, their scan over tiles, the stable scatter (tiles of BLK x kRsItems
+// rows; 256 threads measured fastest: 512 / 1024-thread tiles lengthen the write-out's digit runs but
+// cut the blocks per CU, +0 / +10 us on the first pass of 10M rows)
+template <int BLK>
+static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in, const uint8_t* valid, size_t n,
+                    int shift, bool last, int desc, bool vbit, bool kbit, uint64_t kmin, uint32_t* hist,
+                    uint32_t* ctot, uint32_t* dtot, uint64_t* kout, uint32_t* ids_out, uint32_t* clr,
+                    const MsdRuns& runs, uint32_t* tick) {
+  const size_t nb = (n + RsTile<BLK>::kRows - 1) / RsTile<BLK>::kRows;
+  hipLaunchKernelGGL(k_rs_hist<BLK>, dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, last, desc,
+                     vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u);
+  hipLaunchKernelGGL(k_rs_scan, dim3((unsigned)((nb + kScanTiles - 1) / kScanTiles)), dim3(kScanThreads), 0, st, hist,
+                     nb, ctot, dtot, tick);
+  hipLaunchKernelGGL(k_rs_scatter<BLK>, dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, desc, vbit,
+                     kbit, last, kmin, hist, ctot, dtot, nb, kout, ids_out, order_xcd(), runs);
+}
+
+size_t rs_tick_words(size_t) { return 1; }
+
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
-                            uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds) {
+                            uint32_t* tick, uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds) {
   if (n == 0) return hipSuccess;
   const size_t nb = rs_blocks(n);
   uint64_t* ka = (uint64_t*)scratch;
@@ -687,10 +762,11 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   uint64_t* red = (uint64_t*)(((uintptr_t)(ctot + (size_t)kRsDigits * nch) + 15) & ~(uintptr_t)15);
   uint64_t* part = red + 2;
   const size_t pb = (n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows);
-  uint32_t* mfirst = (uint32_t*)(((uintptr_t)(part + 2 * pb) + 255) & ~(uintptr_t)255);
-  uint32_t* mend = mfirst + kMsdBuckets;
-  uint32_t* mmulti = mend + kMsdBuckets;
-  uint32_t* mctl = mmulti + kMsdBuckets;  // right after the multi flags: one memset clears both
+  // MSD bucket table (MsdRuns layout), then the control words and the big-bucket list
+  uint32_t* mtab = (uint32_t*)(((uintptr_t)(part + 2 * pb) + 255) & ~(uintptr_t)255);
+  MsdRuns runs{mtab, (unsigned long long*)(mtab + kMsdBuckets), mtab + 3 * kMsdBuckets,
+               (unsigned long long*)(mtab + 4 * kMsdBuckets), mtab + 6 * kMsdBuckets, 0};
+  uint32_t* mctl = mtab + 7 * kMsdBuckets;
   uint32_t* mbig = mctl + 8;
   uint64_t hred[2];
   hipError_t e = hipSuccess;
@@ -711,41 +787,36 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   const uint64_t kmin = hred[0] <= hred[1] ? hred[0] : 0ull;
   const uint64_t span = hred[0] <= hred[1] ? hred[1] - hred[0] : 0ull;
   const int sb = span ? 64 - __builtin_clzll(span) : 0;  // bits of the span
-  const bool vbit = valid && n <= (size_t)kRsLack;
-  // executed pass j writes ids to fin when (np-1-j) is even, so the last one lands there
-  auto run_passes = [&](const int* shifts, int np, bool keep_keys, uint32_t* fin, uint32_t* tmp) -> const uint64_t* {
+  const bool kbit = valid && sb <= 56;                    // validity in key bit 63 (every shift <= 48)
+  const bool vbit = valid && !kbit && n <= (size_t)kRsLack;
+  // executed pass j writes ids to fin when (np-1-j) is even, so the last one lands there; with
+  // msd.first set the first pass clears the bucket table and the last fills it (no keys written out)
+  const int keys2 = order_env("DDSHE_ORDER_KEYS2", 0);
+  auto run_passes = [&](const int* shifts, int np, uint32_t* fin, uint32_t* tmp, const MsdRuns& msd) {
     const uint32_t* ids_in = nullptr;  // identity before the first pass
     const uint64_t* kin = (const uint64_t*)col;  // raw column before the first pass
     uint64_t* kout = ka;
+    const MsdRuns none{};
     for (int j = 0; j < np; ++j) {
       uint32_t* ids_out = ((np - 1 - j) % 2 == 0) ? fin : tmp;
       const bool last = j == np - 1;
-      hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)nb), dim3(kRsBlock), 0, st, kin, ids_in, valid, n, shifts[j], last,
-                         desc, vbit, kmin, hist, nb);
-      hipLaunchKernelGGL(k_rs_scan_tiles, dim3((unsigned)nch), dim3(kScanThreads), 0, st, hist, nb, ctot);
-      hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nch, dtot);
-      hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)nb), dim3(kRsBlock), 0, st, kin, ids_in, valid, n, shifts[j],
-                         desc, vbit, last, kmin, hist, ctot, dtot, nb, (last && !keep_keys) ? nullptr : kout, ids_out);
+      rs_pass<256>(st, kin, ids_in, valid, n, shifts[j], last, desc, vbit, kbit, kmin, hist, ctot, dtot,
+                   last ? (msd.first && keys2 ? kout : nullptr) : kout, ids_out, j == 0 ? msd.first : nullptr,
+                   last ? msd : none, tick);
       kin = kout;
       kout = kout == ka ? kb : ka;
       ids_in = ids_out;
     }
-    return kin;
   };
   if (msd_enabled(n, sb)) {
-    const int s1 = sb - kMsdBits;
-    const int shifts[2] = {s1, sb - 8};
-    // grouped ids -> out_ids (one-key buckets are final there); ib (the first pass's ids) is then free
-    // and serves as the side copy of the multi-key buckets (k_msd_local)
-    const uint64_t* sorted = run_passes(shifts, 2, true, out_ids, ib);
-    if ((e = hipMemsetAsync(mmulti, 0, (kMsdBuckets + 8) * 4, st)) != hipSuccess) return e;  // flags + control
-    const size_t nbd = (n + 256 * kMsdBoundsRows - 1) / (256 * kMsdBoundsRows);  // over <= n holder rows
-    hipLaunchKernelGGL(k_msd_bounds, dim3((unsigned)nbd), dim3(256), 0, st, sorted, n, s1, dtot, desc, valid != nullptr,
-                       mfirst, mend, mmulti);
-    hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / 4), dim3(256), 0, st, sorted, ib, out_ids, mfirst, mend, mmulti,
-                       s1, mctl, mbig);
-    hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, sorted, ib, out_ids, mfirst, mend, s1, mctl,
-                       mbig);
+    runs.s1 = sb - kMsdBits;
+    const int shifts[2] = {runs.s1, sb - 8};
+    // grouped ids -> out_ids (one-key buckets are final there) + the bucket table; ib (the first pass's
+    // ids) and kb are then free: the side copies of the multi-key buckets' ids and keys (k_msd_local)
+    run_passes(shifts, 2, out_ids, ib, runs);
+    hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / 4), dim3(256), 0, st, keys2 ? nullptr : col, desc, kmin, kb, ib,
+                       out_ids, runs, mctl, mbig);
+    hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, kb, ib, out_ids, runs, mctl, mbig);
     uint32_t hctl[2];
     if ((e = hipMemcpyAsync(hctl, mctl, sizeof(hctl), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
@@ -759,7 +830,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     hipLaunchKernelGGL(k_rs_iota, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out_ids, n);
     return hipGetLastError();
   }
-  run_passes(shifts, np, false, out_ids, ib);
+  run_passes(shifts, np, out_ids, ib, MsdRuns{});
   return hipGetLastError();
 }
 

@@ -34,6 +34,7 @@ _lib = C.CDLL(LIB_PATH)
 DDS_OK, DDS_E_EMPTY, DDS_E_RANGE, DDS_E_HIP, DDS_E_ARG = 0, 1, 2, 3, 4
 DDS_E_NOMEM, DDS_E_UNSUPPORTED, DDS_E_BUFSIZE, DDS_E_FORMAT = 5, 6, 7, 8
 OPE_OPS = {"gt": 0, "ge": 1, "lt": 2, "le": 3}
+DDS_PAIR_GPU, DDS_PAIR_LONE, DDS_PAIR_HOST = 0, 1, 2  # dds_pair_set_policy
 
 # every symbol the header declares (checked by tests/test_abi.py without a GPU)
 EXPORTS = [
@@ -54,7 +55,7 @@ EXPORTS = [
     "dds_mctx_create", "dds_mctx_create_devices", "dds_mctx_destroy", "dds_mctx_shards", "dds_mcol_create",
     "dds_mcol_destroy", "dds_mcol_count", "dds_mcol_append", "dds_mcol_append_dec", "dds_mcol_fill_paillier_synth",
     "dds_mcol_fold", "dds_mcol_fold_rows", "dds_mcol_fold_dec",
-    "dds_pair_modmul_dec", "dds_pair_stats", "dds_pair_timing",
+    "dds_pair_modmul_dec", "dds_pair_stats", "dds_pair_timing", "dds_pair_set_policy", "dds_pair_cpu",
     "dds_col_write_rows", "dds_col_write_rows_dec", "dds_col_set_live", "dds_col_live_count",
     "dds_mcol_write_rows", "dds_mcol_write_rows_dec", "dds_mcol_set_live", "dds_mcol_live_count",
     "dds_opecol_write_rows", "dds_opecol_write_rows_dec", "dds_opecol_set_live", "dds_opecol_live_count",
@@ -141,6 +142,8 @@ _u64p = C.POINTER(C.c_uint64)
 _sig("dds_pair_modmul_dec", C.c_int, C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, _sz, _szp)
 _sig("dds_pair_stats", C.c_int, C.c_void_p, _u64p, _u64p)
 _sig("dds_pair_timing", C.c_int, C.c_void_p, _u64p, _u64p, _u64p, _u64p)
+_sig("dds_pair_set_policy", C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int))
+_sig("dds_pair_cpu", C.c_int, C.c_void_p, _u64p, _u64p, _u64p, _u64p, _u64p, _u64p)
 _sig("dds_ctx_cache_stats", C.c_int, C.c_void_p, _szp, _szp)
 _sig("dds_col_fold_rows", C.c_int, C.c_void_p, _u64p, _sz, _u8p, _sz, _szp)
 _sig("dds_col_fold_dec", C.c_int, C.c_void_p, _u64p, _sz, C.c_char_p, _sz, _szp)
@@ -401,6 +404,20 @@ class Engine:
         b, g, m, mg = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64()
         _check(_lib.dds_pair_timing(self._h, C.byref(b), C.byref(g), C.byref(m), C.byref(mg)), "dds_pair_timing")
         return b.value, g.value, m.value, mg.value
+
+    def pair_set_policy(self, policy: int) -> int:
+        """Serve pair_modmul_dec by GPU batches (DDS_PAIR_GPU), lone requests on the host
+        (DDS_PAIR_LONE) or every request on the host (DDS_PAIR_HOST); policy < 0 only queries.
+        Returns the policy in force before the call."""
+        prev = C.c_int()
+        _check(_lib.dds_pair_set_policy(self._h, int(policy), C.byref(prev)), "dds_pair_set_policy")
+        return prev.value
+
+    def pair_cpu(self) -> dict:
+        """Cumulative host CPU ns of pair_modmul_dec by phase (dds_pair_cpu) and host-served requests."""
+        v = [C.c_uint64() for _ in range(6)]
+        _check(_lib.dds_pair_cpu(self._h, *[C.byref(x) for x in v]), "dds_pair_cpu")
+        return dict(zip(("codec_ns", "pack_ns", "queue_ns", "wait_ns", "host_ns", "host_calls"), (x.value for x in v)))
 
     def cache_stats(self):
         """(cached modulus constants, live pairwise queues) of this engine"""

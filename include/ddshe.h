@@ -113,6 +113,24 @@ int dds_pair_stats(dds_ctx* ctx, uint64_t* calls, uint64_t* launches);
  * bounds the rate, well below it the callers' own scheduling does. */
 int dds_pair_timing(dds_ctx* ctx, uint64_t* batch_ns, uint64_t* gpu_ns, uint64_t* max_batch_ns,
                     uint64_t* max_gpu_ns);
+/* Which engine serves dds_pair_modmul_dec's products on this context (policy < 0: query only; the
+ * policy in force before the call goes to *previous when given):
+ *   DDS_PAIR_GPU  every request through the coalescing queue (k_pairs batches);
+ *   DDS_PAIR_LONE a request that finds its modulus' queue empty, no batch in flight and no other host
+ *                 product running is served by the engine's host product (64-bit-limb Comba product +
+ *                 Barrett reduction, bn_host.hpp); requests arriving meanwhile queue for a GPU batch;
+ *   DDS_PAIR_HOST every request by the host product.
+ * Default DDS_PAIR_LONE (environment DDSHE_PAIR_POLICY overrides it). Results are identical. */
+#define DDS_PAIR_GPU 0
+#define DDS_PAIR_LONE 1
+#define DDS_PAIR_HOST 2
+int dds_pair_set_policy(dds_ctx* ctx, int policy, int* previous);
+/* Host CPU of dds_pair_modmul_dec on this context by phase, cumulative thread-CPU ns: decimal codec
+ * (operand and modulus parse, reply), limb packing of the GPU batches, the callers' queue and
+ * condition-variable time, the batch leaders' wait for the GPU round trip (hipStreamSynchronize), the
+ * host products; and the number of requests the host products served. */
+int dds_pair_cpu(dds_ctx* ctx, uint64_t* codec_ns, uint64_t* pack_ns, uint64_t* queue_ns, uint64_t* wait_ns,
+                 uint64_t* host_ns, uint64_t* host_calls);
 /* Sizes of the per-request caches: modulus constants (LRU, at most DDSHE_MAX_MODULI, default 64) and
  * pairwise queues (one per modulus with calls in flight; dropped when idle). */
 int dds_ctx_cache_stats(dds_ctx* ctx, size_t* moduli, size_t* pair_queues);

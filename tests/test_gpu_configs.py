@@ -79,3 +79,50 @@ def test_modexp_edge_exponents(eng, keys):
     assert eng.modexp_batch(n, 0, xs) == [1 % n] * len(xs)
     assert eng.modexp_batch(n, 1, xs) == [x % n for x in xs]
     assert eng.modexp_batch(n, 65537, xs) == [pow(x, 65537, n) for x in xs]
+
+
+def test_config3_full_size_product(eng, keys):
+    """Config 3's product at its BASELINE size inside the test suite: 10M RSA-2048 ciphertexts
+    (rows table[h_i], table = Enc(1..9999) on the GPU, as the bench's column), one MultAll fold through
+    the natural dispatch (k_fold1 first level, then the tail shapes over its partials); checked against
+    prod_j table[j]^count[j] mod n, and a 5k-row prefix against the oracle (DDSRestServer.scala:506-524)."""
+    import ddshe
+    k = keys["rsa2048_seed3"]
+    n, rows = k["n"], 10_000_000
+    table = eng.modexp_batch(n, k["e"], list(range(1, 10000)))
+    col = eng.column(n, rows)
+    col.fill_table_synth(table, 3, 0, rows)
+    prod = col.fold()
+    cnt = np.bincount(ddshe.synth_indices(3, 0, rows, 9999), minlength=9999)
+    want = 1
+    for t, c in zip(table, cnt.tolist()):
+        if c:
+            want = want * pow(t, c, n) % n
+    assert prod == want
+    assert col.fold(0, 5000) == homo.modmul_fold(col.read(0, 5000), n)
+    col.close()
+
+
+def test_config4_full_size_encrypt_then_sum(eng, keys):
+    """Config 4 at the bench's 1M-row sub-batch inside the test suite: 1M Paillier
+    encryptions under the 3072-bit key (CRT halves; r from the seeded device stream, m as config 2),
+    then SumAll over the fresh ciphertexts: Dec(sum) == sum(m), and 32 rows spread over the batch equal
+    the oracle's g^m r^n mod n^2 (SJHomoLibProvider.scala:58)."""
+    import torch
+
+    import ddshe
+    k = keys["paillier3072_seed4"]
+    rows = 1_000_000
+    ms = ddshe.synth_plaintexts(4, 0, rows)
+    d_m = torch.from_numpy(ms.astype(np.int32)).to("cuda")
+    rcol = eng.column(k["nsquare"], rows)
+    rcol.fill_random(k["n"].bit_length() - 1, 4, 0, rows)
+    out = eng.column(k["nsquare"], rows)
+    out.encrypt_paillier(rcol, 0, d_m.data_ptr(), rows, k["n"], k["g"], k["p"], k["q"])
+    torch.cuda.synchronize()
+    s = out.fold()
+    assert homo.paillier_decrypt(s, k) == int(ms.astype(np.int64).sum()) % k["n"]
+    for i in np.linspace(0, rows - 1, 32).astype(int).tolist():
+        assert out.read(i, 1)[0] == homo.paillier_encrypt(int(ms[i]), rcol.read(i, 1)[0], k), i
+    out.close()
+    rcol.close()

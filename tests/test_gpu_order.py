@@ -121,7 +121,8 @@ def test_order_sl_non_holders_32_rows(eng):
         assert [k for k in got if k in set(lack)] == lack  # non-holders keep their input order
 
 
-@pytest.mark.parametrize("kind", ["uniform_2p40", "ope_map_ties", "block_buckets", "overflow_bucket"])
+@pytest.mark.parametrize("kind", ["uniform_2p40", "ope_map_ties", "block_buckets", "overflow_bucket", "span_2p56",
+                                  "span_2p57", "seam_two_keys"])
 def test_order_msd_buckets(eng, kind):
     """Spans of > 24 bits over >= 65,536 rows take the MSD split: two stable passes over the top 16
     bits of the span, then each of the 65,536 buckets sorted by the rest of its keys (one wave up to
@@ -131,6 +132,18 @@ def test_order_msd_buckets(eng, kind):
     n = 400_009
     if kind == "uniform_2p40":
         col = rng.integers(-(1 << 39), 1 << 39, size=n, dtype=np.int64)
+    elif kind in ("span_2p56", "span_2p57"):  # validity in key bit 63 up to a 56-bit span, in the row id above
+        bits = 56 if kind == "span_2p56" else 57
+        col = rng.integers(0, 1 << bits, size=n, dtype=np.int64) - (1 << (bits - 1))
+        col[:2] = [-(1 << (bits - 1)), (1 << (bits - 1)) - 1]
+    elif kind == "seam_two_keys":
+        # a bucket whose keys differ only ACROSS tiles (each tile's run of it holds one key): the last
+        # pass's scatter must flag it through the per-bucket min / max of the runs' keys
+        col = rng.integers(0, 1 << 40, size=n, dtype=np.int64)
+        col[: n // 2 : 50] = (77 << 24) + 9
+        col[n // 2 :: 50] = (77 << 24) + 3
+        col[1 : n // 2 : 50] = (78 << 24) + 1
+        col[n // 2 + 1 :: 50] = (78 << 24) + 1
     elif kind == "ope_map_ties":  # the bench's generator: 10^4 distinct values, ~40 rows each here
         ope_map = np.cumsum(rng.integers(1, 1 << 40, size=10001, dtype=np.int64)) - (1 << 52)
         col = ope_map[rng.integers(1, 10001, size=n)]

@@ -1,12 +1,12 @@
 #!/bin/bash
 # rocprofv3 kernel statistics for every bench workload, then PMC HBM-traffic passes (one counter
 # per pass) for the HBM-bound workloads. Run on the GPU box from the repo root:
-#   gpurun -- tools/profile_all.sh
+#   gpurun -- tools/gpurun/profile_all.sh
 # Outputs under gpurun_out/prof/<name>/ (CSV); copy the summaries to be judged into profiles/.
 export TMPDIR=/tmp
 P=gpurun_out/prof
 B="python3 bench.py --no-cpu-baseline --no-e2e"
-exec tools/gpu_steps.sh \
+exec tools/gpurun/steps.sh \
   "300 ks_sum rocprofv3 --kernel-trace --stats --output-format csv -d $P/sum -o run -- $B --steps 5" \
   "300 ks_e2e rocprofv3 --kernel-trace --stats --output-format csv -d $P/e2e -o run -- python3 bench.py --no-cpu-baseline --no-extras --steps 1" \
   "300 ks_pf rocprofv3 --kernel-trace --stats --output-format csv -d $P/product_filter -o run -- $B --workload product_filter --steps 5" \

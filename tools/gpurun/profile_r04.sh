@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 profiles (run on the GPU box from the repo root: gpurun -- tools/profile_r04.sh):
+# Round-4 profiles (run on the GPU box from the repo root: gpurun -- tools/gpurun/profile_r04.sh):
 #   * rocprofv3 kernel stats of the headline with ONE fold size (10M rows: no strong-split share, no CPU
 #     prefix fold), so the k_fold row's Average is the headline launch;
 #   * kernel stats of the order, product_filter (Search route) and entry_search (string table) workloads;
@@ -8,7 +8,7 @@
 export TMPDIR=/tmp
 P=gpurun_out/prof
 B="python3 bench.py --no-cpu-baseline --no-e2e"
-exec tools/gpu_steps.sh \
+exec tools/gpurun/steps.sh \
   "300 ks_sum rocprofv3 --kernel-trace --stats --output-format csv -d $P/sum -o run -- $B --no-extras --verify 0 --steps 5" \
   "300 ks_order rocprofv3 --kernel-trace --stats --output-format csv -d $P/order -o run -- $B --workload order --steps 5" \
   "300 ks_pf rocprofv3 --kernel-trace --stats --output-format csv -d $P/product_filter -o run -- $B --workload product_filter --steps 5" \

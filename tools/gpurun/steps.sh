@@ -1,6 +1,6 @@
 #!/bin/bash
-# Run GPU steps in order; stop at the first step that faulted, aborted or timed out.
-# usage: tools/gpu_steps.sh "<limit_s> <name> <cmd>" ...
+# Run GPU steps in order; stop at the first step that fails (a fault, abort, time limit or error).
+# usage: tools/gpurun/steps.sh "<limit_s> <name> <cmd>" ...
 mkdir -p gpurun_out
 for spec in "$@"; do
   limit=${spec%% *}; rest=${spec#* }; name=${rest%% *}; cmd=${rest#* }
@@ -8,5 +8,5 @@ for spec in "$@"; do
   timeout -k 10 "$limit" bash -c "$cmd" > "gpurun_out/$name.log" 2>&1
   rc=$?
   echo "== $name rc=$rc" | tee -a gpurun_out/steps.log
-  case $rc in 124|134|137|139|-6|-11) echo "stopping after $name (rc=$rc)"; exit $rc;; esac
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 done

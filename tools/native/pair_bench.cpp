@@ -2,7 +2,9 @@
 // concurrently on one context, as the proxy's ForkJoin pool runs /Sum routes (DDSRestServer.scala:21,
 // 355-395), with no interpreter lock between them. Reports calls per k_pairs launch, pairs/s and the
 // per-call latency distribution as one JSON line, plus a few (a, b, result) samples for the caller to
-// check (bench.py verifies them with Python ints).
+// check (bench.py verifies them with Python ints). The serving policy is the context default
+// (DDSHE_PAIR_POLICY; dds_pair_set_policy); the line carries the host CPU per call, whole process and by
+// phase (dds_pair_cpu).
 //
 //   pair_bench <modulus_dec> <threads> <calls_per_thread> [seed] [warmup_calls_per_thread=20]
 #include <chrono>
@@ -88,6 +90,8 @@ int main(int argc, char** argv) {
   while (ready.load() < T) std::this_thread::yield();
   dds_pair_stats(ctx, &c0, &l0);
   dds_pair_timing(ctx, &b0, &g0, &mx, &mg);  // also restarts the longest-batch windows
+  uint64_t p0[6], p1[6];  // host CPU by phase (dds_pair_cpu)
+  dds_pair_cpu(ctx, &p0[0], &p0[1], &p0[2], &p0[3], &p0[4], &p0[5]);
   struct rusage ru0, ru1;
   getrusage(RUSAGE_SELF, &ru0);
   const auto t0 = std::chrono::steady_clock::now();
@@ -99,6 +103,11 @@ int main(int argc, char** argv) {
   const double cpu_s = tv(ru0.ru_utime, ru1.ru_utime) + tv(ru0.ru_stime, ru1.ru_stime);
   dds_pair_stats(ctx, &c1, &l1);
   dds_pair_timing(ctx, &b1, &g1, &mx, &mg);
+  dds_pair_cpu(ctx, &p1[0], &p1[1], &p1[2], &p1[3], &p1[4], &p1[5]);
+  int policy = -1;
+  dds_pair_set_policy(ctx, -1, &policy);
+  const double ncalls = c1 > c0 ? (double)(c1 - c0) : 1.0;
+  auto per_call_us = [&](int i) { return (double)(p1[i] - p0[i]) / ncalls * 1e-3; };
   const double nl = l1 > l0 ? (double)(l1 - l0) : 1.0;
   std::vector<double> all;
   for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
@@ -111,12 +120,16 @@ int main(int argc, char** argv) {
          "\"cached_moduli\": %zu, \"pair_queues_after\": %zu, \"hw_threads\": %u, "
          "\"batch_us_per_launch\": %.2f, \"gpu_round_trip_us_per_launch\": %.2f, \"wall_us_per_launch\": %.2f, "
          "\"mean_batches_in_flight\": %.3f, \"max_batch_ms\": %.3f, \"max_gpu_round_trip_ms\": %.3f, \"cpu_cores_busy\": %.2f, "
-         "\"involuntary_switches\": %ld, \"voluntary_switches\": %ld, \"samples\": [",
+         "\"involuntary_switches\": %ld, \"voluntary_switches\": %ld, \"policy\": %d, \"cpu_us_per_call\": %.2f, "
+         "\"phase_cpu_us_per_call\": {\"codec\": %.2f, \"pack\": %.2f, \"queue\": %.2f, \"gpu_wait\": %.2f, "
+         "\"host_product\": %.2f}, \"host_served\": %llu, \"samples\": [",
          T, (unsigned long long)(c1 - c0), (unsigned long long)(l1 - l0),
          (l1 > l0) ? (double)(c1 - c0) / (double)(l1 - l0) : 0.0, (double)all.size() / secs, pct(0.5), pct(0.99),
          all.empty() ? 0.0 : all.back(), errors.load(), mod.size(), moduli, queues, std::thread::hardware_concurrency(),
          (double)(b1 - b0) / nl * 1e-3, (double)(g1 - g0) / nl * 1e-3, secs / nl * 1e6, (double)(b1 - b0) * 1e-9 / secs,
-         (double)mx * 1e-6, (double)mg * 1e-6, cpu_s / secs, ru1.ru_nivcsw - ru0.ru_nivcsw, ru1.ru_nvcsw - ru0.ru_nvcsw);
+         (double)mx * 1e-6, (double)mg * 1e-6, cpu_s / secs, ru1.ru_nivcsw - ru0.ru_nivcsw, ru1.ru_nvcsw - ru0.ru_nvcsw,
+         policy, cpu_s / ncalls * 1e6, per_call_us(0), per_call_us(1), per_call_us(2), per_call_us(3), per_call_us(4),
+         (unsigned long long)(p1[5] - p0[5]));
   bool first = true;
   for (int t = 0; t < std::min(T, 4); ++t)
     for (size_t i = 0; i < R[t].size(); ++i) {

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""HBM traffic per kernel from the rocprofv3 --pmc passes of tools/profile_all.sh (tool, not product).
+"""HBM traffic per kernel from the rocprofv3 --pmc passes of tools/gpurun/profile_all.sh (tool, not product).
 
 usage: tools/pmc_summary.py <prof dir> <out.json>
 Reads <prof dir>/pmc_<workload>_{fetch,write}/**/*counter_collection.csv and writes, per
@@ -55,7 +55,7 @@ def main(prof, out):
                                     "hbm_bytes_max_dispatch": 2 * fe.get(k, {}).get("max", 0.0) * 1024
                                     + wr.get(k, {}).get("max", 0.0) * 1024}
     json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, one bench step each "
-                         "(tools/profile_all.sh; tools/pmc_summary.py)",
+                         "(tools/gpurun/profile_all.sh; tools/pmc_summary.py)",
                "correction": "gfx950 FETCH_SIZE counts half the bytes of a coalesced stream (MI355X_MICROARCH.md "
                              "HBM section): read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE x 1024 as is",
                "rows_per_dispatch": 10000000, "kernels": kernels}, open(out, "w"), indent=1)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""VALU issue summary of one kernel's largest dispatch from the tools/pmc_valu.sh pass (tool, not product).
+"""VALU issue summary of one kernel's largest dispatch from the tools/gpurun/pmc_valu.sh pass (tool, not product).
 
 usage: tools/pmc_valu_summary.py <counter_collection.csv> <kernel substring> <products> <S> <out.json>
 <products> Montgomery products that dispatch ran, <S> its limb count: the expected mad count is
@@ -39,7 +39,7 @@ def main(path, kern, products, s, out):
         "waitcnt_share": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
     }
     counters = {k: v for k, v in c.items() if k not in ("dur_ns", "name")}
-    json.dump({"kernel": c["name"][:120], "source": "rocprofv3 --pmc (tools/pmc_valu.sh), largest dispatch of the kernel",
+    json.dump({"kernel": c["name"][:120], "source": "rocprofv3 --pmc (tools/gpurun/pmc_valu.sh), largest dispatch of the kernel",
                "products": products, "S": s, "counters": counters, "duration_s": dur, "derived": derived},
               open(out, "w"), indent=1)
     print(json.dumps(derived, indent=1))
