@@ -703,7 +703,7 @@ def run_extra_configs(main_wl):
 
 
 # tools/gpurun/profile_all.sh passes, summarised by tools/pmc_summary.py (newest round first)
-PMC_FILE = next((f for f in ("r04_pmc.json", "r03_pmc.json", "r02_pmc_filter_order.json")
+PMC_FILE = next((f for f in ("r05_pmc.json", "r04_pmc.json", "r03_pmc.json", "r02_pmc_filter_order.json")
                  if os.path.exists(os.path.join(ROOT, "profiles", f))), "r02_pmc_filter_order.json")
 
 
@@ -734,9 +734,9 @@ def order_pmc_traffic():
     one raw call (k_rs_prep + k_rs_red once) and the resident line's calls (no prep), so the other
     kernels' bytes are divided by the calls (one k_msd_bounds dispatch per call)."""
     once = pmc_traffic("order", ("k_rs_prep", "k_rs_red"), per_step=True)
-    rest = pmc_traffic("order", ("k_rs_hist", "k_rs_scan_tiles", "k_rs_scan_chunks", "k_rs_scatter", "k_msd_bounds",
-                                 "k_msd_local", "k_msd_big"), per_step=True)
-    calls = (pmc_entry(["order"], "k_msd_bounds") or (None, 0))[1]
+    rest = pmc_traffic("order", ("k_rs_hist<256>", "k_rs_scan", "k_rs_scatter<256>", "k_msd_local", "k_msd_big"),
+                       per_step=True)
+    calls = (pmc_entry(["order"], "k_msd_local") or (None, 0))[1]
     if once is None or rest is None or not calls:
         return None
     return once + rest / calls
@@ -1066,13 +1066,14 @@ class OrderWorkload(_Workload):
                 print("VERIFY FAILED", file=sys.stderr)
         step_s = elapsed / a.steps
         alg = 13 * self.mine  # read key + valid byte, write one row id
-        roof = {"bound": "hbm", "kernel": "k_rs_prep + 2 LSD passes over the top 16 bits of the key span (k_rs_hist/k_rs_scan_tiles/"
-                "k_rs_scan_chunks/k_rs_scatter) + k_msd_bounds + k_msd_local/k_msd_big (in-bucket order of the "
-                "buckets holding two distinct keys)",
+        roof = {"bound": "hbm", "kernel": "k_rs_prep + 2 LSD passes over the top 16 bits of the key span (k_rs_hist/k_rs_scan/"
+                "k_rs_scatter; the last scatter also fills the bucket table) + k_msd_local/k_msd_big (in-bucket order "
+                "of the buckets holding two distinct keys)",
                 "achieved": alg / step_s / 1e9, "peak": 8000.0, "unit": "GB/s", "frac": alg / step_s / 1e9 / 8000.0,
                 "algorithmic_bytes": alg,
-                # prep 9 + 2 passes x (hist 8 + scatter 24) + bounds 8 (+ the multi-key buckets' rounds)
-                "issued_bytes_est": self.mine * (9 + 2 * 32 + 8),
+                # prep 9 + pass 1 (hist 9 + scatter 9 + 12) + pass 2 (hist 8 + scatter 12 + 4) (+ the multi-key
+                # buckets' key gathers and rounds)
+                "issued_bytes_est": self.mine * (9 + 30 + 24),
                 "traffic": order_pmc_traffic(),
                 "traffic_unit": "HBM bytes per OrderLS call (PMC, profiles/" + PMC_FILE + ")"}
         roof["issued_GBps"] = roof["issued_bytes_est"] / step_s / 1e9  # what the MSD-split design moves

@@ -14,7 +14,7 @@ import os
 import re
 import sys
 
-WORKLOADS = {"pf": "product_filter", "order": "order", "sum": "sum"}
+WORKLOADS = {"pf": "product_filter", "order": "order", "sum": "sum", "enc": "encrypt_sum"}
 
 
 def short(name):
