@@ -265,7 +265,7 @@ size_t narrow_fold_rows() {
 // Level 1 (throughput shape, G groups: group g holds prod_g * R^(1 - c_g)) over `count` rows of X (or
 // rows d_ids[0..count)), unless the fold is small enough for the tree alone.
 int fold_level1(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
-                size_t count, const uint32_t* d_ids, Leaves* lv) {
+                size_t count, const uint32_t* d_ids, Leaves* lv, size_t max_groups) {
   const int S = mc.S, S2 = mc.S2;
   if (use_tree() && mc.tree_direct && count <= tree_direct_rows()) {
     *lv = Leaves{X, xstride, S, mc.W, count, 0, d_ids};
@@ -291,6 +291,7 @@ int fold_level1(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const ui
     if (fold1_occupancy(S1, &bpc) != hipSuccess || bpc < 1) bpc = 1;
     gmax = (size_t)ctx->cus * bpc * 256;
   }
+  if (max_groups) gmax = std::min(gmax, max_groups);
   size_t G = std::min(gmax, std::max<size_t>(1, count / 2));
   size_t ps = round_up(G, 64);
   HIP_TRY(w->p0.ensure((size_t)S2 * ps * 4));
@@ -447,8 +448,14 @@ int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const 
 
 int fold_partial_device(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
                         size_t count, const uint32_t** part, size_t* part_stride, int64_t* E, const uint32_t* d_ids) {
+  // DDSHE_PARTIAL_GROUPS (A/B of the strong-split share): cap level 1's groups so the
+  // share's partials go straight to the tree (<= 4096) instead of through the tail launches
+  static const size_t cap = [] {
+    const char* e = getenv("DDSHE_PARTIAL_GROUPS");
+    return e ? (size_t)atoll(e) : (size_t)0;
+  }();
   Leaves lv;
-  int rc = fold_level1(ctx, w, st, mc, X, xstride, count, d_ids, &lv);
+  int rc = fold_level1(ctx, w, st, mc, X, xstride, count, d_ids, &lv, cap);
   if (rc) return rc;
   *part_stride = 1;
   return reduce_leaves(ctx, w, st, mc, lv, false, nullptr, part, E);

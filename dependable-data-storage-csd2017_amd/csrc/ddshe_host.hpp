@@ -568,7 +568,7 @@ struct Leaves {
   size_t rows = 0;  // rows folded into these leaves (finalize: how the host waits for the root)
 };
 int fold_level1(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint32_t* X, size_t xstride,
-                size_t count, const uint32_t* d_ids, Leaves* lv);
+                size_t count, const uint32_t* d_ids, Leaves* lv, size_t max_groups = 0);
 int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const Leaves& lv, bool finalize,
                   bn::Limbs* value, const uint32_t** part, int64_t* Eout);
 // canonical product of `count` rows (rows d_ids[0..count) when given); synchronises the stream

@@ -21,6 +21,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "ddshe_launch.hpp"
 
 namespace ddshe {
@@ -205,7 +207,7 @@ __global__ void __launch_bounds__(BLK) k_rs_hist(const uint64_t* __restrict__ ke
                                                       const uint8_t* __restrict__ valid, size_t n, int shift,
                                                       bool last, int desc, bool vbit, bool kbit, uint64_t kmin,
                                                       uint32_t* __restrict__ hist, size_t nblocks,
-                                                      uint32_t* __restrict__ clr, uint32_t nclr) {
+                                                      uint32_t* __restrict__ clr, uint32_t nclr, bool pairs) {
   using T = RsTile<BLK>;
   __shared__ uint32_t cnt[kRsDigits];
   for (int d = threadIdx.x; d < kRsDigits; d += BLK) cnt[d] = 0;
@@ -221,15 +223,41 @@ __global__ void __launch_bounds__(BLK) k_rs_hist(const uint64_t* __restrict__ ke
   // all loads first (independent, in flight together), then the LDS counting
   uint64_t key[kRsItems];
   uint32_t id[kRsItems];
+  size_t rix[kRsItems];
+  if (pairs) {
+    // the tile's rows as 16-byte key pairs (a wave instruction reads 1 KiB; the counts do not depend on
+    // which lane holds which row): pair q = 2 rows; an odd last row on its own. keys 16-byte aligned,
+    // valid 2-byte aligned, no id needed (host-checked)
+    const size_t np = n / 2;
 #pragma unroll
-  for (int k = 0; k < kRsItems; ++k) {  // unconditional loads (index clamped), masked below
-    const size_t i = min(T::row(blockIdx.x, wid, k, lane), n - 1);
-    key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc, kmin, kbit);  // first pass: keys = the column
-    id[k] = need_id ? rs_load_id(ids, i, valid, vbit) : 0u;
+    for (int k = 0; k < kRsItems / 2; ++k) {
+      const size_t q = (size_t)blockIdx.x * (T::kRows / 2) + (size_t)k * BLK + threadIdx.x;
+      const size_t qc = min(q, np ? np - 1 : 0);
+      ulonglong2 kv = np ? reinterpret_cast<const ulonglong2*>(keys)[qc] : make_ulonglong2(0, 0);
+      uint32_t hv = (!ids && valid && np) ? reinterpret_cast<const uint16_t*>(valid)[qc] : 0x0101u;
+      rix[2 * k] = q < np ? 2 * q : ~(size_t)0;
+      rix[2 * k + 1] = q < np ? 2 * q + 1 : ~(size_t)0;
+      if ((n & 1) && q == np) {  // the odd last row
+        kv.x = keys[n - 1];
+        hv = (!ids && valid) ? valid[n - 1] : 1u;
+        rix[2 * k] = n - 1;
+      }
+      key[2 * k] = ids ? kv.x : (hv & 0xFFu) ? rs_ukey(kv.x, desc) - kmin : (kbit ? kRsNoHold : 0ull);
+      key[2 * k + 1] = ids ? kv.y : (hv >> 8) ? rs_ukey(kv.y, desc) - kmin : (kbit ? kRsNoHold : 0ull);
+      id[2 * k] = id[2 * k + 1] = 0u;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kRsItems; ++k) {  // unconditional loads (index clamped), masked below
+      const size_t i = min(T::row(blockIdx.x, wid, k, lane), n - 1);
+      key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc, kmin, kbit);  // first pass: keys = the column
+      id[k] = need_id ? rs_load_id(ids, i, valid, vbit) : 0u;
+      rix[k] = T::row(blockIdx.x, wid, k, lane);
+    }
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
-    const size_t i = T::row(blockIdx.x, wid, k, lane);
+    const size_t i = rix[k];
     const uint32_t d = i < n ? rs_digit(key[k], id[k], valid, shift, last, desc, vbit, kbit) : kRsNone;
     // one LDS atomic per distinct digit of the wave (OPE columns repeat digits a lot; measured
     // faster than per-wave histograms with one atomic per row)
@@ -738,8 +766,13 @@ static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in,
                     uint32_t* ctot, uint32_t* dtot, uint64_t* kout, uint32_t* ids_out, uint32_t* clr,
                     const MsdRuns& runs, uint32_t* tick) {
   const size_t nb = (n + RsTile<BLK>::kRows - 1) / RsTile<BLK>::kRows;
+  // 16-byte key pairs for the counts: aligned keys (and valid bytes when the first pass reads them), no
+  // id read (DDSHE_ORDER_HPAIR=0: one row per lane, A/B)
+  static const int hpair = order_env("DDSHE_ORDER_HPAIR", 1);
+  const bool pairs = hpair && ((uintptr_t)kin & 15) == 0 && (ids_in || !valid || ((uintptr_t)valid & 1) == 0) &&
+                     !(last && valid && !kbit);
   hipLaunchKernelGGL(k_rs_hist<BLK>, dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, last, desc,
-                     vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u);
+                     vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs);
   hipLaunchKernelGGL(k_rs_scan, dim3((unsigned)((nb + kScanTiles - 1) / kScanTiles)), dim3(kScanThreads), 0, st, hist,
                      nb, ctot, dtot, tick);
   hipLaunchKernelGGL(k_rs_scatter<BLK>, dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, desc, vbit,
@@ -816,7 +849,9 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     run_passes(shifts, 2, out_ids, ib, runs);
     hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / 4), dim3(256), 0, st, keys2 ? nullptr : col, desc, kmin, kb, ib,
                        out_ids, runs, mctl, mbig);
-    hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, kb, ib, out_ids, runs, mctl, mbig);
+    static const int big_grid = order_env("DDSHE_ORDER_BIGGRID", kMsdBigBlocks);
+    hipLaunchKernelGGL(k_msd_big, dim3((unsigned)std::max(1, big_grid)), dim3(1024), 0, st, kb, ib, out_ids, runs, mctl,
+                       mbig);
     uint32_t hctl[2];
     if ((e = hipMemcpyAsync(hctl, mctl, sizeof(hctl), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
