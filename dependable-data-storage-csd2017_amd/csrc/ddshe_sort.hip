@@ -201,37 +201,40 @@ struct RsTile {
   }
 };
 
-template <int BLK>
-__global__ void __launch_bounds__(BLK) k_rs_hist(const uint64_t* __restrict__ keys,
-                                                      const uint32_t* __restrict__ ids,
-                                                      const uint8_t* __restrict__ valid, size_t n, int shift,
-                                                      bool last, int desc, bool vbit, bool kbit, uint64_t kmin,
-                                                      uint32_t* __restrict__ hist, size_t nblocks,
-                                                      uint32_t* __restrict__ clr, uint32_t nclr, bool pairs) {
-  using T = RsTile<BLK>;
+// Per-tile digit counts of the scatter's tiles (BLK x kRsItems rows) by HB threads: HB = 64 puts a whole
+// tile on one wave (kRsItems * BLK / 64 rows per lane), so every tile of 10M rows is resident at once
+// instead of 2.4 rounds of 256-thread blocks. The counts do not depend on which lane holds which row.
+template <int BLK, int HB>
+__global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ keys,
+                                                     const uint32_t* __restrict__ ids,
+                                                     const uint8_t* __restrict__ valid, size_t n, int shift,
+                                                     bool last, int desc, bool vbit, bool kbit, uint64_t kmin,
+                                                     uint32_t* __restrict__ hist, size_t nblocks,
+                                                     uint32_t* __restrict__ clr, uint32_t nclr, bool pairs) {
+  constexpr size_t kRows = RsTile<BLK>::kRows;
+  constexpr int kIt = (int)(kRows / HB);  // rows per thread
   __shared__ uint32_t cnt[kRsDigits];
-  for (int d = threadIdx.x; d < kRsDigits; d += BLK) cnt[d] = 0;
+  for (int d = threadIdx.x; d < kRsDigits; d += HB) cnt[d] = 0;
   if (clr) {  // first pass of the MSD path: the bucket tables of the last scatter start at their identities
-    const size_t g = (size_t)blockIdx.x * BLK + threadIdx.x;
-    for (size_t g2 = g; g2 < nclr; g2 += (size_t)gridDim.x * BLK)
+    const size_t g = (size_t)blockIdx.x * HB + threadIdx.x;
+    for (size_t g2 = g; g2 < nclr; g2 += (size_t)gridDim.x * HB)
       clr[g2] = g2 < 3 * (size_t)kMsdBuckets ? ~0u : 0u;  // first[], kmin[] (2 words each): ~0; the rest 0
   }
   __syncthreads();
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63;
   const uint64_t lt = (1ull << lane) - 1ull;
   const bool need_id = last && valid && !kbit;
   // all loads first (independent, in flight together), then the LDS counting
-  uint64_t key[kRsItems];
-  uint32_t id[kRsItems];
-  size_t rix[kRsItems];
+  uint64_t key[kIt];
+  uint32_t id[kIt];
+  size_t rix[kIt];
   if (pairs) {
-    // the tile's rows as 16-byte key pairs (a wave instruction reads 1 KiB; the counts do not depend on
-    // which lane holds which row): pair q = 2 rows; an odd last row on its own. keys 16-byte aligned,
-    // valid 2-byte aligned, no id needed (host-checked)
+    // 16-byte key pairs (a wave instruction reads 1 KiB): pair q = 2 rows; an odd last row on its own.
+    // keys 16-byte aligned, valid 2-byte aligned, no id needed (host-checked)
     const size_t np = n / 2;
 #pragma unroll
-    for (int k = 0; k < kRsItems / 2; ++k) {
-      const size_t q = (size_t)blockIdx.x * (T::kRows / 2) + (size_t)k * BLK + threadIdx.x;
+    for (int k = 0; k < kIt / 2; ++k) {
+      const size_t q = (size_t)blockIdx.x * (kRows / 2) + (size_t)k * HB + threadIdx.x;
       const size_t qc = min(q, np ? np - 1 : 0);
       ulonglong2 kv = np ? reinterpret_cast<const ulonglong2*>(keys)[qc] : make_ulonglong2(0, 0);
       uint32_t hv = (!ids && valid && np) ? reinterpret_cast<const uint16_t*>(valid)[qc] : 0x0101u;
@@ -248,15 +251,16 @@ __global__ void __launch_bounds__(BLK) k_rs_hist(const uint64_t* __restrict__ ke
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < kRsItems; ++k) {  // unconditional loads (index clamped), masked below
-      const size_t i = min(T::row(blockIdx.x, wid, k, lane), n - 1);
+    for (int k = 0; k < kIt; ++k) {  // unconditional loads (index clamped), masked below
+      const size_t r = (size_t)blockIdx.x * kRows + (size_t)k * HB + threadIdx.x;
+      const size_t i = min(r, n - 1);
       key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc, kmin, kbit);  // first pass: keys = the column
       id[k] = need_id ? rs_load_id(ids, i, valid, vbit) : 0u;
-      rix[k] = T::row(blockIdx.x, wid, k, lane);
+      rix[k] = r;
     }
   }
 #pragma unroll
-  for (int k = 0; k < kRsItems; ++k) {
+  for (int k = 0; k < kIt; ++k) {
     const size_t i = rix[k];
     const uint32_t d = i < n ? rs_digit(key[k], id[k], valid, shift, last, desc, vbit, kbit) : kRsNone;
     // one LDS atomic per distinct digit of the wave (OPE columns repeat digits a lot; measured
@@ -270,7 +274,7 @@ __global__ void __launch_bounds__(BLK) k_rs_hist(const uint64_t* __restrict__ ke
     if (d != kRsNone && (peers & lt) == 0) atomicAdd(&cnt[d], (uint32_t)__popcll(peers));
   }
   __syncthreads();
-  for (int d = threadIdx.x; d < kRsDigits; d += BLK) hist[(size_t)blockIdx.x * kRsDigits + d] = cnt[d];  // 1 KiB, coalesced
+  for (int d = threadIdx.x; d < kRsDigits; d += HB) hist[(size_t)blockIdx.x * kRsDigits + d] = cnt[d];  // 1 KiB, coalesced
 }
 
 // Exclusive scan over tiles per digit: one block per chunk of kScanTiles tiles, one thread per digit
@@ -771,8 +775,13 @@ static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in,
   static const int hpair = order_env("DDSHE_ORDER_HPAIR", 1);
   const bool pairs = hpair && ((uintptr_t)kin & 15) == 0 && (ids_in || !valid || ((uintptr_t)valid & 1) == 0) &&
                      !(last && valid && !kbit);
-  hipLaunchKernelGGL(k_rs_hist<BLK>, dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, last, desc,
-                     vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs);
+  static const int hb = order_env("DDSHE_ORDER_HB", 256);  // threads per histogram block (A/B: 64)
+  if (hb == 64)
+    hipLaunchKernelGGL((k_rs_hist<BLK, 64>), dim3((unsigned)nb), dim3(64), 0, st, kin, ids_in, valid, n, shift, last,
+                       desc, vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs);
+  else
+    hipLaunchKernelGGL((k_rs_hist<BLK, BLK>), dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, last,
+                       desc, vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs);
   hipLaunchKernelGGL(k_rs_scan, dim3((unsigned)((nb + kScanTiles - 1) / kScanTiles)), dim3(kScanThreads), 0, st, hist,
                      nb, ctot, dtot, tick);
   hipLaunchKernelGGL(k_rs_scatter<BLK>, dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, desc, vbit,
