@@ -172,7 +172,9 @@ def main():
             try:  # extra lines never cost the headline line (nor leave the other ranks in the barrier)
                 out.update(wl.extra_rank0())
             except Exception as e:  # noqa: BLE001
+                import traceback
                 out["extras_error"] = f"{type(e).__name__}: {e}"
+                out["extras_traceback"] = traceback.format_exc()[-1500:]
         if world > 1:
             dist.barrier()
     if rank == 0:
@@ -459,11 +461,13 @@ class SumWorkload(_Workload):
         def cpu_per_fold(c, count, reps):
             """host CPU of the calling thread (thread clock) and wall time per dds_col_fold, timing off"""
             out, ln = (C.c_uint8 * (c.mb + 4096))(), C.c_size_t()
-            assert fold_c(c._h, 0, count, out, len(out), C.byref(ln)) == 0
+            st = fold_c(c._h, 0, count, out, len(out), C.byref(ln))
+            assert st == 0, (count, st, self.ddshe._lib.dds_last_error())
             cs, ws = [], []
             for _ in range(reps):
                 c0, w0 = time.thread_time(), time.perf_counter()
-                assert fold_c(c._h, 0, count, out, len(out), C.byref(ln)) == 0
+                st = fold_c(c._h, 0, count, out, len(out), C.byref(ln))
+                assert st == 0, (count, st)
                 cs.append(time.thread_time() - c0)
                 ws.append(time.perf_counter() - w0)
             cs.sort()
@@ -497,7 +501,8 @@ class SumWorkload(_Workload):
         a, b = (str(x) for x in (self.col_sample[0], self.col_sample[1]))
         pair, pair_ms, pair_p99 = med(lambda: eng.pair_modmul_dec(a, b, str(k2["nsquare"])), 200)
         conc = self.concurrent_pairs(k2["nsquare"], threads=64, per_thread=32)
-        native = self.native_pairs(k2["nsquare"], threads=64, per_thread=200)
+        native = self.native_pairs(k2["nsquare"], threads=64, per_thread=200)  # engine default (host products)
+        native_gpu = self.native_pairs(k2["nsquare"], threads=64, per_thread=200, policy=0)  # GPU batches only
         rng = np.random.default_rng(5)
         n_pairs = 65536
         xa = [self.col_sample[i % len(self.col_sample)] for i in range(n_pairs)]
@@ -543,6 +548,7 @@ class SumWorkload(_Workload):
                                            "matches": pair == str(int(a) * int(b) % k2["nsquare"])},
                 "pair_sum_route_concurrent_2048bit": conc,
                 "pair_sum_route_native_threads_2048bit": native,
+                "pair_sum_route_native_threads_gpu_batches_2048bit": native_gpu,
                 "pairs_batched_2048bit": {"pairs": n_pairs, "pairs_per_s": pairs_c_s,
                                           "path": "dds_modmul_pairs (k_pairs + k_egress_be), big-endian host buffers in and out",
                                           "pairs_per_s_with_python_int_marshalling": pairs_s,
@@ -585,18 +591,24 @@ class SumWorkload(_Workload):
         return {"threads": threads, "calls": threads * per_thread, "pairs_per_s": threads * per_thread / wall,
                 "median_ms": lat[len(lat) // 2] * 1e3, "p99_ms": lat[int(len(lat) * 0.99)] * 1e3,
                 "calls_per_launch": (c1 - c0) / max(1, l1 - l0),
-                "path": "dds_pair_modmul_dec from concurrent threads: one k_pairs launch per burst",
+                "path": "dds_pair_modmul_dec from concurrent threads (engine default policy: host products; "
+                        "DDS_PAIR_GPU: one k_pairs launch per burst)",
                 "matches": not bad}
 
-    def native_pairs(self, m, threads, per_thread):
+    def native_pairs(self, m, threads, per_thread, policy=None):
         """The same /Sum load from native threads (tools/native/pair_bench: C++ std::threads calling
         dds_pair_modmul_dec, no interpreter lock), as the JVM's ForkJoin pool would (DDSRestServer.scala:21).
-        Runs as a child process on the same GPU; its samples are checked here with Python ints."""
+        Runs as a child process on the same GPU; its samples are checked here with Python ints. policy:
+        the context's serving policy (DDSHE_PAIR_POLICY; None: the engine default)."""
         exe = os.path.join(ROOT, "tools", "native", "pair_bench")
         if not os.path.exists(exe):
             return {"skipped": "tools/native/pair_bench not built"}
         import subprocess
-        pr = subprocess.run([exe, str(m), str(threads), str(per_thread)], capture_output=True, text=True, timeout=300)
+        env = dict(os.environ)
+        if policy is not None:
+            env["DDSHE_PAIR_POLICY"] = str(policy)
+        pr = subprocess.run([exe, str(m), str(threads), str(per_thread)], capture_output=True, text=True, timeout=300,
+                            env=env)
         if pr.returncode != 0:
             return {"error": pr.stderr[-400:]}
         res = json.loads(pr.stdout.strip().splitlines()[-1])

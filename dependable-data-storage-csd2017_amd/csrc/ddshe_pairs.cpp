@@ -60,7 +60,7 @@ int pair_policy(dds_ctx* ctx) {
   if (p >= 0) return p;
   static const int dflt = [] {
     const char* e = getenv("DDSHE_PAIR_POLICY");
-    return e ? atoi(e) : DDS_PAIR_LONE;
+    return e ? atoi(e) : DDS_PAIR_HOST;
   }();
   return dflt;
 }

@@ -201,9 +201,9 @@ struct RsTile {
   }
 };
 
-// Per-tile digit counts of the scatter's tiles (BLK x kRsItems rows) by HB threads: HB = 64 puts a whole
-// tile on one wave (kRsItems * BLK / 64 rows per lane), so every tile of 10M rows is resident at once
-// instead of 2.4 rounds of 256-thread blocks. The counts do not depend on which lane holds which row.
+// Per-tile digit counts of the scatter's tiles (BLK x kRsItems rows) by HB threads (the counts do not
+// depend on which lane holds which row). HB = 64, a whole tile per wave (every tile of 10M rows resident
+// at once instead of 2.4 rounds of 256-thread blocks), measured slower: 30 -> 43 us on the first pass.
 template <int BLK, int HB>
 __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ keys,
                                                      const uint32_t* __restrict__ ids,
@@ -775,13 +775,8 @@ static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in,
   static const int hpair = order_env("DDSHE_ORDER_HPAIR", 1);
   const bool pairs = hpair && ((uintptr_t)kin & 15) == 0 && (ids_in || !valid || ((uintptr_t)valid & 1) == 0) &&
                      !(last && valid && !kbit);
-  static const int hb = order_env("DDSHE_ORDER_HB", 256);  // threads per histogram block (A/B: 64)
-  if (hb == 64)
-    hipLaunchKernelGGL((k_rs_hist<BLK, 64>), dim3((unsigned)nb), dim3(64), 0, st, kin, ids_in, valid, n, shift, last,
-                       desc, vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs);
-  else
-    hipLaunchKernelGGL((k_rs_hist<BLK, BLK>), dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, last,
-                       desc, vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs);
+  hipLaunchKernelGGL((k_rs_hist<BLK, BLK>), dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, last,
+                     desc, vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs);
   hipLaunchKernelGGL(k_rs_scan, dim3((unsigned)((nb + kScanTiles - 1) / kScanTiles)), dim3(kScanThreads), 0, st, hist,
                      nb, ctot, dtot, tick);
   hipLaunchKernelGGL(k_rs_scatter<BLK>, dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, desc, vbit,
@@ -833,7 +828,9 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   const bool vbit = valid && !kbit && n <= (size_t)kRsLack;
   // executed pass j writes ids to fin when (np-1-j) is even, so the last one lands there; with
   // msd.first set the first pass clears the bucket table and the last fills it (no keys written out)
-  const int keys2 = order_env("DDSHE_ORDER_KEYS2", 0);
+  // the last pass writes the sorted keys too (DDSHE_ORDER_KEYS2=0: k_msd_local gathers its buckets' keys
+  // from the column by id instead: 80 MB less written, but k_msd_local 42 -> 59 us against scatter 76 -> 66)
+  static const int keys2 = order_env("DDSHE_ORDER_KEYS2", 1);
   auto run_passes = [&](const int* shifts, int np, uint32_t* fin, uint32_t* tmp, const MsdRuns& msd) {
     const uint32_t* ids_in = nullptr;  // identity before the first pass
     const uint64_t* kin = (const uint64_t*)col;  // raw column before the first pass
@@ -858,9 +855,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     run_passes(shifts, 2, out_ids, ib, runs);
     hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / 4), dim3(256), 0, st, keys2 ? nullptr : col, desc, kmin, kb, ib,
                        out_ids, runs, mctl, mbig);
-    static const int big_grid = order_env("DDSHE_ORDER_BIGGRID", kMsdBigBlocks);
-    hipLaunchKernelGGL(k_msd_big, dim3((unsigned)std::max(1, big_grid)), dim3(1024), 0, st, kb, ib, out_ids, runs, mctl,
-                       mbig);
+    hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, kb, ib, out_ids, runs, mctl, mbig);
     uint32_t hctl[2];
     if ((e = hipMemcpyAsync(hctl, mctl, sizeof(hctl), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
