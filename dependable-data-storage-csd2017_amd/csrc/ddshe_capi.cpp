@@ -397,17 +397,19 @@ int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const 
     }
   }
   // finalize: the root block writes the result straight into the pinned stage (no copy launch after it)
-  // and then a sequence number the host spins on (the stream's own completion is noticed later by its
-  // next user). Only short folds spin (DDSHE_FOLD_SPIN_ROWS, default 100k rows: ~0.2 ms of device time
-  // at 2048-bit keys): a long fold's caller sleeps on a blocking-sync event instead of holding a core of
-  // the ForkJoin pool the proxy shares between routes (DDSRestServer.scala:21). Timing on:
-  // hipStreamSynchronize.
+  // and then a sequence number the host waits for (the stream's own completion is noticed later by its
+  // next user). Short folds spin on it (DDSHE_FOLD_SPIN_ROWS, default 100k rows: ~0.2 ms of device time
+  // at 2048-bit keys); a longer fold's caller polls it between 50 us sleeps instead of holding a core of
+  // the ForkJoin pool the proxy shares between routes (DDSRestServer.scala:21) for the whole fold (an
+  // event made with hipEventBlockingSync measured no different from a spin on ROCm 7: its
+  // hipEventSynchronize took the 10M-row fold's 14.5 ms of host CPU). Timing on: hipStreamSynchronize.
   static const size_t spin_rows = [] {
     const char* e = getenv("DDSHE_FOLD_SPIN_ROWS");
     return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)100000;
   }();
   const bool timing = ctx->timing.load();
-  const bool spin = finalize && !timing && lv.rows <= spin_rows;
+  const bool spin = finalize && !timing;
+  const bool nap = spin && lv.rows > spin_rows;
   volatile uint32_t* dflag = nullptr;
   uint32_t seq = 0;
   if (spin) {
@@ -425,19 +427,19 @@ int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const 
     return DDS_OK;
   }
   if (spin) {
-    // bounded: past 50 ms (a loaded GPU, a fault) the stream synchronisation decides
+    // bounded: past 50 ms of spinning, or 60 s of naps (a loaded GPU, a fault), the stream
+    // synchronisation decides
     const auto t0 = std::chrono::steady_clock::now();
+    const auto limit = nap ? std::chrono::milliseconds(60000) : std::chrono::milliseconds(50);
     while (*dflag != seq) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+      if (std::chrono::steady_clock::now() - t0 > limit) {
         HIP_TRY(hipStreamSynchronize(st));
         break;
       }
-      __builtin_ia32_pause();
+      if (nap) std::this_thread::sleep_for(std::chrono::microseconds(50));
+      else __builtin_ia32_pause();
     }
     std::atomic_thread_fence(std::memory_order_acquire);
-  } else if (!timing) {
-    HIP_TRY(hipEventRecord(w->ev_block, st));
-    HIP_TRY(hipEventSynchronize(w->ev_block));
   } else {
     HIP_TRY(hipStreamSynchronize(st));
   }

@@ -107,7 +107,6 @@ struct Worker {
   bool ctr_zero = false;
   DevBuf rstick;  // the OPE sort's scan tickets (ensure_zeroed; left at zero by the sort)
   hipEvent_t ev_done = {};
-  hipEvent_t ev_block = {};  // hipEventBlockingSync: the host sleeps on long folds instead of spinning
   DevBuf crt[7];  // CRT encryption scratch (see encrypt_crt_device)
   hipEvent_t ev[4] = {};
   // decimal codec: double-buffered pinned chunks (chars, offsets), their device copies,
@@ -133,7 +132,6 @@ struct Worker {
       if (e) (void)hipEventDestroy(e);
     if (ev_peer) (void)hipEventDestroy(ev_peer);
     if (ev_done) (void)hipEventDestroy(ev_done);
-    if (ev_block) (void)hipEventDestroy(ev_block);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -386,8 +384,7 @@ inline int new_worker(dds_ctx* ctx, Worker** out) {
   for (auto& e : nw->ev_dec)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(DDS_E_HIP, "hipEventCreate");
   if (hipEventCreateWithFlags(&nw->ev_peer, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&nw->ev_done, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&nw->ev_block, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess)
+      hipEventCreateWithFlags(&nw->ev_done, hipEventDisableTiming) != hipSuccess)
     return fail(DDS_E_HIP, "hipEventCreate");
   std::lock_guard<std::mutex> lk(ctx->mu);
   *out = nw.get();
