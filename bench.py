@@ -1030,6 +1030,13 @@ class EncryptSumWorkload(_Workload):
                 roof["traffic_unit"] = (f"HBM bytes per k_modexp_ladder<112,4,28> dispatch (PMC, profiles/{PMC_FILE});"
                                         " the per-row window tables are streamed from HBM")
                 roof["traffic_rows_per_dispatch"] = self.mine
+            sf = os.path.join(ROOT, "profiles", "r05_pmc_enc_ladder.json")
+            if os.path.exists(sf):  # the same kernel's wait counters: what the ladder waits on
+                dv = json.load(open(sf))["dispatches"][0]["derived"]
+                roof["stall_pmc"] = {k: dv[k] for k in ("hbm_GBps", "waitcnt_share_of_wave_cycles",
+                                                        "issue_stall_share_of_wave_cycles",
+                                                        "valu_active_share_of_wave_cycles")}
+                roof["stall_pmc"]["source"] = "profiles/r05_pmc_enc_ladder.json"
         cpu = None
         if self.world == 1 and not a.no_cpu_baseline:
             cpu = cpu_encrypt_baseline(k, self.rcol, self.ms, a.cpu_seconds, self.out)

@@ -295,14 +295,23 @@ __global__ void __launch_bounds__(kScanThreads) k_rs_scan(uint32_t* __restrict__
   const int d = threadIdx.x;
   const size_t t0 = (size_t)blockIdx.x * kScanTiles, nch = gridDim.x;
   if (d < kRsDigits) {
-    uint32_t v[kScanTiles];
-#pragma unroll
-    for (int r = 0; r < kScanTiles; ++r) v[r] = t0 + r < nblocks ? hist[(t0 + r) * kRsDigits + d] : 0u;
+    uint32_t* p = hist + t0 * kRsDigits + d;
     uint32_t run = 0;
+    if (t0 + kScanTiles <= nblocks) {  // a whole chunk: all loads in flight, no bound checks
+      uint32_t v[kScanTiles];
 #pragma unroll
-    for (int r = 0; r < kScanTiles; ++r) {
-      if (t0 + r < nblocks) hist[(t0 + r) * kRsDigits + d] = run;
-      run += v[r];
+      for (int r = 0; r < kScanTiles; ++r) v[r] = p[r * kRsDigits];
+#pragma unroll
+      for (int r = 0; r < kScanTiles; ++r) {
+        p[r * kRsDigits] = run;
+        run += v[r];
+      }
+    } else {
+      for (size_t r = 0; t0 + r < nblocks; ++r) {
+        const uint32_t v = p[r * kRsDigits];
+        p[r * kRsDigits] = run;
+        run += v;
+      }
     }
     __hip_atomic_store(ctot + (size_t)blockIdx.x * kRsDigits + d, run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -312,17 +321,22 @@ __global__ void __launch_bounds__(kScanThreads) k_rs_scan(uint32_t* __restrict__
   __syncthreads();
   if (!s_go || d >= kRsDigits) return;
   uint32_t run = 0;
-  for (size_t c0 = 0; c0 < nch; c0 += 16) {
-    uint32_t v[16];
+  uint32_t* p = ctot + d;
+  size_t c0 = 0;
+  for (; c0 + 32 <= nch; c0 += 32, p += 32 * kRsDigits) {  // 32 loads in flight per round
+    uint32_t v[32];
 #pragma unroll
-    for (int q = 0; q < 16; ++q)
-      v[q] = c0 + q < nch ? __hip_atomic_load(ctot + (c0 + q) * kRsDigits + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                          : 0u;
+    for (int q = 0; q < 32; ++q) v[q] = __hip_atomic_load(p + q * kRsDigits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      if (c0 + q < nch) ctot[(c0 + q) * kRsDigits + d] = run;  // read by the scatter (next launch)
+    for (int q = 0; q < 32; ++q) {
+      p[q * kRsDigits] = run;  // read by the scatter (next launch)
       run += v[q];
     }
+  }
+  for (; c0 < nch; ++c0, p += kRsDigits) {
+    const uint32_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *p = run;
+    run += v;
   }
   dtot[d] = run;
   if (d == 0) *tick = 0u;  // every chunk has taken its ticket
