@@ -1,9 +1,11 @@
 // Host-side multiprecision helpers for the C-ABI boundary.
 //
-// Used only for per-modulus constants (n', R mod N, R^2 mod N, R^k mod N) and for
+// Used for per-modulus constants (n', R mod N, R^2 mod N, R^k mod N, Barrett mu), for
 // the boundary codecs the JVM side would otherwise do (BigInteger.toByteArray /
-// new BigInteger(String), DDSRestServer.scala:417,419,422). No per-row
-// arithmetic of the hot path runs here: that is on the GPU.
+// new BigInteger(String), DDSRestServer.scala:417,419,422), and for the single product
+// of a pairwise /Sum or /Mult request (barrett64_modmul, ddshe_pairs.cpp).
+// No per-row arithmetic of the folds, filters, encryption or ordering runs here: that is on
+// the GPU.
 #pragma once
 #include <cstdio>
 #include <stdint.h>
