@@ -210,7 +210,8 @@ __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ key
                                                      const uint8_t* __restrict__ valid, size_t n, int shift,
                                                      bool last, int desc, bool vbit, bool kbit, uint64_t kmin,
                                                      uint32_t* __restrict__ hist, size_t nblocks,
-                                                     uint32_t* __restrict__ clr, uint32_t nclr, bool pairs) {
+                                                     uint32_t* __restrict__ clr, uint32_t nclr, bool pairs,
+                                                     const uint32_t* __restrict__ khi) {
   constexpr size_t kRows = RsTile<BLK>::kRows;
   constexpr int kIt = (int)(kRows / HB);  // rows per thread
   __shared__ uint32_t cnt[kRsDigits];
@@ -228,7 +229,26 @@ __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ key
   uint64_t key[kIt];
   uint32_t id[kIt];
   size_t rix[kIt];
-  if (pairs) {
+  if (khi) {
+    // split keys (the MSD path's last pass, digit and validity bits >= 32): only the high words, four rows
+    // per 16-byte load; an unaligned tail row by row
+    const size_t nq = n / 4;
+#pragma unroll
+    for (int k = 0; k < kIt / 4; ++k) {
+      const size_t q = (size_t)blockIdx.x * (kRows / 4) + (size_t)k * HB + threadIdx.x;
+      uint4 h = nq ? reinterpret_cast<const uint4*>(khi)[min(q, nq - 1)] : make_uint4(0, 0, 0, 0);
+      const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const size_t r = 4 * q + e;
+        uint32_t w = hw[e];
+        if (q >= nq && r < n) w = khi[r];  // the last n % 4 rows
+        key[4 * k + e] = (uint64_t)w << 32;
+        id[4 * k + e] = 0u;
+        rix[4 * k + e] = r;
+      }
+    }
+  } else if (pairs) {
     // 16-byte key pairs (a wave instruction reads 1 KiB): pair q = 2 rows; an odd last row on its own.
     // keys 16-byte aligned, valid 2-byte aligned, no id needed (host-checked)
     const size_t np = n / 2;
@@ -373,7 +393,9 @@ __global__ void __launch_bounds__(BLK) k_rs_scatter(const uint64_t* __restrict__
                                                          const uint32_t* __restrict__ ctot,
                                                          const uint32_t* __restrict__ dtot, size_t nblocks,
                                                          uint64_t* __restrict__ keys_out,
-                                                         uint32_t* __restrict__ ids_out, int xcd, MsdRuns runs) {
+                                                         uint32_t* __restrict__ ids_out, int xcd, MsdRuns runs,
+                                                         const uint32_t* __restrict__ khi,
+                                                         uint32_t* __restrict__ khi_out) {
   const size_t tile = rs_tile(nblocks, xcd);
   using T = RsTile<BLK>;
   constexpr int W = T::kWaves;
@@ -415,7 +437,10 @@ __global__ void __launch_bounds__(BLK) k_rs_scatter(const uint64_t* __restrict__
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {  // all loads first, unconditional (index clamped), masked below
     const size_t i = min(T::row(tile, wid, k, lane), n - 1);
-    key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc, kmin, kbit);  // first pass: keys = the column
+    if (khi)  // split keys: high words + low words (keys points at the low words)
+      key[k] = ((uint64_t)khi[i] << 32) | reinterpret_cast<const uint32_t*>(keys)[i];
+    else
+      key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc, kmin, kbit);  // first pass: keys = the column
     id[k] = rs_load_id(ids, i, valid, vbit);  // ids == nullptr: first executed pass, identity
   }
 #pragma unroll
@@ -478,7 +503,13 @@ __global__ void __launch_bounds__(BLK) k_rs_scatter(const uint64_t* __restrict__
   for (uint32_t q = threadIdx.x; q < rows; q += BLK) {
     const uint32_t d = sdig[q];
     const uint32_t dst = dbase[d] + (q - lstart[d]);
-    if (keys_out) keys_out[dst] = skey[q];
+    if (khi_out) {  // split: high and low words to their own arrays (keys_out points at the low words)
+      const uint64_t kk = skey[q];
+      khi_out[dst] = (uint32_t)(kk >> 32);
+      reinterpret_cast<uint32_t*>(keys_out)[dst] = (uint32_t)kk;
+    } else if (keys_out) {
+      keys_out[dst] = skey[q];
+    }
     ids_out[dst] = sid[q];
     // bucket runs (last pass of the MSD path; rows lacking the position sit in digit 256 / 0: skipped)
     if (runs.first && !(valid && d == (desc ? 256u : 0u))) {
@@ -782,7 +813,7 @@ template <int BLK>
 static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in, const uint8_t* valid, size_t n,
                     int shift, bool last, int desc, bool vbit, bool kbit, uint64_t kmin, uint32_t* hist,
                     uint32_t* ctot, uint32_t* dtot, uint64_t* kout, uint32_t* ids_out, uint32_t* clr,
-                    const MsdRuns& runs, uint32_t* tick) {
+                    const MsdRuns& runs, uint32_t* tick, const uint32_t* khi = nullptr, uint32_t* khi_out = nullptr) {
   const size_t nb = (n + RsTile<BLK>::kRows - 1) / RsTile<BLK>::kRows;
   // 16-byte key pairs for the counts: aligned keys (and valid bytes when the first pass reads them), no
   // id read (DDSHE_ORDER_HPAIR=0: one row per lane, A/B)
@@ -790,11 +821,11 @@ static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in,
   const bool pairs = hpair && ((uintptr_t)kin & 15) == 0 && (ids_in || !valid || ((uintptr_t)valid & 1) == 0) &&
                      !(last && valid && !kbit);
   hipLaunchKernelGGL((k_rs_hist<BLK, BLK>), dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, last,
-                     desc, vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs);
+                     desc, vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs && !khi, khi);
   hipLaunchKernelGGL(k_rs_scan, dim3((unsigned)((nb + kScanTiles - 1) / kScanTiles)), dim3(kScanThreads), 0, st, hist,
                      nb, ctot, dtot, tick);
   hipLaunchKernelGGL(k_rs_scatter<BLK>, dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, desc, vbit,
-                     kbit, last, kmin, hist, ctot, dtot, nb, kout, ids_out, order_xcd(), runs);
+                     kbit, last, kmin, hist, ctot, dtot, nb, kout, ids_out, order_xcd(), runs, khi, khi_out);
 }
 
 size_t rs_tick_words(size_t) { return 1; }
@@ -845,17 +876,23 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   // the last pass writes the sorted keys too (DDSHE_ORDER_KEYS2=0: k_msd_local gathers its buckets' keys
   // from the column by id instead: 80 MB less written, but k_msd_local 42 -> 59 us against scatter 76 -> 66)
   static const int keys2 = order_env("DDSHE_ORDER_KEYS2", 1);
+  // the MSD path's first pass writes its keys as high and low 32-bit words in two arrays (the first n
+  // words of ka: low, the next n: high) when the last pass's digit and the validity bit are in the high
+  // words (span >= 2^40): the last histogram then reads 4 B per row (DDSHE_ORDER_SPLIT=0: 8 B, A/B)
+  static const int split_env = order_env("DDSHE_ORDER_SPLIT", 1);
   auto run_passes = [&](const int* shifts, int np, uint32_t* fin, uint32_t* tmp, const MsdRuns& msd) {
     const uint32_t* ids_in = nullptr;  // identity before the first pass
     const uint64_t* kin = (const uint64_t*)col;  // raw column before the first pass
     uint64_t* kout = ka;
     const MsdRuns none{};
+    const bool split = msd.first && np == 2 && split_env && (!valid || kbit) && shifts[1] >= 32;
+    uint32_t* hi = split ? reinterpret_cast<uint32_t*>(ka) + n : nullptr;  // ka = [low n words | high n words]
     for (int j = 0; j < np; ++j) {
       uint32_t* ids_out = ((np - 1 - j) % 2 == 0) ? fin : tmp;
       const bool last = j == np - 1;
       rs_pass<256>(st, kin, ids_in, valid, n, shifts[j], last, desc, vbit, kbit, kmin, hist, ctot, dtot,
                    last ? (msd.first && keys2 ? kout : nullptr) : kout, ids_out, j == 0 ? msd.first : nullptr,
-                   last ? msd : none, tick);
+                   last ? msd : none, tick, j == 1 ? hi : nullptr, j == 0 ? hi : nullptr);
       kin = kout;
       kout = kout == ka ? kb : ka;
       ids_in = ids_out;
