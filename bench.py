@@ -751,7 +751,7 @@ def order_pmc_traffic():
     one raw call (k_rs_prep + k_rs_red once) and the resident line's calls (no prep), so the other
     kernels' bytes are divided by the calls (one k_msd_bounds dispatch per call)."""
     once = pmc_traffic("order", ("k_rs_prep", "k_rs_red"), per_step=True)
-    rest = pmc_traffic("order", ("k_rs_hist<256>", "k_rs_scan", "k_rs_scatter<256>", "k_msd_local", "k_msd_big"),
+    rest = pmc_traffic("order", ("k_rs_hist<256>", "k_rs_scan_tiles", "k_rs_scan_chunks", "k_rs_scatter<256>", "k_msd_local", "k_msd_big"),
                        per_step=True)
     calls = (pmc_entry(["order"], "k_msd_local") or (None, 0))[1]
     if once is None or rest is None or not calls:
@@ -1090,7 +1090,7 @@ class OrderWorkload(_Workload):
                 print("VERIFY FAILED", file=sys.stderr)
         step_s = elapsed / a.steps
         alg = 13 * self.mine  # read key + valid byte, write one row id
-        roof = {"bound": "hbm", "kernel": "k_rs_prep + 2 LSD passes over the top 16 bits of the key span (k_rs_hist/k_rs_scan/"
+        roof = {"bound": "hbm", "kernel": "k_rs_prep + 2 LSD passes over the top 16 bits of the key span (k_rs_hist/k_rs_scan_tiles/k_rs_scan_chunks/"
                 "k_rs_scatter; the last scatter also fills the bucket table) + k_msd_local/k_msd_big (in-bucket order "
                 "of the buckets holding two distinct keys)",
                 "achieved": alg / step_s / 1e9, "peak": 8000.0, "unit": "GB/s", "frac": alg / step_s / 1e9 / 8000.0,

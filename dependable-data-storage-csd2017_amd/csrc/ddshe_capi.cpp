@@ -2383,9 +2383,7 @@ int dds_ope_order_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_va
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
     HIP_TRY(w->tab.ensure(rs_scratch_bytes(n)));
-    HIP_TRY(ensure_zeroed(w->rstick, rs_tick_words(n) * 4, wl.st));
-    HIP_TRY(launch_ope_order(d_col, d_valid, n, descending ? 1 : 0, w->tab.p, w->rstick.as<uint32_t>(), d_out_idx,
-                             wl.st));
+    HIP_TRY(launch_ope_order(d_col, d_valid, n, descending ? 1 : 0, w->tab.p, d_out_idx, wl.st));
     HIP_TRY(hipStreamSynchronize(wl.st));
     return DDS_OK;
   } catch (const std::bad_alloc&) {
@@ -2408,9 +2406,8 @@ int dds_ope_order(dds_ctx* ctx, const int64_t* col, const uint8_t* valid, size_t
     HIP_TRY(hipMemcpyAsync(w->in.p, col, n * 8, hipMemcpyHostToDevice, wl.st));
     if (valid) HIP_TRY(hipMemcpyAsync(w->in2.p, valid, n, hipMemcpyHostToDevice, wl.st));
     HIP_TRY(w->tab.ensure(rs_scratch_bytes(n)));
-    HIP_TRY(ensure_zeroed(w->rstick, rs_tick_words(n) * 4, wl.st));
     HIP_TRY(launch_ope_order(w->in.as<int64_t>(), valid ? w->in2.as<uint8_t>() : nullptr, n, descending ? 1 : 0,
-                             w->tab.p, w->rstick.as<uint32_t>(), w->out.as<uint32_t>(), wl.st));
+                             w->tab.p, w->out.as<uint32_t>(), wl.st));
     HIP_TRY(hipMemcpyAsync(out_idx, w->out.p, n * 4, hipMemcpyDeviceToHost, wl.st));
     HIP_TRY(hipStreamSynchronize(wl.st));
     return DDS_OK;

@@ -62,15 +62,6 @@ struct DevBuf {
   }
 };
 
-// a device buffer kept at zero between uses (the kernels that count into it reset it themselves):
-// zeroed on the stream when (re)allocated
-inline hipError_t ensure_zeroed(DevBuf& b, size_t bytes, hipStream_t st) {
-  if (bytes <= b.cap) return hipSuccess;
-  hipError_t e = b.ensure(bytes);
-  if (e == hipSuccess) e = hipMemsetAsync(b.p, 0, b.cap, st);
-  return e;
-}
-
 struct HostBuf {  // pinned staging (truly asynchronous H2D)
   void* p = nullptr;
   size_t cap = 0;
@@ -105,7 +96,6 @@ struct Worker {
   // tiles add into it, it is read, then re-zeroed on the stream after the read); ev_done marks the read
   DevBuf ctr;
   bool ctr_zero = false;
-  DevBuf rstick;  // the OPE sort's scan tickets (ensure_zeroed; left at zero by the sort)
   hipEvent_t ev_done = {};
   DevBuf crt[7];  // CRT encryption scratch (see encrypt_crt_device)
   hipEvent_t ev[4] = {};

@@ -143,13 +143,10 @@ hipError_t launch_perm_keep(const uint32_t* perm, const uint8_t* dead, size_t n,
 hipError_t launch_gather_u32(const uint32_t* src, const uint32_t* idx, size_t n, uint32_t* dst, hipStream_t st);
 // OPE ordering (ddshe_sort.hip): stable radix sort of the int64 column -> row ids
 size_t rs_scratch_bytes(size_t n);
-// words of the sort's scan tickets: a device buffer the caller keeps for it, zero before the first
-// call (ensure_zeroed); the sort leaves it at zero
-size_t rs_tick_words(size_t n);
 // ubounds (host, nullable): [lo, hi] of (value ^ 2^63) over a superset of the holders (a resident
 // column tracks them on its writes): no min/max pass over the column and no mid-sort host round trip
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
-                            uint32_t* tick, uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds = nullptr);
+                            uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds = nullptr);
 // deterministic-equality scans (ddshe_strscan.hip)
 // 64-bit digest of an element string (FNV-1a over the bytes, splitmix finaliser); identical on
 // host (needles) and device (table). The table keeps its top 32 bits as a per-element fingerprint.

@@ -623,14 +623,12 @@ int dds_opecol_order(dds_opecol* col, int descending, uint32_t* out_idx, size_t*
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
     HIP_TRY(w->tab.ensure(rs_scratch_bytes(n)));
-    HIP_TRY(ensure_zeroed(w->rstick, rs_tick_words(n) * 4, wl.st));
     HIP_TRY(w->out.ensure(n * 4));
     // the sort's valid test is flag != 0, i.e. kHold (rows lacking the position have no other bit; a
     // removed set's device byte is 0, so it sorts with them)
     const uint64_t ub[2] = {col->ulo, col->uhi};
     record_time(col->ctx, w, wl.st, true, 2);
-    HIP_TRY(launch_ope_order(col->d_val, col->d_flg, n, descending ? 1 : 0, w->tab.p, w->rstick.as<uint32_t>(),
-                             w->out.as<uint32_t>(), wl.st,
+    HIP_TRY(launch_ope_order(col->d_val, col->d_flg, n, descending ? 1 : 0, w->tab.p, w->out.as<uint32_t>(), wl.st,
                              ub));
     const uint32_t* res = w->out.as<uint32_t>();
     size_t m = n;

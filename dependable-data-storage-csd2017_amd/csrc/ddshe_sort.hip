@@ -297,69 +297,65 @@ __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ key
   for (int d = threadIdx.x; d < kRsDigits; d += HB) hist[(size_t)blockIdx.x * kRsDigits + d] = cnt[d];  // 1 KiB, coalesced
 }
 
-// Exclusive scan over tiles per digit: one block per chunk of kScanTiles tiles, one thread per digit
-// (coalesced rows across the digit threads): the chunk's counts are replaced in place by their
-// exclusive prefix within the chunk and the chunk total goes out write-through (sc1) to
-// ctot[chunk][digit]; the last chunk to finish (ticket) then replaces the chunk totals by their
-// exclusive prefix and stores the digit totals to dtot (k_tree's in-kernel hand-off: sc1 stores ->
-// s_waitcnt vmcnt(0) -> barrier -> agent atomic; sc1 loads after the ticket) and puts the ticket back
-// to zero. A tile's offset for digit d is then dbase[d] + ctot[chunk][d] + hist[tile][d].
-// (Round 4 ran the chunk-total scan as a second launch, 6 us per pass; doing both scans inside the
-// histogram kernel's last blocks instead made it 2x slower: every block then waits for its
-// write-through row before its ticket.)
 constexpr int kScanThreads = 320;  // >= kRsDigits
-__global__ void __launch_bounds__(kScanThreads) k_rs_scan(uint32_t* __restrict__ hist, size_t nblocks,
-                                                          uint32_t* __restrict__ ctot, uint32_t* __restrict__ dtot,
-                                                          uint32_t* __restrict__ tick) {
-  __shared__ int s_go;
+// Exclusive scan over tiles per digit, in two launches: k_rs_scan_tiles, one block per chunk of
+// kScanTiles tiles and one thread per digit (coalesced rows across the digit threads), replaces the
+// chunk's counts by their exclusive prefix within the chunk and stores the chunk total to
+// ctot[chunk][digit]; k_rs_scan_chunks, one block, replaces the chunk totals by their exclusive prefix
+// and stores the digit totals to dtot. A tile's offset for digit d is then dbase[d] + ctot[chunk][d] +
+// hist[tile][d]. One launch instead (the chunks' last block scanning the totals after a ticket, with
+// write-through chunk totals) measured slower on one box: 14-18 us against 6.4 + 5.9 us; the scans
+// inside the histogram's last blocks made the histogram 2x slower (every block waits for its
+// write-through row before its ticket).
+__global__ void __launch_bounds__(kScanThreads) k_rs_scan_tiles(uint32_t* __restrict__ hist, size_t nblocks,
+                                                                uint32_t* __restrict__ ctot) {
   const int d = threadIdx.x;
-  const size_t t0 = (size_t)blockIdx.x * kScanTiles, nch = gridDim.x;
-  if (d < kRsDigits) {
-    uint32_t* p = hist + t0 * kRsDigits + d;
-    uint32_t run = 0;
-    if (t0 + kScanTiles <= nblocks) {  // a whole chunk: all loads in flight, no bound checks
-      uint32_t v[kScanTiles];
+  if (d >= kRsDigits) return;
+  const size_t t0 = (size_t)blockIdx.x * kScanTiles;
+  uint32_t* p = hist + t0 * kRsDigits + d;
+  uint32_t run = 0;
+  if (t0 + kScanTiles <= nblocks) {
+    uint32_t v[kScanTiles];
 #pragma unroll
-      for (int r = 0; r < kScanTiles; ++r) v[r] = p[r * kRsDigits];
+    for (int r = 0; r < kScanTiles; ++r) v[r] = p[r * kRsDigits];
 #pragma unroll
-      for (int r = 0; r < kScanTiles; ++r) {
-        p[r * kRsDigits] = run;
-        run += v[r];
-      }
-    } else {
-      for (size_t r = 0; t0 + r < nblocks; ++r) {
-        const uint32_t v = p[r * kRsDigits];
-        p[r * kRsDigits] = run;
-        run += v;
-      }
+    for (int r = 0; r < kScanTiles; ++r) {
+      p[r * kRsDigits] = run;
+      run += v[r];
     }
-    __hip_atomic_store(ctot + (size_t)blockIdx.x * kRsDigits + d, run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    for (size_t r = 0; t0 + r < nblocks; ++r) {
+      const uint32_t v = p[r * kRsDigits];
+      p[r * kRsDigits] = run;
+      run += v;
+    }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (d == 0) s_go = __hip_atomic_fetch_add(tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nch - 1;
-  __syncthreads();
-  if (!s_go || d >= kRsDigits) return;
+  ctot[(size_t)blockIdx.x * kRsDigits + d] = run;
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_rs_scan_chunks(uint32_t* __restrict__ ctot, size_t nchunks,
+                                                                 uint32_t* __restrict__ dtot) {
+  const int d = threadIdx.x;
+  if (d >= kRsDigits) return;
   uint32_t run = 0;
   uint32_t* p = ctot + d;
   size_t c0 = 0;
-  for (; c0 + 32 <= nch; c0 += 32, p += 32 * kRsDigits) {  // 32 loads in flight per round
+  for (; c0 + 32 <= nchunks; c0 += 32, p += 32 * kRsDigits) {
     uint32_t v[32];
 #pragma unroll
-    for (int q = 0; q < 32; ++q) v[q] = __hip_atomic_load(p + q * kRsDigits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int q = 0; q < 32; ++q) v[q] = p[q * kRsDigits];
 #pragma unroll
     for (int q = 0; q < 32; ++q) {
-      p[q * kRsDigits] = run;  // read by the scatter (next launch)
+      p[q * kRsDigits] = run;
       run += v[q];
     }
   }
-  for (; c0 < nch; ++c0, p += kRsDigits) {
-    const uint32_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (; c0 < nchunks; ++c0, p += kRsDigits) {
+    const uint32_t v = *p;
     *p = run;
     run += v;
   }
   dtot[d] = run;
-  if (d == 0) *tick = 0u;  // every chunk has taken its ticket
 }
 
 // Tile counts are tile-major (hist[tile][digit]: each histogram block writes 1 KiB in one go; the
@@ -813,7 +809,7 @@ template <int BLK>
 static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in, const uint8_t* valid, size_t n,
                     int shift, bool last, int desc, bool vbit, bool kbit, uint64_t kmin, uint32_t* hist,
                     uint32_t* ctot, uint32_t* dtot, uint64_t* kout, uint32_t* ids_out, uint32_t* clr,
-                    const MsdRuns& runs, uint32_t* tick, const uint32_t* khi = nullptr, uint32_t* khi_out = nullptr) {
+                    const MsdRuns& runs, const uint32_t* khi = nullptr, uint32_t* khi_out = nullptr) {
   const size_t nb = (n + RsTile<BLK>::kRows - 1) / RsTile<BLK>::kRows;
   // 16-byte key pairs for the counts: aligned keys (and valid bytes when the first pass reads them), no
   // id read (DDSHE_ORDER_HPAIR=0: one row per lane, A/B)
@@ -822,16 +818,15 @@ static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in,
                      !(last && valid && !kbit);
   hipLaunchKernelGGL((k_rs_hist<BLK, BLK>), dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, last,
                      desc, vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs && !khi, khi);
-  hipLaunchKernelGGL(k_rs_scan, dim3((unsigned)((nb + kScanTiles - 1) / kScanTiles)), dim3(kScanThreads), 0, st, hist,
-                     nb, ctot, dtot, tick);
+  const size_t nch = (nb + kScanTiles - 1) / kScanTiles;
+  hipLaunchKernelGGL(k_rs_scan_tiles, dim3((unsigned)nch), dim3(kScanThreads), 0, st, hist, nb, ctot);
+  hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nch, dtot);
   hipLaunchKernelGGL(k_rs_scatter<BLK>, dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, desc, vbit,
                      kbit, last, kmin, hist, ctot, dtot, nb, kout, ids_out, order_xcd(), runs, khi, khi_out);
 }
 
-size_t rs_tick_words(size_t) { return 1; }
-
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
-                            uint32_t* tick, uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds) {
+                            uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds) {
   if (n == 0) return hipSuccess;
   const size_t nb = rs_blocks(n);
   uint64_t* ka = (uint64_t*)scratch;
@@ -892,7 +887,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
       const bool last = j == np - 1;
       rs_pass<256>(st, kin, ids_in, valid, n, shifts[j], last, desc, vbit, kbit, kmin, hist, ctot, dtot,
                    last ? (msd.first && keys2 ? kout : nullptr) : kout, ids_out, j == 0 ? msd.first : nullptr,
-                   last ? msd : none, tick, j == 1 ? hi : nullptr, j == 0 ? hi : nullptr);
+                   last ? msd : none, j == 1 ? hi : nullptr, j == 0 ? hi : nullptr);
       kin = kout;
       kout = kout == ka ? kb : ka;
       ids_in = ids_out;
