@@ -1250,7 +1250,14 @@ class EntrySearchWorkload(_Workload):
         alg = (alg_or + alg_eq) / 2
         roof = {"bound": "hbm", "kernel": "k_str_any + k_byte_count/k_ope_scatter (OR), k_str_eq_count + k_ope_scatter (Eq); device time",
                 "achieved": alg / scan_s / 1e9, "peak": 8000.0, "unit": "GB/s", "frac": alg / scan_s / 1e9 / 8000.0,
-                "avg_scan_ms": scan_s * 1e3, "algorithmic_bytes": alg, "traffic": None}
+                "avg_scan_ms": scan_s * 1e3, "algorithmic_bytes": alg,
+                # HBM bytes per scan from the PMC pass (per dispatch): OR = k_str_any + k_byte_count +
+                # k_ope_scatter, Eq = k_str_eq_count + k_ope_scatter, averaged over the two scans like alg
+                "traffic": None, "traffic_unit": "HBM bytes per scan (PMC, profiles/" + PMC_FILE + ")"}
+        t_or = pmc_traffic("entry_search", ("k_str_any", "k_byte_count", "k_ope_scatter"))
+        t_eq = pmc_traffic("entry_search", ("k_str_eq_count", "k_ope_scatter"))
+        if t_or is not None and t_eq is not None:
+            roof["traffic"] = (t_or + t_eq) / 2
         mut = None
         if self.world == 1:  # before the CPU baseline (its 1.6M Python strings slow every later Python call)
             try:

@@ -2,8 +2,8 @@
 # Round-5 profiles (GPU box, repo root: gpurun -- tools/gpurun/profile_r05.sh):
 #   * rocprofv3 kernel stats: the headline with ONE fold size (10M rows, --no-extras), order, product_filter
 #     (Search route), encrypt_sum (config 4) and entry_search;
-#   * PMC HBM-traffic passes (FETCH_SIZE and WRITE_SIZE in separate runs) of sum, order, product_filter and
-#     encrypt_sum (the k_modexp_ladder traffic of config 4's roofline);
+#   * PMC HBM-traffic passes (FETCH_SIZE and WRITE_SIZE in separate runs) of sum, order, product_filter,
+#     entry_search and encrypt_sum (the k_modexp_ladder traffic of config 4's roofline);
 #   * the ladder's issue / wait counters (one SQ + GRBM pass) on encrypt_sum.
 # Outputs under gpurun_out/prof/<name>/; tools/pmc_summary.py and tools/pmc_valu_summary.py make the
 # profiles/ summaries.
@@ -22,6 +22,8 @@ exec tools/gpurun/steps.sh \
   "240 pmc_order_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/pmc_order_write -o run -- $B --workload order --steps 1 --warmup 0 --verify 0" \
   "240 pmc_pf_fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/pmc_pf_fetch -o run -- $B --workload product_filter --steps 1 --warmup 0 --verify 0" \
   "240 pmc_pf_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/pmc_pf_write -o run -- $B --workload product_filter --steps 1 --warmup 0 --verify 0" \
+  "240 pmc_es_fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/pmc_es_fetch -o run -- $B --workload entry_search --steps 1 --warmup 0 --verify 0" \
+  "240 pmc_es_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/pmc_es_write -o run -- $B --workload entry_search --steps 1 --warmup 0 --verify 0" \
   "300 pmc_enc_fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/pmc_enc_fetch -o run -- $B --workload encrypt_sum --steps 1 --warmup 0 --verify 0" \
   "300 pmc_enc_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/pmc_enc_write -o run -- $B --workload encrypt_sum --steps 1 --warmup 0 --verify 0" \
   "300 pmc_enc_stall rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM GRBM_GUI_ACTIVE --output-format csv -d $P/pmc_enc_stall -o run -- $B --workload encrypt_sum --steps 1 --warmup 0 --verify 0"

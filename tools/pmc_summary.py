@@ -14,7 +14,7 @@ import os
 import re
 import sys
 
-WORKLOADS = {"pf": "product_filter", "order": "order", "sum": "sum", "enc": "encrypt_sum"}
+WORKLOADS = {"pf": "product_filter", "order": "order", "sum": "sum", "enc": "encrypt_sum", "es": "entry_search"}
 
 
 def short(name):
