@@ -610,7 +610,8 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
   const size_t crows = std::min(kDecChunkRows, std::max<size_t>(4096, (count + 1) / 2));
   bool used[2] = {false, false};
   int slot = 0;
-  std::vector<size_t> lens;
+  std::unique_ptr<uint32_t[]> lens;  // String[] rows: lens[i] valid for i < lens_hi (uninitialised beyond)
+  size_t lens_hi = 0;
   for (size_t b = 0; b < count;) {
     if (used[slot]) HIP_TRY(hipEventSynchronize(w->ev_copy[slot]));  // the H2D out of this host slot is done
     HIP_TRY(w->hch[slot].ensure(kDecChunkBytes + 64));
@@ -636,22 +637,30 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
     }
     if (src.strs && std::min(count - b, crows) >= 1024) {
       // NUL-terminated rows (JNA String[]): lengths and copies spread over the host pool; the
-      // chunk cut and the offsets are one sequential pass over the lengths
+      // chunk cut and the offsets are one sequential pass over the lengths. Lengths are measured
+      // in blocks as the cut reaches them and kept for the next chunk (a chunk ends on its byte
+      // budget long before crows rows of ciphertext text: measuring [b, b + crows) per chunk read
+      // every row ~5 times for 4096-bit rows)
       const size_t hi = std::min(count, b + crows);
-      lens.resize(hi - b);
-      CopyPool::get().parallel_for(hi - b, 1024, [&](size_t x, size_t y) {
-        for (size_t i = x; i < y; ++i) lens[i] = strlen(src.strs[b + i]);
-      });
+      if (!lens) lens.reset(new uint32_t[count]);
       while (e < hi) {
-        const size_t n = lens[e - b] > kDecChunkBytes - 64 ? 1 : lens[e - b];
+        if (e == lens_hi) {
+          const size_t lb = lens_hi, le = std::min(count, lb + kDecLenBlock);
+          CopyPool::get().parallel_for(le - lb, 256, [&](size_t x, size_t y) {
+            for (size_t i = lb + x; i < lb + y; ++i)  // past the chunk budget: a long row either way
+              lens[i] = (uint32_t)std::min<size_t>(strlen(src.strs[i]), kDecChunkBytes);
+          });
+          lens_hi = le;
+        }
+        const size_t n = lens[e] > kDecChunkBytes - 64 ? 1 : lens[e];
         if (pos + n > kDecChunkBytes) break;
-        if (n != lens[e - b]) long_rows->push_back(e);
+        if (n != lens[e]) long_rows->push_back(e);
         pos += n;
         o[++e - b] = pos;
       }
       CopyPool::get().parallel_for(e - b, 256, [&](size_t x, size_t y) {
         for (size_t i = x; i < y; ++i)
-          memcpy(dst + o[i], o[i + 1] - o[i] == lens[i] ? src.strs[b + i] : "0", o[i + 1] - o[i]);
+          memcpy(dst + o[i], o[i + 1] - o[i] == lens[b + i] ? src.strs[b + i] : "0", o[i + 1] - o[i]);
       });
     }
     while (e < count && e - b < crows) {

@@ -518,6 +518,7 @@ struct DecRows {
 
 constexpr size_t kDecChunkBytes = (size_t)64 << 20;  // chars per pinned chunk
 constexpr size_t kDecChunkRows = (size_t)1 << 18;
+constexpr size_t kDecLenBlock = (size_t)1 << 14;  // String[] rows measured per host-pool pass
 
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // rows of one rW matrix of this modulus' shape must stay addressable by the kernels (max_stride)
