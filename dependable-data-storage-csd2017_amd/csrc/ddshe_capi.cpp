@@ -2392,7 +2392,9 @@ int dds_ope_order_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_va
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
     HIP_TRY(w->tab.ensure(rs_scratch_bytes(n)));
-    HIP_TRY(launch_ope_order(d_col, d_valid, n, descending ? 1 : 0, w->tab.p, d_out_idx, wl.st));
+    OrderHostWords ow;
+    HIP_TRY(order_words(w, &ow));
+    HIP_TRY(launch_ope_order(d_col, d_valid, n, descending ? 1 : 0, w->tab.p, d_out_idx, wl.st, nullptr, &ow));
     HIP_TRY(hipStreamSynchronize(wl.st));
     return DDS_OK;
   } catch (const std::bad_alloc&) {
@@ -2415,8 +2417,10 @@ int dds_ope_order(dds_ctx* ctx, const int64_t* col, const uint8_t* valid, size_t
     HIP_TRY(hipMemcpyAsync(w->in.p, col, n * 8, hipMemcpyHostToDevice, wl.st));
     if (valid) HIP_TRY(hipMemcpyAsync(w->in2.p, valid, n, hipMemcpyHostToDevice, wl.st));
     HIP_TRY(w->tab.ensure(rs_scratch_bytes(n)));
+    OrderHostWords ow;
+    HIP_TRY(order_words(w, &ow));
     HIP_TRY(launch_ope_order(w->in.as<int64_t>(), valid ? w->in2.as<uint8_t>() : nullptr, n, descending ? 1 : 0,
-                             w->tab.p, w->out.as<uint32_t>(), wl.st));
+                             w->tab.p, w->out.as<uint32_t>(), wl.st, nullptr, &ow));
     HIP_TRY(hipMemcpyAsync(out_idx, w->out.p, n * 4, hipMemcpyDeviceToHost, wl.st));
     HIP_TRY(hipStreamSynchronize(wl.st));
     return DDS_OK;

@@ -106,6 +106,7 @@ struct Worker {
   uint32_t done_seq = 0;  // fold finalize: the last sequence number the root stored at kStageDoneWord
   HostBuf hcnt;    // coherent + mapped: the Search bitmask's per-tile match counts, stored by the device
   HostBuf hpair;   // pairwise batches: operands and results, coherent + mapped (k_pairs_sos reads and writes it)
+  HostBuf hord;    // coherent + mapped: the OPE ordering's bounds / overflow words (OrderHostWords)
   HostBuf hbig;    // large read-backs (Search ids / match masks, Order permutations) before the caller's copy
   DevBuf dch[2], doff[2], rflags;
   hipEvent_t ev_dec[2] = {};
@@ -352,6 +353,15 @@ inline hipError_t stage_ptr(Worker* w, uint32_t** p) {
   return e;
 }
 // copy `bytes` (<= 64) device -> host through the pinned slot and synchronise the stream
+// the worker's OrderHostWords (launch_ope_order's read-back words), allocated on first use
+inline hipError_t order_words(Worker* w, OrderHostWords* ow) {
+  w->hord.flags = hipHostMallocCoherent | hipHostMallocMapped;
+  hipError_t e = w->hord.ensure(64);
+  ow->h = (volatile uint64_t*)w->hord.p;
+  ow->d = (uint64_t*)w->hord.dptr;
+  return e;
+}
+
 inline hipError_t read_sync(Worker* w, hipStream_t st, const void* dsrc, void* dst, size_t bytes) {
   uint32_t* h = nullptr;
   hipError_t e = stage_ptr(w, &h);

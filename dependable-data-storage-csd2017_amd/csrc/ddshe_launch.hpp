@@ -145,8 +145,17 @@ hipError_t launch_gather_u32(const uint32_t* src, const uint32_t* idx, size_t n,
 size_t rs_scratch_bytes(size_t n);
 // ubounds (host, nullable): [lo, hi] of (value ^ 2^63) over a superset of the holders (a resident
 // column tracks them on its writes): no min/max pass over the column and no mid-sort host round trip
+// hw (nullable): 4 words of coherent, device-mapped host memory (h: host address, d: its device address)
+// the ordering stores its small read-backs into (bounds, overflow flag) instead of copying them back; with
+// it, a raw call whose previous raw call had a 40..56-bit key span runs the MSD plan without a mid-sort
+// host round trip (planned on the device, checked after)
+struct OrderHostWords {
+  volatile uint64_t* h;
+  uint64_t* d;
+};
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
-                            uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds = nullptr);
+                            uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds = nullptr,
+                            const OrderHostWords* hw = nullptr);
 // deterministic-equality scans (ddshe_strscan.hip)
 // 64-bit digest of an element string (FNV-1a over the bytes, splitmix finaliser); identical on
 // host (needles) and device (table). The table keeps its top 32 bits as a per-element fingerprint.

@@ -628,8 +628,10 @@ int dds_opecol_order(dds_opecol* col, int descending, uint32_t* out_idx, size_t*
     // removed set's device byte is 0, so it sorts with them)
     const uint64_t ub[2] = {col->ulo, col->uhi};
     record_time(col->ctx, w, wl.st, true, 2);
+    OrderHostWords ow;
+    HIP_TRY(order_words(w, &ow));
     HIP_TRY(launch_ope_order(col->d_val, col->d_flg, n, descending ? 1 : 0, w->tab.p, w->out.as<uint32_t>(), wl.st,
-                             ub));
+                             ub, &ow));
     const uint32_t* res = w->out.as<uint32_t>();
     size_t m = n;
     if (col->ndead) {  // drop removed sets from the permutation, order kept (filter(nonEmpty), :553, :586)

@@ -22,6 +22,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "ddshe_launch.hpp"
 
@@ -144,14 +145,40 @@ __global__ void __launch_bounds__(256) k_rs_prep(const int64_t* __restrict__ col
 }
 
 // min / max of the per-block partials -> red[0..1] (one block; no holder at all: red[0] > red[1])
+// hout (host-mapped, nullable): red[0..1] also stored to host memory (read after the stream synchronises,
+// no copy). spec_lo <= spec_hi: the plan of a speculative MSD call (launch_ope_order) to red[2..3]:
+// red[2] = kmin, red[3] = s1 (the first pass's shift, span bits - 16) when the span has spec_lo..spec_hi
+// bits, else kRsNoPlan (every later kernel of the call then returns at once).
+constexpr uint64_t kRsNoPlan = ~0ull;
 __global__ void __launch_bounds__(1024) k_rs_red(const uint64_t* __restrict__ part, size_t nparts,
-                                                 uint64_t* __restrict__ red) {
+                                                 uint64_t* __restrict__ red, int spec_lo, int spec_hi,
+                                                 uint64_t* __restrict__ hout) {
   uint64_t lo = ~0ull, hi = 0;
   for (size_t i = threadIdx.x; i < nparts; i += 1024) {
     lo = min(lo, part[2 * i]);
     hi = max(hi, part[2 * i + 1]);
   }
   rs_minmax_block(lo, hi, red);
+  if (threadIdx.x == 0) {  // the thread that stored red[0..1]
+    const uint64_t mn = red[0], mx = red[1];
+    if (hout) {
+      hout[0] = mn;
+      hout[1] = mx;
+    }
+    if (spec_lo <= spec_hi) {
+      const uint64_t span = mn <= mx ? mx - mn : 0ull;
+      const int sb = span ? 64 - __builtin_clzll(span) : 0;
+      red[2] = mn <= mx ? mn : 0ull;
+      red[3] = (sb >= spec_lo && sb <= spec_hi) ? (uint64_t)(sb - kMsdBits) : kRsNoPlan;
+    }
+  }
+}
+
+// the end of a call's device work: plan and overflow flag to host memory (one thread)
+__global__ void k_rs_publish(const uint32_t* __restrict__ ctl, const uint64_t* __restrict__ plan,
+                             uint64_t* __restrict__ hout) {
+  hout[2] = ctl[1];  // kMsdCtlOverflow
+  hout[3] = plan ? plan[1] : 0ull;
 }
 
 __global__ void k_rs_iota(uint32_t* __restrict__ ids, size_t n) {
@@ -211,7 +238,14 @@ __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ key
                                                      bool last, int desc, bool vbit, bool kbit, uint64_t kmin,
                                                      uint32_t* __restrict__ hist, size_t nblocks,
                                                      uint32_t* __restrict__ clr, uint32_t nclr, bool pairs,
-                                                     const uint32_t* __restrict__ khi) {
+                                                     const uint32_t* __restrict__ khi,
+                                                     const uint64_t* __restrict__ plan) {
+  if (plan) {  // speculative call: kmin and the shift (relative to s1) from k_rs_red's plan
+    const uint64_t s1 = plan[1];
+    if (s1 == kRsNoPlan) return;
+    kmin = plan[0];
+    shift += (int)s1;
+  }
   constexpr size_t kRows = RsTile<BLK>::kRows;
   constexpr int kIt = (int)(kRows / HB);  // rows per thread
   __shared__ uint32_t cnt[kRsDigits];
@@ -391,7 +425,15 @@ __global__ void __launch_bounds__(BLK) k_rs_scatter(const uint64_t* __restrict__
                                                          uint64_t* __restrict__ keys_out,
                                                          uint32_t* __restrict__ ids_out, int xcd, MsdRuns runs,
                                                          const uint32_t* __restrict__ khi,
-                                                         uint32_t* __restrict__ khi_out) {
+                                                         uint32_t* __restrict__ khi_out,
+                                                         const uint64_t* __restrict__ plan) {
+  if (plan) {
+    const uint64_t s1 = plan[1];
+    if (s1 == kRsNoPlan) return;
+    kmin = plan[0];
+    shift += (int)s1;
+    runs.s1 = (int)s1;
+  }
   const size_t tile = rs_tile(nblocks, xcd);
   using T = RsTile<BLK>;
   constexpr int W = T::kWaves;
@@ -685,7 +727,14 @@ __device__ __forceinline__ void msd_wave_sort(const uint64_t* __restrict__ keys,
 __global__ void __launch_bounds__(256) k_msd_local(const int64_t* __restrict__ col, int desc, uint64_t kmin,
                                                    uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
                                                    uint32_t* __restrict__ ids, MsdRuns runs,
-                                                   uint32_t* __restrict__ ctl, uint32_t* __restrict__ big) {
+                                                   uint32_t* __restrict__ ctl, uint32_t* __restrict__ big,
+                                                   const uint64_t* __restrict__ plan) {
+  if (plan) {
+    const uint64_t s1 = plan[1];
+    if (s1 == kRsNoPlan) return;
+    kmin = plan[0];
+    runs.s1 = (int)s1;
+  }
   const int lane = threadIdx.x & 63;
   {  // one wave per bucket (a grid-stride loop over the buckets measured 34 -> 56 us: the multi-key
      // buckets' rounds serialise within a wave)
@@ -754,7 +803,12 @@ __device__ __forceinline__ void msd_block_sort(const uint64_t* __restrict__ keys
 // workgroup each (grid-stride over the list); larger ones: overflow flag (host falls back to LSD)
 __global__ void __launch_bounds__(1024) k_msd_big(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ src,
                                                   uint32_t* __restrict__ ids, MsdRuns runs, uint32_t* __restrict__ ctl,
-                                                  const uint32_t* __restrict__ big) {
+                                                  const uint32_t* __restrict__ big, const uint64_t* __restrict__ plan) {
+  if (plan) {
+    const uint64_t s1 = plan[1];
+    if (s1 == kRsNoPlan) return;
+    runs.s1 = (int)s1;
+  }
   __shared__ uint64_t xch[kMsdBlockMax];
   const uint32_t nbig = ctl[kMsdCtlBig];
   const uint64_t rmask = (1ull << runs.s1) - 1ull;
@@ -778,7 +832,7 @@ size_t rs_scratch_bytes(size_t n) {
   // MSD bucket starts + control words + big-bucket list
   return 2 * n * 8 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 1024 +
          (size_t)kRsDigits * ((rs_blocks(n) + kScanTiles - 1) / kScanTiles) * 4 + 256 +
-         16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows)) + 768 + (8 * (size_t)kMsdBuckets + 8) * 4;
+         16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows)) + 800 + (8 * (size_t)kMsdBuckets + 8) * 4;
 }
 
 // the MSD path pays off from 4 LSD passes on (a span of > 24 bits) and enough rows to fill the buckets
@@ -809,7 +863,7 @@ template <int BLK>
 static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in, const uint8_t* valid, size_t n,
                     int shift, bool last, int desc, bool vbit, bool kbit, uint64_t kmin, uint32_t* hist,
                     uint32_t* ctot, uint32_t* dtot, uint64_t* kout, uint32_t* ids_out, uint32_t* clr,
-                    const MsdRuns& runs, const uint32_t* khi = nullptr, uint32_t* khi_out = nullptr) {
+                    const MsdRuns& runs, const uint32_t* khi, uint32_t* khi_out, const uint64_t* plan) {
   const size_t nb = (n + RsTile<BLK>::kRows - 1) / RsTile<BLK>::kRows;
   // 16-byte key pairs for the counts: aligned keys (and valid bytes when the first pass reads them), no
   // id read (DDSHE_ORDER_HPAIR=0: one row per lane, A/B)
@@ -817,16 +871,24 @@ static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in,
   const bool pairs = hpair && ((uintptr_t)kin & 15) == 0 && (ids_in || !valid || ((uintptr_t)valid & 1) == 0) &&
                      !(last && valid && !kbit);
   hipLaunchKernelGGL((k_rs_hist<BLK, BLK>), dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, last,
-                     desc, vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs && !khi, khi);
+                     desc, vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs && !khi, khi, plan);
   const size_t nch = (nb + kScanTiles - 1) / kScanTiles;
   hipLaunchKernelGGL(k_rs_scan_tiles, dim3((unsigned)nch), dim3(kScanThreads), 0, st, hist, nb, ctot);
   hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nch, dtot);
   hipLaunchKernelGGL(k_rs_scatter<BLK>, dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, desc, vbit,
-                     kbit, last, kmin, hist, ctot, dtot, nb, kout, ids_out, order_xcd(), runs, khi, khi_out);
+                     kbit, last, kmin, hist, ctot, dtot, nb, kout, ids_out, order_xcd(), runs, khi, khi_out, plan);
 }
 
+// Spans of kSpecLo..kSpecHi bits take the MSD path with split keys and (with a valid array) the key-bit
+// validity; a raw call whose previous raw call had such a span launches that plan right after the
+// min / max pass without reading the bounds back first (speculative: the plan's shifts and kmin come
+// from k_rs_red on the device; another span makes every kernel of the plan return at once and the
+// call continues on the host-planned path from the bounds the same pass stored to host memory).
+constexpr int kSpecLo = 40, kSpecHi = 56;
+static std::atomic<int> g_order_spec{0};
+
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
-                            uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds) {
+                            uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds, const OrderHostWords* hw) {
   if (n == 0) return hipSuccess;
   const size_t nb = rs_blocks(n);
   uint64_t* ka = (uint64_t*)scratch;
@@ -837,7 +899,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   const size_t nch = (nb + kScanTiles - 1) / kScanTiles;
   uint32_t* ctot = (uint32_t*)(((uintptr_t)(dtot + kRsDigits) + 255) & ~(uintptr_t)255);
   uint64_t* red = (uint64_t*)(((uintptr_t)(ctot + (size_t)kRsDigits * nch) + 15) & ~(uintptr_t)15);
-  uint64_t* part = red + 2;
+  uint64_t* part = red + 4;  // red[0..1] min / max, red[2..3] the speculative plan
   const size_t pb = (n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows);
   // MSD bucket table (MsdRuns layout), then the control words and the big-bucket list
   uint32_t* mtab = (uint32_t*)(((uintptr_t)(part + 2 * pb) + 255) & ~(uintptr_t)255);
@@ -845,29 +907,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
                (unsigned long long*)(mtab + 4 * kMsdBuckets), mtab + 6 * kMsdBuckets, 0};
   uint32_t* mctl = mtab + 7 * kMsdBuckets;
   uint32_t* mbig = mctl + 8;
-  uint64_t hred[2];
   hipError_t e = hipSuccess;
-  if (ubounds) {  // bounds of the raw values from the caller: the keys' bounds follow (desc: complemented)
-    hred[0] = ubounds[0] <= ubounds[1] ? (desc ? ~ubounds[1] : ubounds[0]) : 1;
-    hred[1] = ubounds[0] <= ubounds[1] ? (desc ? ~ubounds[0] : ubounds[1]) : 0;
-  } else {
-    if (((uintptr_t)col & 15) == 0 && ((uintptr_t)valid & 1) == 0)
-      hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
-    else
-      hipLaunchKernelGGL(k_rs_prep_rows, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
-    hipLaunchKernelGGL(k_rs_red, dim3(1), dim3(1024), 0, st, part, pb, red);
-    e = hipMemcpyAsync(hred, red, sizeof(hred), hipMemcpyDeviceToHost, st);
-    if (e != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-  }
-  // the bytes of max - min (at least one pass when rows may lack the position: its last pass buckets them)
-  const uint64_t kmin = hred[0] <= hred[1] ? hred[0] : 0ull;
-  const uint64_t span = hred[0] <= hred[1] ? hred[1] - hred[0] : 0ull;
-  const int sb = span ? 64 - __builtin_clzll(span) : 0;  // bits of the span
-  const bool kbit = valid && sb <= 56;                    // validity in key bit 63 (every shift <= 48)
-  const bool vbit = valid && !kbit && n <= (size_t)kRsLack;
-  // executed pass j writes ids to fin when (np-1-j) is even, so the last one lands there; with
-  // msd.first set the first pass clears the bucket table and the last fills it (no keys written out)
   // the last pass writes the sorted keys too (DDSHE_ORDER_KEYS2=0: k_msd_local gathers its buckets' keys
   // from the column by id instead: 80 MB less written, but k_msd_local 42 -> 59 us against scatter 76 -> 66)
   static const int keys2 = order_env("DDSHE_ORDER_KEYS2", 1);
@@ -875,37 +915,101 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   // words of ka: low, the next n: high) when the last pass's digit and the validity bit are in the high
   // words (span >= 2^40): the last histogram then reads 4 B per row (DDSHE_ORDER_SPLIT=0: 8 B, A/B)
   static const int split_env = order_env("DDSHE_ORDER_SPLIT", 1);
-  auto run_passes = [&](const int* shifts, int np, uint32_t* fin, uint32_t* tmp, const MsdRuns& msd) {
+  static const int spec_env = order_env("DDSHE_ORDER_SPEC", 1);  // 0: bounds always read back first (A/B)
+  // executed pass j writes ids to fin when (np-1-j) is even, so the last one lands there; with msd.first
+  // set the first pass clears the bucket table and the last fills it. plan: shifts relative to s1, kmin
+  // and s1 from the device
+  auto run_passes = [&](const int* shifts, int np, uint32_t* fin, uint32_t* tmp, const MsdRuns& msd, bool split,
+                        bool kbit, bool vbit, uint64_t kmin, const uint64_t* plan) {
     const uint32_t* ids_in = nullptr;  // identity before the first pass
     const uint64_t* kin = (const uint64_t*)col;  // raw column before the first pass
     uint64_t* kout = ka;
     const MsdRuns none{};
-    const bool split = msd.first && np == 2 && split_env && (!valid || kbit) && shifts[1] >= 32;
     uint32_t* hi = split ? reinterpret_cast<uint32_t*>(ka) + n : nullptr;  // ka = [low n words | high n words]
     for (int j = 0; j < np; ++j) {
       uint32_t* ids_out = ((np - 1 - j) % 2 == 0) ? fin : tmp;
       const bool last = j == np - 1;
       rs_pass<256>(st, kin, ids_in, valid, n, shifts[j], last, desc, vbit, kbit, kmin, hist, ctot, dtot,
                    last ? (msd.first && keys2 ? kout : nullptr) : kout, ids_out, j == 0 ? msd.first : nullptr,
-                   last ? msd : none, j == 1 ? hi : nullptr, j == 0 ? hi : nullptr);
+                   last ? msd : none, j == 1 ? hi : nullptr, j == 0 ? hi : nullptr, plan);
       kin = kout;
       kout = kout == ka ? kb : ka;
       ids_in = ids_out;
     }
   };
-  if (msd_enabled(n, sb)) {
+  auto msd_tail = [&](uint64_t kmin, const uint64_t* plan) {
+    hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / 4), dim3(256), 0, st, keys2 ? nullptr : col, desc, kmin, kb, ib,
+                       out_ids, runs, mctl, mbig, plan);
+    hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, kb, ib, out_ids, runs, mctl, mbig, plan);
+  };
+  // words 2..3 of hw after the call's device work: overflow flag, plan
+  auto read_ctl = [&](const uint64_t* plan, uint64_t* ovf, uint64_t* pl) -> hipError_t {
+    if (hw) {
+      hipLaunchKernelGGL(k_rs_publish, dim3(1), dim3(1), 0, st, mctl, plan, hw->d);
+      hipError_t r = hipStreamSynchronize(st);
+      *ovf = hw->h[2];
+      *pl = hw->h[3];
+      return r;
+    }
+    uint32_t hctl[2];
+    hipError_t r = hipMemcpyAsync(hctl, mctl, sizeof(hctl), hipMemcpyDeviceToHost, st);
+    if (r == hipSuccess) r = hipStreamSynchronize(st);
+    *ovf = hctl[kMsdCtlOverflow];
+    *pl = 0;
+    return r;
+  };
+  uint64_t hred[2];
+  bool skip_msd = false;  // a speculative call's MSD plan ran and overflowed: straight to the LSD passes
+  if (ubounds) {  // bounds of the raw values from the caller: the keys' bounds follow (desc: complemented)
+    hred[0] = ubounds[0] <= ubounds[1] ? (desc ? ~ubounds[1] : ubounds[0]) : 1;
+    hred[1] = ubounds[0] <= ubounds[1] ? (desc ? ~ubounds[0] : ubounds[1]) : 0;
+  } else {
+    const bool spec = hw && spec_env && split_env && msd_enabled(n, kSpecLo) && g_order_spec.load(std::memory_order_relaxed);
+    if (((uintptr_t)col & 15) == 0 && ((uintptr_t)valid & 1) == 0)
+      hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
+    else
+      hipLaunchKernelGGL(k_rs_prep_rows, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
+    hipLaunchKernelGGL(k_rs_red, dim3(1), dim3(1024), 0, st, part, pb, red, spec ? kSpecLo : 1, spec ? kSpecHi : 0,
+                       hw ? hw->d : nullptr);
+    if (spec) {
+      const uint64_t* plan = red + 2;
+      const int rel[2] = {0, 8};
+      run_passes(rel, 2, out_ids, ib, runs, true, valid != nullptr, false, 0, plan);
+      msd_tail(0, plan);
+      uint64_t ovf = 0, pl = 0;
+      if ((e = read_ctl(plan, &ovf, &pl)) != hipSuccess) return e;
+      if (pl != kRsNoPlan && !ovf) return hipGetLastError();
+      if (pl == kRsNoPlan) g_order_spec.store(0, std::memory_order_relaxed);
+      else skip_msd = true;
+      hred[0] = hw->h[0];
+      hred[1] = hw->h[1];
+    } else if (hw) {
+      if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+      hred[0] = hw->h[0];
+      hred[1] = hw->h[1];
+    } else {
+      if ((e = hipMemcpyAsync(hred, red, sizeof(hred), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+      if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    }
+  }
+  // the bytes of max - min (at least one pass when rows may lack the position: its last pass buckets them)
+  const uint64_t kmin = hred[0] <= hred[1] ? hred[0] : 0ull;
+  const uint64_t span = hred[0] <= hred[1] ? hred[1] - hred[0] : 0ull;
+  const int sb = span ? 64 - __builtin_clzll(span) : 0;  // bits of the span
+  const bool kbit = valid && sb <= 56;                    // validity in key bit 63 (every shift <= 48)
+  const bool vbit = valid && !kbit && n <= (size_t)kRsLack;
+  if (!ubounds && hw) g_order_spec.store(sb >= kSpecLo && sb <= kSpecHi, std::memory_order_relaxed);
+  if (!skip_msd && msd_enabled(n, sb)) {
     runs.s1 = sb - kMsdBits;
     const int shifts[2] = {runs.s1, sb - 8};
+    const bool split = split_env && (!valid || kbit) && shifts[1] >= 32;
     // grouped ids -> out_ids (one-key buckets are final there) + the bucket table; ib (the first pass's
     // ids) and kb are then free: the side copies of the multi-key buckets' ids and keys (k_msd_local)
-    run_passes(shifts, 2, out_ids, ib, runs);
-    hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / 4), dim3(256), 0, st, keys2 ? nullptr : col, desc, kmin, kb, ib,
-                       out_ids, runs, mctl, mbig);
-    hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, kb, ib, out_ids, runs, mctl, mbig);
-    uint32_t hctl[2];
-    if ((e = hipMemcpyAsync(hctl, mctl, sizeof(hctl), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-    if (!hctl[kMsdCtlOverflow]) return hipGetLastError();
+    run_passes(shifts, 2, out_ids, ib, runs, split, kbit, vbit, kmin, nullptr);
+    msd_tail(kmin, nullptr);
+    uint64_t ovf = 0, pl = 0;
+    if ((e = read_ctl(nullptr, &ovf, &pl)) != hipSuccess) return e;
+    if (!ovf) return hipGetLastError();
     // a bucket of > 8192 rows with > 16 distinct keys: redo the whole sort with the LSD passes
   }
   int shifts[8], np = 0;
@@ -915,7 +1019,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     hipLaunchKernelGGL(k_rs_iota, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out_ids, n);
     return hipGetLastError();
   }
-  run_passes(shifts, np, out_ids, ib, MsdRuns{});
+  run_passes(shifts, np, out_ids, ib, MsdRuns{}, false, kbit, vbit, kmin, nullptr);
   return hipGetLastError();
 }
 

@@ -163,6 +163,40 @@ def test_order_msd_buckets(eng, kind):
     assert np.array_equal(eng.ope_order(col, None, True), expected(col, np.ones(n, np.uint8), True)), kind
 
 
+def test_order_speculative_plan_sequence(eng):
+    """A raw call after one whose key span had 40..56 bits launches the MSD plan before the bounds are
+    back on the host (kmin and the shifts planned on the device). Calls in a row whose spans leave that
+    range (39, 57, 60 bits, 24 bits) must fall back to the host-planned path, a crowded bucket inside it
+    must still reach the LSD fallback, and the range's edges (40, 56 bits) must sort on the plan: every
+    call of the sequence against numpy."""
+    rng = np.random.default_rng(31)
+    n = 200_003
+
+    def span_col(bits):
+        c = rng.integers(0, 1 << bits, size=n, dtype=np.int64) - (1 << (bits - 1))
+        c[:2] = [-(1 << (bits - 1)), (1 << (bits - 1)) - 1]  # exactly `bits` bits of span
+        c[2:40] = c[2]                                        # ties
+        return c
+
+    def crowded():
+        c = rng.integers(0, 1 << 44, size=n, dtype=np.int64)
+        rows = rng.choice(n, size=20_000, replace=False)      # > 8192 rows, > 16 keys in one bucket
+        c[rows] = (123 << 28) + rng.integers(0, 1 << 28, size=20_000)
+        c[:2] = [0, (1 << 44) - 1]
+        return c
+
+    ope_map = np.cumsum(rng.integers(1, 1 << 40, size=10001, dtype=np.int64)) - (1 << 52)
+    ope = ope_map[rng.integers(1, 10001, size=n)]
+    seq = [ope, ope, span_col(24), ope, ope, span_col(39), span_col(40), span_col(40), span_col(56),
+           span_col(57), span_col(48), crowded(), span_col(60), ope, ope]
+    for k, col in enumerate(seq):
+        valid = (rng.random(n) > 0.07).astype(np.uint8)
+        desc = bool(k % 2)
+        assert np.array_equal(eng.ope_order(col, valid, desc), expected(col, valid, desc)), k
+        assert np.array_equal(eng.ope_order(col, None, not desc),
+                              expected(col, np.ones(n, np.uint8), not desc)), k
+
+
 @pytest.mark.parametrize("offset", [0, 1])
 def test_order_device_pointers(eng, offset):
     """dds_ope_order_device on caller-owned device buffers: the min/max prep reads 16-byte key pairs
