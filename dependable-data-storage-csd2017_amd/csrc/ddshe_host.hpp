@@ -352,7 +352,6 @@ inline hipError_t stage_ptr(Worker* w, uint32_t** p) {
   *p = e == hipSuccess ? (uint32_t*)w->hstage.p : nullptr;
   return e;
 }
-// copy `bytes` (<= 64) device -> host through the pinned slot and synchronise the stream
 // the worker's OrderHostWords (launch_ope_order's read-back words), allocated on first use
 inline hipError_t order_words(Worker* w, OrderHostWords* ow) {
   w->hord.flags = hipHostMallocCoherent | hipHostMallocMapped;
@@ -362,6 +361,8 @@ inline hipError_t order_words(Worker* w, OrderHostWords* ow) {
   return e;
 }
 
+// copy `bytes` (<= 64) device -> host through the pinned slot and synchronise the stream (a one-wave
+// kernel storing them there instead measured the same on the config-1 decimal route)
 inline hipError_t read_sync(Worker* w, hipStream_t st, const void* dsrc, void* dst, size_t bytes) {
   uint32_t* h = nullptr;
   hipError_t e = stage_ptr(w, &h);

@@ -499,9 +499,15 @@ int dds_opecol_search(dds_opecol* col, const char* bound_dec, int op, uint32_t* 
     record_time(ctx, w, wl.st, false, 2);
     uint64_t total = 0;
     HIP_TRY(read_sync(w, wl.st, w->flags.p, &total, 8));
-    // straight into the caller's buffer (measured: a pinned stage + host copy was slower at 20 MB); the
-    // route-shaped answer is dds_opecol_search_mask (n/8 bytes instead of 4 bytes per match)
-    if (total) HIP_TRY(hipMemcpy(out_idx, w->out.p, total * 4, hipMemcpyDeviceToHost));
+    // straight into the caller's buffer (measured: a pinned stage + host copy was slower at 20 MB; a
+    // page-locked reply buffer takes one DMA); the route-shaped answer is dds_opecol_search_mask (n/8
+    // bytes instead of 4 bytes per match)
+    if (total && host_registered(ctx, out_idx, total * 4)) {
+      HIP_TRY(hipMemcpyAsync(out_idx, w->out.p, total * 4, hipMemcpyDeviceToHost, wl.st));
+      HIP_TRY(hipStreamSynchronize(wl.st));
+    } else if (total) {
+      HIP_TRY(hipMemcpy(out_idx, w->out.p, total * 4, hipMemcpyDeviceToHost));
+    }
     add_filter_time(ctx, w);
     size_t got = (size_t)total;
     const std::vector<uint32_t> extra = wide_matches(col, sb, op);  // merged in row order

@@ -728,12 +728,17 @@ class OpeColumn:
                                           None if st is None else st.ctypes.data_as(C.c_void_p), n),
                "dds_opecol_append_dec")
 
-    def search(self, bound, op: str) -> np.ndarray:
-        out = np.empty(max(1, len(self)), dtype=np.uint32)
+    def search(self, bound, op: str, out: np.ndarray | None = None) -> np.ndarray:
+        """dds_opecol_search: matching row ids in row order. out: a reusable uint32 buffer of at least
+        len(self) entries (Engine.host_register it once to have the ids DMA'd straight in); the result is
+        then a view of it."""
+        buf = np.empty(max(1, len(self)), dtype=np.uint32) if out is None else out
+        if len(buf) < len(self):
+            raise ValueError("out holds fewer entries than the column's rows")
         got = C.c_size_t()
         _check(_lib.dds_opecol_search(self._h, None if bound is None else str(bound).encode(), OPE_OPS[op],
-                                      out.ctypes.data_as(C.c_void_p), C.byref(got)), "dds_opecol_search")
-        return out[: got.value].copy()
+                                      buf.ctypes.data_as(C.c_void_p), C.byref(got)), "dds_opecol_search")
+        return buf[: got.value] if out is not None else buf[: got.value].copy()
 
     def search_mask(self, bound, op: str, out: np.ndarray | None = None):
         """dds_opecol_search_mask: (uint64 words, bit r%64 of word r/64 = row r matches; match count).

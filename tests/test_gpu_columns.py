@@ -102,6 +102,36 @@ def test_opecol_search_and_order_vs_oracle(eng):
         assert routes.order(eng, route, clean, 1) == homo.order(route, clean, 1)
 
 
+def test_opecol_search_into_reply_buffers(eng):
+    """dds_opecol_search into the caller's reusable reply buffer: an engine-allocated one (one DMA), a
+    registered numpy array, and a plain array, each equal to the fresh-array answer, with wide (beyond
+    int64) matches merged in row order and a buffer reused across calls of different match counts."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    n = 300_001
+    vals = [str(int(v)) for v in rng.integers(-10**9, 10**9, size=n)]
+    vals[17] = str(2**70)
+    vals[250_000] = str(-2**70)
+    col = eng.opecol(n)
+    col.append_dec(vals, cls=[2] * n)
+    ebuf = eng.host_alloc(n, np.uint32)
+    rbuf = np.empty(n, dtype=np.uint32)
+    eng.host_register(rbuf)
+    pbuf = np.empty(n, dtype=np.uint32)
+    try:
+        for op in ("gt", "ge", "lt", "le"):
+            for bound in ("0", "999999999", "-1000000000", str(2**64)):
+                want = col.search(bound, op)
+                for buf in (ebuf, rbuf, pbuf):
+                    got = col.search(bound, op, out=buf)
+                    assert np.array_equal(got, want), (op, bound)
+        with pytest.raises(ValueError):
+            col.search("0", "gt", out=np.empty(10, dtype=np.uint32))
+    finally:
+        eng.host_unregister(rbuf)
+        eng.host_free(ebuf)
+
+
 def test_opecol_resident_api(eng):
     """The resident column across requests: appends, truncate, int64 appends, lazy bound parse."""
     import ddshe
