@@ -547,6 +547,92 @@ int ingest(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint8_t
 
 
 
+// the worker's copy stream (H2D copies overlapping the compute stream) and its two events
+hipError_t copy_stream(Worker* w) {
+  if (w->cstream) return hipSuccess;
+  hipError_t e = hipStreamCreateWithFlags(&w->cstream, hipStreamNonBlocking);
+  for (auto& ev : w->ev_copy)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  return e;
+}
+
+// Long folds of host rows (dds_paillier_sum / dds_rsa_product / dds_modmul_fold over millions of rows):
+// the rows are folded in pieces as they arrive, so the fold of piece p runs while piece p + 1 crosses
+// PCIe instead of after the last chunk. Copy stream: per 64 MiB chunk, the DMA out of the pinned slot the
+// host pool filled, then k_ingest_be; compute stream, after a piece's last chunk: k_reduce_rows gated on
+// the device by the ingest flags (rows >= 2N), the piece's fold to a partial (fold_partial_device), its
+// copy to column p of the partials; then one tree over the pieces' partials. The flags are read after
+// the result (a row wider than the limb width fails the call, as ingest() does).
+// DDSHE_INGEST_PIECES: pieces (default 8; 1: ingest everything, then fold); from DDSHE_INGEST_PIPE_ROWS
+// rows (default 2^21). 10M 512-byte rows, one box: 122.9 ms in one piece, 104.5 in 4, 97.9 in 8.
+size_t ingest_pieces(size_t count) {
+  static const size_t pieces = [] {
+    const char* e = getenv("DDSHE_INGEST_PIECES");
+    return e ? (size_t)atoll(e) : (size_t)8;
+  }();
+  static const size_t min_rows = [] {
+    const char* e = getenv("DDSHE_INGEST_PIPE_ROWS");
+    return e ? (size_t)atoll(e) : ((size_t)1 << 21);
+  }();
+  return count >= min_rows ? pieces : 1;
+}
+
+int fold_be_pipelined(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const uint8_t* ops, size_t width,
+                      size_t count, size_t pieces, bn::Limbs* value) {
+  const size_t crows = std::max<size_t>(1, kIngestChunkBytes / width);
+  const size_t prow = round_up((count + pieces - 1) / pieces, crows);  // rows per piece: whole chunks
+  const size_t np = (count + prow - 1) / prow;
+  const size_t stride = round_up(count, 64), S2 = (size_t)mc.S2, pst = round_up(np, 64);
+  HIP_TRY(w->x.ensure((size_t)mc.S * stride * 4));
+  HIP_TRY(w->in.ensure(2 * crows * width));
+  HIP_TRY(w->flags.ensure(16));
+  HIP_TRY(w->gather.ensure(S2 * pst * 4));
+  HIP_TRY(copy_stream(w));
+  uint32_t* X = w->x.as<uint32_t>();
+  uint32_t* flags = w->flags.as<uint32_t>();
+  uint32_t* parts = w->gather.as<uint32_t>();
+  const uint32_t* n2x = mc.d + (size_t)kConstN2x * mc.S;
+  hipStream_t cs = w->cstream;
+  HIP_TRY(hipMemsetAsync(flags, 0, 4, st));
+  HIP_TRY(hipEventRecord(w->ev_copy[1], st));  // the copy stream starts after the clear (and st's earlier work)
+  HIP_TRY(hipStreamWaitEvent(cs, w->ev_copy[1], 0));
+  int64_t E = 0;
+  bool used[2] = {false, false};
+  size_t slot = 0;
+  for (size_t p = 0; p < np; ++p) {
+    const size_t p0 = p * prow, pn = std::min(prow, count - p0);
+    for (size_t b = p0; b < p0 + pn; b += crows, slot ^= 1) {
+      const size_t nrows = std::min(crows, p0 + pn - b), bytes = nrows * width;
+      if (used[slot]) HIP_TRY(hipEventSynchronize(w->ev_dec[slot]));  // the DMA out of this host slot is done
+      HIP_TRY(w->hch[slot].ensure(crows * width));
+      CopyPool::get().copy(w->hch[slot].p, ops + b * width, bytes);
+      uint8_t* d = w->in.as<uint8_t>() + slot * crows * width;  // reused two chunks later, after this ingest (cs)
+      HIP_TRY(hipMemcpyAsync(d, w->hch[slot].p, bytes, hipMemcpyHostToDevice, cs));
+      HIP_TRY(hipEventRecord(w->ev_dec[slot], cs));
+      HIP_TRY(launch_ingest_be(d, width, nrows, mc.S, mc.W, n2x, X + b, stride, flags, cs));
+      used[slot] = true;
+    }
+    HIP_TRY(hipEventRecord(w->ev_copy[0], cs));
+    HIP_TRY(hipStreamWaitEvent(st, w->ev_copy[0], 0));
+    HIP_TRY(launch_reduce_rows(mc.S, X + p0, stride, pn, mc.d, mc.n0, st, flags));
+    const uint32_t* part = nullptr;
+    size_t ps = 0;
+    int64_t Ep = 0;
+    int rc = fold_partial_device(ctx, w, st, mc, X + p0, stride, pn, &part, &ps, &Ep, nullptr);
+    if (rc) return rc;
+    HIP_TRY(launch_strided_copy(part, 0, 1, parts + p, 0, pst, 1, S2, st));  // S2 limbs -> column p
+    E += Ep;
+  }
+  Leaves lv{parts, pst, (int)S2, mc.W, np, E, nullptr};
+  lv.rows = count;
+  int rc = reduce_leaves(ctx, w, st, mc, lv, true, value, nullptr, nullptr);
+  if (rc) return rc;
+  uint32_t fl = 0;
+  HIP_TRY(read_sync(w, st, flags, &fl, 4));
+  if (fl & 2u) return fail(DDS_E_RANGE, "operand wider than the modulus limb width");
+  return DDS_OK;
+}
+
 int dec_table(ModConsts& mc) {
   std::lock_guard<std::mutex> lk(mc.decmu);
   if (mc.dtab) return DDS_OK;
@@ -598,10 +684,7 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
   HIP_TRY(w->rflags.ensure(count));
   HIP_TRY(w->flags.ensure(16));
   HIP_TRY(hipMemsetAsync(w->flags.p, 0, 4, st));
-  if (!w->cstream) {
-    HIP_TRY(hipStreamCreateWithFlags(&w->cstream, hipStreamNonBlocking));
-    for (auto& e : w->ev_copy) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  }
+  HIP_TRY(copy_stream(w));
   hipStream_t cs = w->cstream;
   // rows per chunk: a request of fewer than 2 x 2^18 rows still splits into two chunks (>= 4096 rows
   // each), so the second chunk's host and H2D copies overlap the first one's parse (config 1: 10k
@@ -721,10 +804,15 @@ int modmul_fold_be(dds_ctx* ctx, const uint8_t* mod_be, size_t mod_bytes, size_t
   WorkerLease wl(ctx);
   if ((rc = wl.acquire())) return rc;
   Worker* w = wl.w;
+  bn::Limbs v;
+  const size_t pieces = ingest_pieces(count);
+  if (pieces > 1) {
+    if ((rc = fold_be_pipelined(ctx, w, wl.st, *mc, ops, width, count, pieces, &v))) return rc;
+    return emit_be(v, mod_bytes, out, out_cap, out_len);
+  }
   const size_t stride = round_up(count, 64);
   HIP_TRY(w->x.ensure((size_t)mc->S * stride * 4));
   if ((rc = ingest(ctx, w, wl.st, *mc, ops, width, count, w->in, w->x.as<uint32_t>(), stride))) return rc;
-  bn::Limbs v;
   if ((rc = fold_value_device(ctx, w, wl.st, *mc, w->x.as<uint32_t>(), stride, count, nullptr, &v))) return rc;
   return emit_be(v, mod_bytes, out, out_cap, out_len);
 }

@@ -214,9 +214,12 @@ __global__ void __launch_bounds__(256) k_egress_be(const uint32_t* __restrict__ 
 }
 
 // rows >= 2N: x <- MonPro(MonPro(x, R^2 mod N), 1) = x mod N
+// gate (nullable): skip unless gate[0] & 1 (an ingest's flags word, read on the device: no host round trip)
 template <int S, int TPI, int W>
 __global__ void __launch_bounds__(256, 2) k_reduce_rows(uint32_t* __restrict__ X, size_t stride, size_t count,
-                                                     const uint32_t* __restrict__ consts, uint32_t n0) {
+                                                     const uint32_t* __restrict__ consts, uint32_t n0,
+                                                     const uint32_t* __restrict__ gate) {
+  if (gate && !(gate[0] & 1u)) return;
   using G = Grp<S, TPI, W>;
   using M = Mont<S, TPI, W>;
   constexpr int L = G::L;
@@ -1013,10 +1016,10 @@ hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S
 }
 
 hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, const uint32_t* consts, uint32_t n0,
-                              hipStream_t st) {
+                              hipStream_t st, const uint32_t* gate) {
   if (count == 0) return hipSuccess;
   DDSHE_SWITCH(S, hipLaunchKernelGGL((k_reduce_rows<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256), 0, st, X, stride,
-                                     count, consts, n0));
+                                     count, consts, n0, gate));
   return hipGetLastError();
 }
 

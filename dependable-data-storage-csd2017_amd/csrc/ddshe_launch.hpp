@@ -35,8 +35,9 @@ hipError_t launch_ingest_be(const uint8_t* in, size_t width, size_t count, int S
 hipError_t launch_egress_be(const uint32_t* X, size_t stride, size_t count, int S, int W, const uint32_t* nmod,
                             size_t width, uint8_t* out, hipStream_t st);
 constexpr int kEgressMaxLimbs = 160;
+// gate (nullable): the kernel does nothing unless gate[0] & 1 (k_ingest_be's "some row >= 2N" flag)
 hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, const uint32_t* consts, uint32_t n0,
-                              hipStream_t st);
+                              hipStream_t st, const uint32_t* gate = nullptr);
 // main fold level (throughput shape); partial rows are zero-extended to s_out limbs
 // qp_mod (nullable): N~ = N·n0 in main limbs (when W·S >= bits(N~) + 2; see Mont QP)
 hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,

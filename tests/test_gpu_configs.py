@@ -126,3 +126,33 @@ def test_config4_full_size_encrypt_then_sum(eng, keys):
         assert out.read(i, 1)[0] == homo.paillier_encrypt(int(ms[i]), rcol.read(i, 1)[0], k), i
     out.close()
     rcol.close()
+
+
+def test_fold_buffer_pipelined_pieces(eng, keys):
+    """dds_modmul_fold over >= 2^21 host rows folds them in pieces as they cross PCIe (copy stream: DMA +
+    k_ingest_be per 64 MiB chunk; compute stream: each piece's fold to a partial, then one tree over the
+    pieces): equal to the resident column's fold, also with rows >= 2N in the first and the last piece
+    (reduced on the device by k_reduce_rows gated on the ingest flags) and zero-padded wider rows; a row
+    wider than the limb width still fails the call."""
+    import ddshe
+    k = keys["paillier1024_seed1"]
+    N = k["nsquare"]
+    n = (1 << 21) + 12_345
+    col = eng.column(N, n)
+    col.fill_paillier_synth(k["n"], k["g"], seed=5, row0=0, count=n, pool=64)
+    buf = col.read_buffer(0, n)
+    want = col.fold()
+    col.close()
+    assert eng.fold_buffer(N, buf) == want
+    width = buf.shape[1] + 64  # 512 more bits than n^2: past the column's limbs too
+    wide = np.zeros((n, width), dtype=np.uint8)
+    wide[:, 64:] = buf
+    del buf
+    for i, mult in ((3, 2), (17, 3), (n - 2, 2), (n // 2, 5)):
+        x = int.from_bytes(wide[i].tobytes(), "big") + mult * N
+        wide[i] = np.frombuffer(x.to_bytes(width, "big"), dtype=np.uint8)
+    assert eng.fold_buffer(N, wide) == want
+    wide[n - 7, 0] = 0x80  # >= 2^(8 width - 1): wider than the column's limbs
+    with pytest.raises(ddshe.DDSError) as ei:
+        eng.fold_buffer(N, wide)
+    assert ei.value.status == ddshe.DDS_E_RANGE
