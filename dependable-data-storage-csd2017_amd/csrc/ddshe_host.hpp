@@ -107,6 +107,7 @@ struct Worker {
   HostBuf hcnt;    // coherent + mapped: the Search bitmask's per-tile match counts, stored by the device
   HostBuf hpair;   // pairwise batches: operands and results, coherent + mapped (k_pairs_sos reads and writes it)
   HostBuf hord;    // coherent + mapped: the OPE ordering's bounds / overflow words (OrderHostWords)
+  HostBuf hscan;   // coherent + mapped: string-table scans' match count, needle bytes and row ids
   HostBuf hbig;    // large read-backs (Search ids / match masks, Order permutations) before the caller's copy
   DevBuf dch[2], doff[2], rflags;
   hipEvent_t ev_dec[2] = {};

@@ -360,17 +360,29 @@ int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values
   HIP_TRY(w->in2.ensure(std::max<size_t>(nb.size(), 1)));
   HIP_TRY(w->x.ensure(nrows * 4));
   HIP_TRY(w->misc.ensure(ope_scratch_bytes(nrows)));
-  HIP_TRY(w->flags.ensure(16));
-  HIP_TRY(w->out.ensure(nrows * 4));
-  if (!nb.empty()) HIP_TRY(hipMemcpyAsync(w->in2.p, nb.data(), nb.size(), hipMemcpyHostToDevice, wl.st));
+  // the worker's coherent, device-mapped scan buffer: [0, 8) the match count, then the needle bytes
+  // (DMA'd from there: pinned, no staging), then the row ids. The compaction stores the count and the
+  // ids over PCIe straight into it, so a scan is its launches and one stream synchronisation (no copy
+  // launch and no second round trip for the ids)
+  const size_t nbal = round_up(std::max<size_t>(nb.size(), 1), 64);
+  w->hscan.flags = hipHostMallocCoherent | hipHostMallocMapped;
+  HIP_TRY(w->hscan.ensure(64 + nbal + std::max<size_t>(nrows, 1) * 4));
+  uint8_t* hs = (uint8_t*)w->hscan.p;
+  uint8_t* ds = (uint8_t*)w->hscan.dptr;
+  if (!ds) return fail(DDS_E_HIP, "scan buffer has no device mapping");
+  uint64_t* d_total = (uint64_t*)ds;
+  *(volatile uint64_t*)hs = 0;  // no rows: no scatter block stores the count
+  uint32_t* dst = (uint32_t*)(ds + 64 + nbal);
+  if (!nb.empty()) {
+    memcpy(hs + 64, nb.data(), nb.size());
+    HIP_TRY(hipMemcpyAsync(w->in2.p, hs + 64, nb.size(), hipMemcpyHostToDevice, wl.st));
+  }
   std::shared_ptr<PosIdx> px;
   if (mode == 0 && (rc = pos_index(t, position, wl.st, &px))) return rc;
   record_time(ctx, w, wl.st, true, 2);
-  uint32_t* dst = w->out.as<uint32_t>();
   if (mode == 0) {  // SearchEq / NEq over the position index, straight into the compaction masks
     HIP_TRY(launch_str_eq_compact(px->fp, px->present, row0, nrows, t->row_beg, t->elem_off, t->chars,
-                                  w->in2.as<uint8_t>(), nd, position, negate, w->misc.p, w->flags.as<uint64_t>(), dst,
-                                  wl.st));
+                                  w->in2.as<uint8_t>(), nd, position, negate, w->misc.p, d_total, dst, wl.st));
   } else {
     uint8_t* flags = w->x.as<uint8_t>();
     // the whole heap, or one row's current version (IsElement)
@@ -379,12 +391,13 @@ int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values
     HIP_TRY(launch_str_any(t->fp, e_first, ne, t->elem_row, t->live, row0, nrows, t->elem_off, t->chars,
                            w->in2.as<uint8_t>(), nd, flags, wl.st));
     const uint32_t req = mode == 2 ? (1u << nvalues) - 1u : 0u;  // AND: every needle's bit
-    HIP_TRY(launch_byte_compact(flags, nrows, 0xFFu, w->misc.p, w->flags.as<uint64_t>(), dst, wl.st, req));
+    HIP_TRY(launch_byte_compact(flags, nrows, 0xFFu, w->misc.p, d_total, dst, wl.st, req));
   }
   record_time(ctx, w, wl.st, false, 2);
-  uint64_t total = 0;
-  HIP_TRY(read_sync(w, wl.st, w->flags.p, &total, 8));
-  if (total) HIP_TRY(hipMemcpy(out_rows, dst, total * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipStreamSynchronize(wl.st));
+  const uint64_t total = *(volatile uint64_t*)hs;
+  if (total > nrows) return fail(DDS_E_HIP, "scan count out of range");
+  if (total) memcpy(out_rows, hs + 64 + nbal, total * 4);
   if (ctx->timing.load()) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, w->ev[2], w->ev[3]) == hipSuccess) {
