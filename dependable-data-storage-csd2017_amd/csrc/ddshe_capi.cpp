@@ -2418,12 +2418,14 @@ int dds_ope_filter_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_v
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
     HIP_TRY(w->misc.ensure(ope_scratch_bytes(n)));
-    HIP_TRY(w->flags.ensure(16));
+    OrderHostWords hw;  // the match count is stored by the scatter into coherent mapped host memory: no copy
+    HIP_TRY(order_words(w, &hw));
+    hw.h[kCountWord] = 0;  // no rows: no scatter block stores it
     record_time(ctx, w, wl.st, true, 2);
-    HIP_TRY(launch_ope_filter(d_col, d_valid, n, bound, op, w->misc.p, w->flags.as<uint64_t>(), d_out, wl.st));
+    HIP_TRY(launch_ope_filter(d_col, d_valid, n, bound, op, w->misc.p, hw.d + kCountWord, d_out, wl.st));
     record_time(ctx, w, wl.st, false, 2);
-    uint64_t total = 0;  // pinned readback: one small DMA, no staging copy
-    HIP_TRY(read_sync(w, wl.st, w->flags.p, &total, 8));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    const uint64_t total = hw.h[kCountWord];
     if (ctx->timing.load()) {
       float ms = 0;
       if (hipEventElapsedTime(&ms, w->ev[2], w->ev[3]) == hipSuccess) {

@@ -353,7 +353,9 @@ inline hipError_t stage_ptr(Worker* w, uint32_t** p) {
   *p = e == hipSuccess ? (uint32_t*)w->hstage.p : nullptr;
   return e;
 }
-// the worker's OrderHostWords (launch_ope_order's read-back words), allocated on first use
+// the worker's OrderHostWords (launch_ope_order's read-back words, words 0..3; an OPE filter's match count
+// at kCountWord), allocated on first use
+constexpr size_t kCountWord = 4;
 inline hipError_t order_words(Worker* w, OrderHostWords* ow) {
   w->hord.flags = hipHostMallocCoherent | hipHostMallocMapped;
   hipError_t e = w->hord.ensure(64);

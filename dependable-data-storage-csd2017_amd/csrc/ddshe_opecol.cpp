@@ -491,14 +491,16 @@ int dds_opecol_search(dds_opecol* col, const char* bound_dec, int op, uint32_t* 
     Worker* w = wl.w;
     const size_t n = col->count;
     HIP_TRY(w->misc.ensure(ope_scratch_bytes(n)));
-    HIP_TRY(w->flags.ensure(16));
     HIP_TRY(w->out.ensure(n * 4));
+    OrderHostWords hw;  // the match count is stored by the scatter into coherent mapped host memory: no copy
+    HIP_TRY(order_words(w, &hw));
+    hw.h[kCountWord] = 0;  // no rows: no scatter block stores it
     record_time(ctx, w, wl.st, true, 2);
-    HIP_TRY(launch_ope_filter(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, w->flags.as<uint64_t>(),
+    HIP_TRY(launch_ope_filter(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, hw.d + kCountWord,
                               w->out.as<uint32_t>(), wl.st, kSearch, kWide));
     record_time(ctx, w, wl.st, false, 2);
-    uint64_t total = 0;
-    HIP_TRY(read_sync(w, wl.st, w->flags.p, &total, 8));
+    HIP_TRY(hipStreamSynchronize(wl.st));
+    const uint64_t total = hw.h[kCountWord];
     // straight into the caller's buffer (measured: a pinned stage + host copy was slower at 20 MB; a
     // page-locked reply buffer takes one DMA); the route-shaped answer is dds_opecol_search_mask (n/8
     // bytes instead of 4 bytes per match)
