@@ -96,6 +96,8 @@ struct Worker {
   // tiles add into it, it is read, then re-zeroed on the stream after the read); ev_done marks the read
   DevBuf ctr;
   bool ctr_zero = false;
+  DevBuf sflags;            // string scans' row flags, zero between scans when sflags_zero
+  bool sflags_zero = false;
   hipEvent_t ev_done = {};
   DevBuf crt[7];  // CRT encryption scratch (see encrypt_crt_device)
   hipEvent_t ev[4] = {};

@@ -760,15 +760,23 @@ __global__ void __launch_bounds__(kOpeBlock) k_str_eq_count(const uint32_t* __re
 // needle bits): same tile layout and masks as k_ope_count, predicate (b[r] & vmask) != 0 and
 // (b[r] & vall) == vall on a byte per row. `bytes` may start at any
 // offset (a row range of the mask): 4-byte loads only when it is aligned.
+// rezero: every non-zero word / byte read is stored back as 0 (the string scans' row flags stay zeroed
+// between scans: no memset launch before the next one; matches are sparse, so are these stores)
 __global__ void __launch_bounds__(kOpeBlock) k_byte_count(const uint8_t* __restrict__ bytes, size_t n, uint32_t vmask,
                                                           uint32_t vall, uint32_t* __restrict__ masks,
-                                                          uint32_t* __restrict__ counts) {
+                                                          uint32_t* __restrict__ counts, bool rezero) {
   const size_t t0 = (size_t)blockIdx.x * kOpeTile + 4 * (size_t)threadIdx.x;
   uint32_t v[kOpeGroups];
+  uint8_t* zb = const_cast<uint8_t*>(bytes);
   if ((uintptr_t)bytes % 4 == 0 && t0 + (kOpeGroups - 1) * 4 * kOpeBlock + 3 < n) {
 #pragma unroll
     for (int k = 0; k < kOpeGroups; ++k)
       v[k] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(bytes + t0 + (size_t)k * 4 * kOpeBlock));
+    if (rezero) {
+#pragma unroll
+      for (int k = 0; k < kOpeGroups; ++k)
+        if (v[k]) *reinterpret_cast<uint32_t*>(zb + t0 + (size_t)k * 4 * kOpeBlock) = 0u;
+    }
   } else {
 #pragma unroll
     for (int k = 0; k < kOpeGroups; ++k) {
@@ -776,7 +784,9 @@ __global__ void __launch_bounds__(kOpeBlock) k_byte_count(const uint8_t* __restr
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const size_t r = t0 + (size_t)k * 4 * kOpeBlock + j;
-        vk |= (r < n ? (uint32_t)bytes[r] : 0u) << (8 * j);
+        const uint32_t b = r < n ? (uint32_t)bytes[r] : 0u;
+        if (rezero && b) zb[r] = 0;
+        vk |= b << (8 * j);
       }
       v[k] = vk;
     }
@@ -1385,12 +1395,13 @@ hipError_t launch_str_eq_compact(const uint32_t* posfp, const uint64_t* present,
 }
 
 hipError_t launch_byte_compact(const uint8_t* bytes, size_t n, uint32_t vmask, void* scratch, uint64_t* total,
-                               uint32_t* out, hipStream_t st, uint32_t vall) {
+                               uint32_t* out, hipStream_t st, uint32_t vall, bool rezero) {
   const size_t nb = ope_blocks(n);
   if (nb == 0) return hipSuccess;
   uint32_t* counts = (uint32_t*)scratch;
   uint32_t* masks = counts + nb;
-  hipLaunchKernelGGL(k_byte_count, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, bytes, n, vmask, vall, masks, counts);
+  hipLaunchKernelGGL(k_byte_count, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, bytes, n, vmask, vall, masks, counts,
+                     rezero);
   hipLaunchKernelGGL(k_ope_scatter, dim3((unsigned)nb), dim3(kOpeBlock), 0, st, masks, counts, out, total);
   return hipGetLastError();
 }

@@ -130,10 +130,11 @@ hipError_t launch_ope_mask(const int64_t* col, const uint8_t* valid, size_t n, i
                            bool total_zeroed = false, uint32_t* hmask = nullptr, size_t hwords = 0,
                            uint32_t* hcounts = nullptr);
 uint32_t* ope_mask_words(void* scratch, size_t n);
-// rows i with (bytes[i] & vmask) != 0 -> ascending ids in out, count in *total (device); scratch as above
+// rows i with (bytes[i] & vmask) != 0 -> ascending ids in out, count in *total (device); scratch as above.
+// rezero: the count pass stores 0 over every non-zero byte it read (a flag buffer kept zeroed between uses)
 hipError_t launch_byte_compact(const uint8_t* bytes, size_t n, uint32_t vmask, void* scratch, uint64_t* total,
                                uint32_t* out, hipStream_t st,
-                               uint32_t vall = 0);
+                               uint32_t vall = 0, bool rezero = false);
 // resident-row mutations (ddshe_mutate.hip): rows ids[i] of dst (S limbs, stride dstride) <- column i of
 // src (stride sstride); dst[ids[i]] <- vals[i] for bytes / u64; keep[p] = !dead[perm[p]]; dst[i] = src[idx[i]]
 hipError_t launch_scatter_rows(const uint32_t* src, size_t sstride, const uint32_t* ids, size_t n, int S, uint32_t* dst,
@@ -219,10 +220,11 @@ hipError_t launch_str_compact(size_t nrows, const uint64_t* old_beg, const uint3
                               uint8_t* nchars, hipStream_t st);
 // SearchEntry/OR/AND/IsElement: flag byte r - row0 |= bit j for every heap element in [e_first,
 // e_first + nelems) equal to needle j whose owner r is live and in [row0, row0 + nrows) (flags zeroed by
-// the launcher, 4-byte aligned)
+// the launcher unless flags_zeroed, 4-byte aligned)
 hipError_t launch_str_any(const uint32_t* fp, uint64_t e_first, size_t nelems, const uint32_t* elem_row,
                           const uint8_t* live, size_t row0, size_t nrows, const uint64_t* elem_off, const uint8_t* chars,
-                          const uint8_t* nchars, const StrNeedles& nd, uint8_t* flags, hipStream_t st);
+                          const uint8_t* nchars, const StrNeedles& nd, uint8_t* flags, hipStream_t st,
+                          bool flags_zeroed = false);
 hipError_t launch_plain_sum(const uint32_t* X, size_t stride, size_t count, int S, size_t nthreads, uint64_t* part,
                             uint64_t* out, hipStream_t st);
 // unbounded product tree level: rows (2p, 2p+1) of A[count][len] (radix 2^16 in u32)

@@ -227,9 +227,10 @@ hipError_t launch_str_compact(size_t nrows, const uint64_t* old_beg, const uint3
 
 hipError_t launch_str_any(const uint32_t* fp, uint64_t e_first, size_t nelems, const uint32_t* elem_row,
                           const uint8_t* live, size_t row0, size_t nrows, const uint64_t* elem_off, const uint8_t* chars,
-                          const uint8_t* nchars, const StrNeedles& nd, uint8_t* flags, hipStream_t st) {
+                          const uint8_t* nchars, const StrNeedles& nd, uint8_t* flags, hipStream_t st,
+                          bool flags_zeroed) {
   if (nrows == 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(flags, 0, (nrows + 3) & ~(size_t)3, st);  // whole words (the atomics' unit)
+  hipError_t e = flags_zeroed ? hipSuccess : hipMemsetAsync(flags, 0, (nrows + 3) & ~(size_t)3, st);  // whole words
   if (e != hipSuccess || nelems == 0) return e;
   const size_t quads = (nelems + 3) / 4, per_block = (size_t)256 * kStrQuads;
   hipLaunchKernelGGL(k_str_any, dim3((unsigned)((quads + per_block - 1) / per_block)), dim3(256), 0, st, fp, e_first,

@@ -358,7 +358,6 @@ int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values
   if ((rc = wl.acquire())) return rc;
   Worker* w = wl.w;
   HIP_TRY(w->in2.ensure(std::max<size_t>(nb.size(), 1)));
-  HIP_TRY(w->x.ensure(nrows * 4));
   HIP_TRY(w->misc.ensure(ope_scratch_bytes(nrows)));
   // the worker's coherent, device-mapped scan buffer: [0, 8) the match count, then the needle bytes
   // (DMA'd from there: pinned, no staging), then the row ids. The compaction stores the count and the
@@ -384,14 +383,22 @@ int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values
     HIP_TRY(launch_str_eq_compact(px->fp, px->present, row0, nrows, t->row_beg, t->elem_off, t->chars,
                                   w->in2.as<uint8_t>(), nd, position, negate, w->misc.p, d_total, dst, wl.st));
   } else {
-    uint8_t* flags = w->x.as<uint8_t>();
+    // row flags: the worker's own buffer, kept zeroed between scans (the count pass re-zeroes what the
+    // scan set); a fresh or possibly dirty buffer (an earlier scan that failed mid-way) is cleared first
+    const size_t fbytes = round_up(std::max<size_t>(nrows, 1), 4);
+    if (w->sflags.cap < fbytes) w->sflags_zero = false;
+    HIP_TRY(w->sflags.ensure(fbytes));
+    uint8_t* flags = w->sflags.as<uint8_t>();
+    if (!w->sflags_zero) HIP_TRY(hipMemsetAsync(flags, 0, w->sflags.cap, wl.st));  // the whole buffer
+    w->sflags_zero = false;
     // the whole heap, or one row's current version (IsElement)
     const uint64_t e_first = nrows == 1 ? t->h_beg[row0] : 0;
     const uint64_t ne = nrows == 1 ? t->h_len[row0] : t->nheap;
     HIP_TRY(launch_str_any(t->fp, e_first, ne, t->elem_row, t->live, row0, nrows, t->elem_off, t->chars,
-                           w->in2.as<uint8_t>(), nd, flags, wl.st));
+                           w->in2.as<uint8_t>(), nd, flags, wl.st, true));
     const uint32_t req = mode == 2 ? (1u << nvalues) - 1u : 0u;  // AND: every needle's bit
-    HIP_TRY(launch_byte_compact(flags, nrows, 0xFFu, w->misc.p, d_total, dst, wl.st, req));
+    HIP_TRY(launch_byte_compact(flags, nrows, 0xFFu, w->misc.p, d_total, dst, wl.st, req, true));
+    w->sflags_zero = true;
   }
   record_time(ctx, w, wl.st, false, 2);
   HIP_TRY(hipStreamSynchronize(wl.st));

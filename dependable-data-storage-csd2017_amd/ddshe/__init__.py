@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import threading
 
 import numpy as np
 
@@ -926,10 +927,18 @@ class StrTable:
                                       len(elem_off) - 1, row_off.ctypes.data_as(C.c_void_p), len(row_off) - 1,
                                       C.byref(h)), "dds_strtab_create")
         self._h = h
+        self._tls = threading.local()  # per-thread reply buffer of the scans (reused across calls)
 
     @property
     def nrows(self) -> int:
         return _lib.dds_strtab_rows(self._h)
+
+    def _reply(self) -> np.ndarray:
+        n = max(1, self.nrows)
+        buf = getattr(self._tls, "buf", None)
+        if buf is None or len(buf) < n:
+            buf = self._tls.buf = np.empty(n, dtype=np.uint32)
+        return buf
 
     def live_count(self) -> int:
         return _lib.dds_strtab_live_count(self._h)
@@ -985,7 +994,7 @@ class StrTable:
 
     def search_eq(self, position: int, value, negate: bool = False) -> np.ndarray:
         v = element_text(value).encode()
-        out = np.empty(max(1, self.nrows), dtype=np.uint32)
+        out = self._reply()
         n = C.c_size_t()
         _check(_lib.dds_search_eq(self._h, position, v, len(v), int(negate), out.ctypes.data_as(C.c_void_p),
                                   C.byref(n)), "dds_search_eq")
@@ -995,7 +1004,7 @@ class StrTable:
         vs = [element_text(v).encode() for v in values]
         arr = (C.c_char_p * len(vs))(*vs)
         lens = (C.c_size_t * len(vs))(*[len(v) for v in vs])
-        out = np.empty(max(1, self.nrows), dtype=np.uint32)
+        out = self._reply()
         n = C.c_size_t()
         _check(_lib.dds_search_entry(self._h, arr, lens, len(vs), int(require_all), out.ctypes.data_as(C.c_void_p),
                                      C.byref(n)), "dds_search_entry")
