@@ -1296,7 +1296,25 @@ class EntrySearchWorkload(_Workload):
                    roofline=roof, cpu_baseline=cpu, verified=ok, matches={"or": len(res[0]), "eq": len(res[1])})
         if mut is not None:
             out["resident_mutations"] = mut
+        if self.world == 1:
+            out["native_call"] = self.native_scan()
         return out
+
+    def native_scan(self):
+        """The same two routes from C++ (tools/native/scan_bench: the calls a JNA binding makes, without the
+        Python binding's marshalling) over its own seeded table of the same shape, every reply checked in
+        the child against a host scan."""
+        exe = os.path.join(ROOT, "tools", "native", "scan_bench")
+        if not os.path.exists(exe):
+            return {"skipped": "tools/native/scan_bench not built"}
+        import subprocess
+        try:
+            pr = subprocess.run([exe, str(self.mine)], capture_output=True, text=True, timeout=300)
+        except subprocess.TimeoutExpired:
+            return {"error": "timeout"}
+        if pr.returncode != 0:
+            return {"error": pr.stderr[-400:]}
+        return json.loads(pr.stdout.strip().splitlines()[-1])
 
     def close(self):
         self.tab.close()
