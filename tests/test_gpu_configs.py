@@ -156,3 +156,20 @@ def test_fold_buffer_pipelined_pieces(eng, keys):
     with pytest.raises(ddshe.DDSError) as ei:
         eng.fold_buffer(N, wide)
     assert ei.value.status == ddshe.DDS_E_RANGE
+
+
+def test_fold_buffer_pipelined_rsa_product(eng, keys):
+    """The pieced host-row fold on the RSA MultAll shape (2048-bit n, one bignum per lane for long
+    pieces): 2^21 + 3 random rows < n folded from a host buffer equal the resident column's fold."""
+    k = keys["rsa2048_seed3"]
+    n = k["n"]
+    rows = (1 << 21) + 3
+    col = eng.column(n, rows)
+    col.fill_random(2047, seed=9, row0=0, count=rows)
+    buf = col.read_buffer(0, rows)
+    want = col.fold()
+    col.close()
+    assert eng.fold_buffer(n, buf) == want
+    # and a prefix of the same buffer (one piece, ingest then fold) against the oracle
+    prefix = [int.from_bytes(buf[i].tobytes(), "big") for i in range(4000)]
+    assert eng.fold_buffer(n, buf[:4000]) == homo.modmul_fold(prefix, n)
