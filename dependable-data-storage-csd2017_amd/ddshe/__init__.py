@@ -934,10 +934,11 @@ class StrTable:
         return _lib.dds_strtab_rows(self._h)
 
     def _reply(self) -> np.ndarray:
+        # sized with slack: rows another thread appends between this read and the scan fit too
         n = max(1, self.nrows)
         buf = getattr(self._tls, "buf", None)
-        if buf is None or len(buf) < n:
-            buf = self._tls.buf = np.empty(n, dtype=np.uint32)
+        if buf is None or len(buf) < n + n // 8 + 1024:
+            buf = self._tls.buf = np.empty(n + n // 4 + 1024, dtype=np.uint32)
         return buf
 
     def live_count(self) -> int:
