@@ -312,3 +312,35 @@ def test_resident_order_into_engine_allocated_buffer(eng):
     finally:
         eng.host_free(buf)
         oc.close()
+
+
+def test_order_speculative_plan_concurrent(eng):
+    """Raw-array orderings from several threads at once, some with spans in the speculative plan's range
+    and some outside it (the plan flag is shared by the engine; each call checks its own plan on the
+    device and falls back on its own): every reply equals numpy's stable order."""
+    import threading
+    rng = np.random.default_rng(41)
+    n = 120_011
+    cols = []
+    for bits in (54, 30, 44, 60, 48, 20):
+        c = rng.integers(0, 1 << bits, size=n, dtype=np.int64) - (1 << (bits - 1))
+        c[:2] = [-(1 << (bits - 1)), (1 << (bits - 1)) - 1]
+        cols.append((c, (rng.random(n) > 0.1).astype(np.uint8)))
+    errors = []
+
+    def worker(t):
+        try:
+            for k in range(6):
+                col, valid = cols[(t + k) % len(cols)]
+                desc = bool((t + k) % 2)
+                if not np.array_equal(eng.ope_order(col, valid, desc), expected(col, valid, desc)):
+                    errors.append((t, k))
+        except Exception as e:  # noqa: BLE001
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
