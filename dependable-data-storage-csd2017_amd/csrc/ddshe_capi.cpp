@@ -2418,8 +2418,8 @@ int dds_ope_filter_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_v
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
     HIP_TRY(w->misc.ensure(ope_scratch_bytes(n)));
-    OrderHostWords hw;  // the match count is stored by the scatter into coherent mapped host memory: no copy
-    HIP_TRY(order_words(w, &hw));
+    MappedWords hw;  // the match count is stored by the scatter into coherent mapped host memory: no copy
+    HIP_TRY(mapped_words(w, &hw));
     hw.h[kCountWord] = 0;  // no rows: no scatter block stores it
     record_time(ctx, w, wl.st, true, 2);
     HIP_TRY(launch_ope_filter(d_col, d_valid, n, bound, op, w->misc.p, hw.d + kCountWord, d_out, wl.st));
@@ -2482,8 +2482,8 @@ int dds_ope_order_device(dds_ctx* ctx, const int64_t* d_col, const uint8_t* d_va
     if ((rc = wl.acquire())) return rc;
     Worker* w = wl.w;
     HIP_TRY(w->tab.ensure(rs_scratch_bytes(n)));
-    OrderHostWords ow;
-    HIP_TRY(order_words(w, &ow));
+    MappedWords ow;
+    HIP_TRY(mapped_words(w, &ow));
     HIP_TRY(launch_ope_order(d_col, d_valid, n, descending ? 1 : 0, w->tab.p, d_out_idx, wl.st, nullptr, &ow));
     HIP_TRY(hipStreamSynchronize(wl.st));
     return DDS_OK;
@@ -2507,8 +2507,8 @@ int dds_ope_order(dds_ctx* ctx, const int64_t* col, const uint8_t* valid, size_t
     HIP_TRY(hipMemcpyAsync(w->in.p, col, n * 8, hipMemcpyHostToDevice, wl.st));
     if (valid) HIP_TRY(hipMemcpyAsync(w->in2.p, valid, n, hipMemcpyHostToDevice, wl.st));
     HIP_TRY(w->tab.ensure(rs_scratch_bytes(n)));
-    OrderHostWords ow;
-    HIP_TRY(order_words(w, &ow));
+    MappedWords ow;
+    HIP_TRY(mapped_words(w, &ow));
     HIP_TRY(launch_ope_order(w->in.as<int64_t>(), valid ? w->in2.as<uint8_t>() : nullptr, n, descending ? 1 : 0,
                              w->tab.p, w->out.as<uint32_t>(), wl.st, nullptr, &ow));
     HIP_TRY(hipMemcpyAsync(out_idx, w->out.p, n * 4, hipMemcpyDeviceToHost, wl.st));

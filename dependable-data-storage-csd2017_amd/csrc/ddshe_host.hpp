@@ -108,7 +108,7 @@ struct Worker {
   uint32_t done_seq = 0;  // fold finalize: the last sequence number the root stored at kStageDoneWord
   HostBuf hcnt;    // coherent + mapped: the Search bitmask's per-tile match counts, stored by the device
   HostBuf hpair;   // pairwise batches: operands and results, coherent + mapped (k_pairs_sos reads and writes it)
-  HostBuf hord;    // coherent + mapped: the OPE ordering's bounds / overflow words (OrderHostWords)
+  HostBuf hord;    // coherent + mapped: small read-back words stored by kernels (MappedWords)
   HostBuf hscan;   // coherent + mapped: string-table scans' match count, needle bytes and row ids
   HostBuf hbig;    // large read-backs (Search ids / match masks, Order permutations) before the caller's copy
   DevBuf dch[2], doff[2], rflags;
@@ -355,10 +355,10 @@ inline hipError_t stage_ptr(Worker* w, uint32_t** p) {
   *p = e == hipSuccess ? (uint32_t*)w->hstage.p : nullptr;
   return e;
 }
-// the worker's OrderHostWords (launch_ope_order's read-back words, words 0..3; an OPE filter's match count
+// the worker's MappedWords (launch_ope_order's read-back words 0..3; an OPE filter's match count
 // at kCountWord), allocated on first use
 constexpr size_t kCountWord = 4;
-inline hipError_t order_words(Worker* w, OrderHostWords* ow) {
+inline hipError_t mapped_words(Worker* w, MappedWords* ow) {
   w->hord.flags = hipHostMallocCoherent | hipHostMallocMapped;
   hipError_t e = w->hord.ensure(64);
   ow->h = (volatile uint64_t*)w->hord.p;

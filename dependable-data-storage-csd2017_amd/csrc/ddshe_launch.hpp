@@ -151,13 +151,13 @@ size_t rs_scratch_bytes(size_t n);
 // the ordering stores its small read-backs into (bounds, overflow flag) instead of copying them back; with
 // it, a raw call whose previous raw call had a 40..56-bit key span runs the MSD plan without a mid-sort
 // host round trip (planned on the device, checked after)
-struct OrderHostWords {
+struct MappedWords {
   volatile uint64_t* h;
   uint64_t* d;
 };
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
                             uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds = nullptr,
-                            const OrderHostWords* hw = nullptr);
+                            const MappedWords* hw = nullptr);
 // deterministic-equality scans (ddshe_strscan.hip)
 // 64-bit digest of an element string (FNV-1a over the bytes, splitmix finaliser); identical on
 // host (needles) and device (table). The table keeps its top 32 bits as a per-element fingerprint.

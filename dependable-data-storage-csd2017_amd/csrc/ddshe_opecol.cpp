@@ -492,8 +492,8 @@ int dds_opecol_search(dds_opecol* col, const char* bound_dec, int op, uint32_t* 
     const size_t n = col->count;
     HIP_TRY(w->misc.ensure(ope_scratch_bytes(n)));
     HIP_TRY(w->out.ensure(n * 4));
-    OrderHostWords hw;  // the match count is stored by the scatter into coherent mapped host memory: no copy
-    HIP_TRY(order_words(w, &hw));
+    MappedWords hw;  // the match count is stored by the scatter into coherent mapped host memory: no copy
+    HIP_TRY(mapped_words(w, &hw));
     hw.h[kCountWord] = 0;  // no rows: no scatter block stores it
     record_time(ctx, w, wl.st, true, 2);
     HIP_TRY(launch_ope_filter(col->d_val, col->d_flg, n, sb.b, sb.gop, w->misc.p, hw.d + kCountWord,
@@ -636,8 +636,8 @@ int dds_opecol_order(dds_opecol* col, int descending, uint32_t* out_idx, size_t*
     // removed set's device byte is 0, so it sorts with them)
     const uint64_t ub[2] = {col->ulo, col->uhi};
     record_time(col->ctx, w, wl.st, true, 2);
-    OrderHostWords ow;
-    HIP_TRY(order_words(w, &ow));
+    MappedWords ow;
+    HIP_TRY(mapped_words(w, &ow));
     HIP_TRY(launch_ope_order(col->d_val, col->d_flg, n, descending ? 1 : 0, w->tab.p, w->out.as<uint32_t>(), wl.st,
                              ub, &ow));
     const uint32_t* res = w->out.as<uint32_t>();

@@ -888,7 +888,7 @@ constexpr int kSpecLo = 40, kSpecHi = 56;
 static std::atomic<int> g_order_spec{0};
 
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
-                            uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds, const OrderHostWords* hw) {
+                            uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds, const MappedWords* hw) {
   if (n == 0) return hipSuccess;
   const size_t nb = rs_blocks(n);
   uint64_t* ka = (uint64_t*)scratch;
