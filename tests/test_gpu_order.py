@@ -122,7 +122,7 @@ def test_order_sl_non_holders_32_rows(eng):
 
 
 @pytest.mark.parametrize("kind", ["uniform_2p40", "ope_map_ties", "block_buckets", "overflow_bucket", "span_2p56",
-                                  "span_2p57", "seam_two_keys"])
+                                  "span_2p57", "seam_two_keys", "ope_map_600", "ope_map_1000", "ope_map_150"])
 def test_order_msd_buckets(eng, kind):
     """Spans of > 24 bits over >= 65,536 rows take the MSD split: two stable passes over the top 16
     bits of the span, then each of the 65,536 buckets sorted by the rest of its keys (one wave up to
@@ -144,6 +144,12 @@ def test_order_msd_buckets(eng, kind):
         col[n // 2 :: 50] = (77 << 24) + 3
         col[1 : n // 2 : 50] = (78 << 24) + 1
         col[n // 2 + 1 :: 50] = (78 << 24) + 1
+    elif kind.startswith("ope_map_") and kind != "ope_map_ties":
+        # fewer distinct values, more rows each: two-key buckets of ~800 (1000 keys), ~1300 (600) and ~5300
+        # rows (150: past the register partition's 2048 rows), the sizes the 10M-row bench column has
+        nk = int(kind.rsplit("_", 1)[1])
+        ope_map = np.cumsum(rng.integers(1, 1 << 40, size=nk + 1, dtype=np.int64)) - (1 << 52)
+        col = ope_map[rng.integers(1, nk + 1, size=n)]
     elif kind == "ope_map_ties":  # the bench's generator: 10^4 distinct values, ~40 rows each here
         ope_map = np.cumsum(rng.integers(1, 1 << 40, size=10001, dtype=np.int64)) - (1 << 52)
         col = ope_map[rng.integers(1, 10001, size=n)]

@@ -28,10 +28,12 @@ def main(n=10_000_000, reps=15):
     for name, c in cols.items():
         d = torch.from_numpy(c).cuda()
         ts = []
+        print(name, flush=True)
         for r in range(reps + 2):
             torch.cuda.synchronize()
             t = time.perf_counter()
             eng.ope_order_device(d.data_ptr(), valid.data_ptr(), n, True, out.data_ptr())
+            torch.cuda.synchronize()
             ts.append((time.perf_counter() - t) * 1e3)
         ts = sorted(ts[2:])
         res[name] = round(ts[len(ts) // 2], 4)
