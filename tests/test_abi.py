@@ -56,6 +56,15 @@ def test_null_arguments_rejected():
     assert lib.dds_ctx_create(0, None) == ddshe.DDS_E_ARG
     assert lib.dds_col_count(None) == 0
     assert lib.dds_pair_timing(None, None, None, None, None) == ddshe.DDS_E_ARG
+    # round-5 entry points: a NULL context / table / column is an argument error, never a crash
+    assert lib.dds_pair_set_policy(None, ddshe.DDS_PAIR_HOST, None) == ddshe.DDS_E_ARG
+    assert lib.dds_pair_cpu(None, None, None, None, None, None, None) == ddshe.DDS_E_ARG
+    assert lib.dds_ope_order_device(None, None, None, 10, 1, None) == ddshe.DDS_E_ARG
+    assert lib.dds_sum_all_dec(None, None, 0, None, None, 0, None) == ddshe.DDS_E_ARG
+    import ctypes
+    got = ctypes.c_size_t()
+    assert lib.dds_opecol_search(None, b"0", 0, None, ctypes.byref(got)) == ddshe.DDS_E_ARG
+    assert lib.dds_search_entry(None, None, None, 0, 0, None, ctypes.byref(got)) == ddshe.DDS_E_ARG
 
 
 def test_synth_plaintexts_match_kernel_formula():
