@@ -9,7 +9,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FILES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r01_bench_*.json"))) + [
-    os.path.join(ROOT, "profiles", "r02_bench_default_final.json")]
+    os.path.join(ROOT, "profiles", "r02_bench_default_final.json")] + [
+    os.path.join(ROOT, "profiles", f"r05_{w}.json") for w in ("default", "pf", "order", "es")]
 
 TOP = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
        "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
@@ -63,3 +64,19 @@ def test_round2_default_line_carries_configs_3_and_4():
     assert 0 < f["frac"] <= 1 and f["traffic"] is not None
     assert d["latency"]["pair_sum_route_2048bit"]["matches"] is True
     assert d["latency"]["config1_sumall_10k_1024bit"]["matches"] is True
+
+
+def test_round5_default_line_boundary_and_latency():
+    """The round-5 default line: configs 3 and 4 verified, the host-boundary (end_to_end) routes matching the
+    resident fold, the host CPU per fold reported, and the /Sum native line served without errors."""
+    d = json.loads(open(os.path.join(ROOT, "profiles", "r05_default.json")).read())
+    for name in ("config3_product_filter", "config4_encrypt_sum"):
+        assert d["configs"][name].get("verified") is True, name
+    e = d["end_to_end"]
+    assert e["binary"]["matches"] and e["decimal"]["matches_resident_fold"] and e["strings"]["matches"]
+    folds = d["latency"]["host_cpu_per_fold"]["folds"]
+    assert [f["rows"] for f in folds] == [10_000, 1_000_000, 10_000_000]
+    big = folds[-1]
+    assert big["host_cpu_ms"] < 0.1 * big["wall_ms"]  # the long fold's caller sleeps, it does not spin
+    n = d["latency"]["pair_sum_route_native_threads_2048bit"]
+    assert n["errors"] == 0 and n["matches"] is True
