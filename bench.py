@@ -160,6 +160,7 @@ def main():
         elapsed = float(tt.item())
 
     # extra lines measured by every rank together (collectives inside), before rank 0 reports
+    wl.last_res = res
     extra = wl.extra_distributed() if not args.no_extras else {}
     out = None
     if rank == 0:
@@ -241,6 +242,13 @@ class _Workload:
 
     def extra_rank0(self):
         return {}
+
+    def all_ranks_ok(self, ok):
+        """N > 1: every rank's own check (its shard's result against its host restatement), min over ranks."""
+        import torch.distributed as dist
+        t = self.torch.tensor([1 if ok else 0], dtype=self.torch.int32, device=self.coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
 
     def fold_or_combine(self, col, modulus, count=None, rows_all=None):
         """One SumAll/MultAll fold over this rank's rows [0, count); N > 1: the partial is folded into a
@@ -1090,15 +1098,25 @@ class OrderWorkload(_Workload):
                                   self.d_out.data_ptr())
         return None
 
+    def local_ok(self):
+        """This rank's OrderLS permutation against numpy's stable argsort of its shard."""
+        import numpy as np
+        idx = np.arange(self.mine)
+        hold, rest = idx[self.valid != 0], idx[self.valid == 0]
+        want = np.concatenate([hold[np.argsort(~self.col[hold], kind="stable")], rest])
+        return bool(np.array_equal(self.d_out.cpu().numpy().view(np.uint32), want))
+
+    def extra_distributed(self):
+        if self.world == 1 or not self.args.verify:
+            return {}
+        return {"verified": self.all_ranks_ok(self.local_ok())}
+
     def report(self, res, elapsed):
         import numpy as np
         a = self.args
         ok = None
         if a.verify and self.world == 1:
-            idx = np.arange(self.mine)
-            hold, rest = idx[self.valid != 0], idx[self.valid == 0]
-            want = np.concatenate([hold[np.argsort(~self.col[hold], kind="stable")], rest])
-            ok = bool(np.array_equal(self.d_out.cpu().numpy().view(np.uint32), want))
+            ok = self.local_ok()
             if not ok:
                 print("VERIFY FAILED", file=sys.stderr)
         step_s = elapsed / a.steps
@@ -1243,15 +1261,25 @@ class EntrySearchWorkload(_Workload):
         b = self.tab.search_eq(3, self.needles[0])
         return a, b
 
+    def local_ok(self, res):
+        """This rank's SearchEntryOR / SearchEq rows against numpy over its own table."""
+        import numpy as np
+        p = self.pick.reshape(self.mine, self.ELEMS)
+        want_or = np.nonzero(np.isin(p, [11, 222, 3333]).any(axis=1))[0]
+        want_eq = np.nonzero(p[:, 3] == 11)[0]
+        return bool(np.array_equal(res[0], want_or) and np.array_equal(res[1], want_eq))
+
+    def extra_distributed(self):
+        if self.world == 1 or not self.args.verify:
+            return {}
+        return {"verified": self.all_ranks_ok(self.local_ok(self.last_res))}
+
     def report(self, res, elapsed):
         import numpy as np
         a = self.args
         ok = None
         if a.verify and self.world == 1:
-            p = self.pick.reshape(self.mine, self.ELEMS)
-            want_or = np.nonzero(np.isin(p, [11, 222, 3333]).any(axis=1))[0]
-            want_eq = np.nonzero(p[:, 3] == 11)[0]
-            ok = bool(np.array_equal(res[0], want_or) and np.array_equal(res[1], want_eq))
+            ok = self.local_ok(res)
             if not ok:
                 print("VERIFY FAILED", file=sys.stderr)
         _, _, dev_ms, _ = self.eng.timing()
