@@ -170,11 +170,15 @@ __host__ __device__ inline uint64_t str_digest(const uint8_t* p, uint64_t len) {
   h *= 0x94d049bb133111ebull;
   return h ^ (h >> 31);
 }
-struct StrNeedles {  // up to 3 items (SearchEntryAND/OR triplets), bytes in a device buffer
+struct StrNeedles {  // up to 3 items (SearchEntryAND/OR triplets), bytes in a device buffer or inline
   uint64_t h[3];
   uint64_t len[3];
   uint64_t off[3];
   int n;
+  // needles of up to kStrInline bytes in all travel in the kernel arguments (read from the kernarg
+  // segment on a fingerprint hit): no upload before the scan; the kernels get nchars == nullptr then
+  static constexpr int kStrInline = 128;
+  uint8_t inl[kStrInline];
 };
 hipError_t launch_str_digest(const uint8_t* chars, const uint64_t* elem_off, size_t nelems, uint32_t* fp,
                              hipStream_t st);
@@ -189,7 +193,8 @@ __device__ __forceinline__ bool str_hit(uint64_t e, int j, const uint64_t* __res
                                         const uint8_t* __restrict__ chars, const uint8_t* __restrict__ nchars,
                                         const StrNeedles& nd) {
   const uint64_t a = elem_off[e], b = elem_off[e + 1];
-  return b - a == nd.len[j] && str_equal(chars + a, nchars + nd.off[j], nd.len[j]);
+  const uint8_t* nb = nchars ? nchars : nd.inl;
+  return b - a == nd.len[j] && str_equal(chars + a, nb + nd.off[j], nd.len[j]);
 }
 #endif
 constexpr uint32_t kStrDead = 0xFFFFFFFFu;  // elem_row of a superseded element (ddshe_strscan.hip)

@@ -372,16 +372,21 @@ int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values
   uint64_t* d_total = (uint64_t*)ds;
   *(volatile uint64_t*)hs = 0;  // no rows: no scatter block stores the count
   uint32_t* dst = (uint32_t*)(ds + 64 + nbal);
-  if (!nb.empty()) {
+  // short needles ride in the kernel arguments (no upload); longer ones are DMA'd from pinned memory
+  const bool inl = nb.size() <= (size_t)StrNeedles::kStrInline;
+  if (inl) {
+    if (!nb.empty()) memcpy(nd.inl, nb.data(), nb.size());
+  } else {
     memcpy(hs + 64, nb.data(), nb.size());
     HIP_TRY(hipMemcpyAsync(w->in2.p, hs + 64, nb.size(), hipMemcpyHostToDevice, wl.st));
   }
+  const uint8_t* d_needles = inl ? nullptr : w->in2.as<uint8_t>();
   std::shared_ptr<PosIdx> px;
   if (mode == 0 && (rc = pos_index(t, position, wl.st, &px))) return rc;
   record_time(ctx, w, wl.st, true, 2);
   if (mode == 0) {  // SearchEq / NEq over the position index, straight into the compaction masks
     HIP_TRY(launch_str_eq_compact(px->fp, px->present, row0, nrows, t->row_beg, t->elem_off, t->chars,
-                                  w->in2.as<uint8_t>(), nd, position, negate, w->misc.p, d_total, dst, wl.st));
+                                  d_needles, nd, position, negate, w->misc.p, d_total, dst, wl.st));
   } else {
     // row flags: the worker's own buffer, kept zeroed between scans (the count pass re-zeroes what the
     // scan set); a fresh or possibly dirty buffer (an earlier scan that failed mid-way) is cleared first
@@ -395,7 +400,7 @@ int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values
     const uint64_t e_first = nrows == 1 ? t->h_beg[row0] : 0;
     const uint64_t ne = nrows == 1 ? t->h_len[row0] : t->nheap;
     HIP_TRY(launch_str_any(t->fp, e_first, ne, t->elem_row, t->live, row0, nrows, t->elem_off, t->chars,
-                           w->in2.as<uint8_t>(), nd, flags, wl.st, true));
+                           d_needles, nd, flags, wl.st, true));
     const uint32_t req = mode == 2 ? (1u << nvalues) - 1u : 0u;  // AND: every needle's bit
     HIP_TRY(launch_byte_compact(flags, nrows, 0xFFu, w->misc.p, d_total, dst, wl.st, req, true));
     w->sflags_zero = true;

@@ -323,3 +323,30 @@ def test_search_mask_engine_allocated_buffer(eng):
         col.close()
     with pytest.raises(DDSError):
         eng.host_free(buf)
+
+
+def test_scan_needles_inline_and_uploaded(eng):
+    """Needles of up to 128 bytes in all ride in the kernel arguments; longer ones are uploaded: both
+    forms, at the 128-byte edge and past it, answer SearchEntryOR / AND / SearchEq / IsElement as the
+    oracle does (long and short elements, fingerprint hits confirmed on the bytes)."""
+    rng = random.Random(77)
+    longs = [("L%x" % rng.getrandbits(64)) * 20 for _ in range(4)]      # ~340-byte elements
+    shorts = [f"s{rng.getrandbits(24):x}" for _ in range(30)]
+    edge = ["e" * 42, "f" * 43, "g" * 43]                                   # 128 bytes in all
+    words = longs + shorts + edge
+    rows = [[rng.choice(words) for _ in range(rng.randrange(0, 7))] for _ in range(3000)]
+    tab = eng.strtab(rows)
+    keyed = list(enumerate(rows))
+    cases = [shorts[:3], edge, edge[:2] + ["h"], longs[:1], longs[:2] + shorts[:1], [longs[3]]]
+    for v in cases:
+        for route, req in (("SearchEntryOR", False), ("SearchEntryAND", True)):
+            if route == "SearchEntryAND" and len(set(v)) < 3:
+                continue
+            assert tab.search_entry(v, req).tolist() == sorted(homo.search_entry(route, keyed, v)), (route, v)
+    for value in (longs[0], edge[1], shorts[5]):
+        for position in (0, 2):
+            assert tab.search_eq(position, value).tolist() == sorted(homo.search_eq("SearchEq", keyed, position,
+                                                                                   value)), (position, value)
+    r = next(i for i, row in enumerate(rows) if longs[1] in row)
+    assert tab.is_element(r, longs[1])
+    tab.close()
