@@ -8,8 +8,11 @@ range over the ranks. Each rank folds its shard to one partial on its GPU; for N
 the partials (608 B each) are gathered over RCCL and combined on rank 0's GPU.
 value = (k - 1) HomoAdd operations per step * steps / (max-over-ranks wall time).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU).
+Launch: python bench.py [--gpus N --steps K --warmup W]. For N > 1 either under
+torch.distributed.run (one process per GPU, WORLD_SIZE = N), or directly: without WORLD_SIZE the
+process starts N ranks itself (a torch.distributed.run child, before any GPU call), relays rank
+0's JSON line and exits with the child's status. Fewer than N visible devices is an error
+(exit 2), never a silent one-GPU line; DDSHE_DIST_BACKEND=gloo rehearses N ranks on one device.
 """
 from __future__ import annotations
 
@@ -66,9 +69,60 @@ def binary_ladder_modmuls(e: int, m_bits: int = 14) -> int:
     return (e.bit_length() - 1) + (m_bits - 1) + (bin(e).count("1") - 1) + (m_bits // 2 - 1) + 1
 
 
+def visible_devices() -> int:
+    """GPUs this process can see. torch.cuda.device_count() counts them without initialising HIP on
+    this image, so the launcher may call it before it starts the ranks."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(n: int, backend: str) -> int:
+    """`python bench.py --gpus N` without WORLD_SIZE: run the N ranks as one torch.distributed.run
+    child (127.0.0.1 rendezvous on a free port, the same command line otherwise), relay rank 0's JSON
+    line after checking it reports n_gpus == N, and return the child's exit status (non-zero when any
+    rank failed). The parent makes no GPU call and never exec()s."""
+    import socket
+    import subprocess
+    have = visible_devices()
+    need = n if backend == "nccl" else 1
+    if have < need:
+        print(f"bench.py: --gpus {n} needs {need} visible GPU(s) for the {backend} backend, found {have}; "
+              "refusing to report a smaller run", file=sys.stderr)
+        return 2
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool (RCCL peer buffers)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    child = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    lines = []
+    for line in child.stdout:  # ranks' other output passes through to stderr as it comes
+        if line.lstrip().startswith("{"):
+            lines.append(line.strip())
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    rc = child.wait()
+    if rc != 0:
+        print(f"bench.py: ranks exited with status {rc}", file=sys.stderr)
+        return rc
+    if len(lines) != 1:
+        print(f"bench.py: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
+        return 3
+    if json.loads(lines[0]).get("n_gpus") != n:
+        print(f"bench.py: rank 0 reported n_gpus != {n}", file=sys.stderr)
+        return 3
+    print(lines[0], flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default WORLD_SIZE under torch.distributed.run, else 1")
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--workload", choices=("sum", "product_filter", "encrypt_sum", "order", "entry_search"),
@@ -99,18 +153,35 @@ def main():
     args.steps = dflt[1] if args.steps is None else args.steps
     args.warmup = dflt[2] if args.warmup is None else args.warmup
     args.seed = dflt[3] if args.seed is None else args.seed
+    # DDSHE_DIST_BACKEND=gloo rehearses the N > 1 flow with every rank on one GPU (the partial
+    # gather then goes through host memory); the driver's multi-GPU runs use RCCL ("nccl").
+    backend = os.environ.get("DDSHE_DIST_BACKEND", "nccl")
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus is None:
+        args.gpus = int(env_world) if env_world else 1
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args.gpus, backend)
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
+        return 2
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = args.gpus
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # DDSHE_DIST_BACKEND=gloo rehearses the N > 1 flow with every rank on one GPU (the partial
-    # gather then goes through host memory); the driver's multi-GPU runs use RCCL ("nccl").
-    backend = os.environ.get("DDSHE_DIST_BACKEND", "nccl")
+    devices = visible_devices()
     if backend == "gloo":
-        local = local % max(1, torch.cuda.device_count())
+        if devices < 1:
+            print("bench.py: no visible GPU", file=sys.stderr)
+            return 2
+        local = local % devices
+    elif devices <= local:
+        print(f"bench.py: rank {rank} needs device {local}, {devices} visible", file=sys.stderr)
+        return 2
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -159,13 +230,20 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    # extra lines measured by every rank together (collectives inside), before rank 0 reports
+    # every rank's own check of its shard (N > 1, whatever --no-extras says), then the extra lines
+    # measured by every rank together (collectives inside), before rank 0 reports
     wl.last_res = res
+    ranks_ok = wl.verify_distributed() if world > 1 and args.verify else None
     extra = wl.extra_distributed() if not args.no_extras else {}
     out = None
     if rank == 0:
         out = wl.report(res, elapsed)
         out["fill_s"] = t_fill
+        if ranks_ok is not None:
+            out["verified"] = ranks_ok if out.get("verified") is None else bool(out["verified"] and ranks_ok)
+        out["config"]["distinct_devices"] = min(world, devices)
+        if backend == "gloo" and world > 1:
+            out["config"]["note"] = f"gloo rehearsal: {world} ranks on {min(world, devices)} device(s)"
         out.update(extra)
     wl.close()
     if not args.no_extras:
@@ -179,12 +257,13 @@ def main():
         if world > 1:
             dist.barrier()
     if rank == 0:
-        print(json.dumps(out))
+        assert out["n_gpus"] == args.gpus, (out["n_gpus"], args.gpus)
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     eng.close()
-    return out
+    return 0
 
 
 class _Workload:
@@ -236,6 +315,11 @@ class _Workload:
                 "tail_plus_combine_share": (tail_ms + comb_ms) / (share_ms + comb_ms) if tail_ms else None,
                 "note": "an 8-GPU strong-split step is about share_fold_partial_ms + one all-gather of "
                         f"{parts}x{4 * pw} B + combine_ms (host wall clock, each call synchronised)"}
+
+    def verify_distributed(self):
+        """N > 1 and --verify: each rank's check of its own shard, min over ranks (collective: every
+        rank calls it); None where rank 0's report verifies the combined result instead."""
+        return None
 
     def extra_distributed(self):
         return {}
@@ -389,8 +473,10 @@ class SumWorkload(_Workload):
                            "value": (a.strong_rows - 1) * a.steps / el, "unit": "HomoAdd/s", "n_gpus": self.world,
                            "rows": a.strong_rows, "steps": a.steps, "ms_per_step": el / a.steps * 1e3,
                            "scaling": "strong", "verified": ok,
-                           "partials": "device-to-device: dds_col_fold_partial_device -> RCCL all_gather_into_tensor"
-                                       " -> dds_combine_partials_device"}}
+                           "partials": "dds_col_fold_partial_device -> all_gather_into_tensor ("
+                                       + ("RCCL, device to device" if self.coll_dev.type == "cuda" else
+                                          "gloo rehearsal, staged through host memory")
+                                       + ") -> dds_combine_partials_device"}}
 
     def extra_rank0(self):
         out = {"single_process_multi_gpu": self.single_process_line()}
@@ -404,10 +490,10 @@ class SumWorkload(_Workload):
         a JNA caller uses): args.strong_rows rows sharded in 64-row blocks, every shard folded on its
         own GPU, partials copied device-to-device (xGMI peer copies) and combined on GPU 0."""
         a, torch = self.args, self.torch
-        if torch.cuda.device_count() < self.world:
-            return {"skipped": f"{torch.cuda.device_count()} visible devices < {self.world}"}
+        if torch.cuda.device_count() < a.gpus:
+            return {"skipped": f"{torch.cuda.device_count()} visible devices < {a.gpus}"}
         k, rows = self.key, a.strong_rows
-        m = self.ddshe.MultiEngine(list(range(self.world)))
+        m = self.ddshe.MultiEngine(list(range(a.gpus)))
         col = m.column(self.nsq, rows)
         col.fill_paillier_synth(k["n"], k["g"], a.seed, rows, a.pool)
         for _ in range(a.warmup):
@@ -424,7 +510,7 @@ class SumWorkload(_Workload):
         col.close()
         m.close()
         return {"metric": "Paillier homomorphic adds/sec (2048-bit key, mod n^2), one process, all GPUs",
-                "value": (rows - 1) * a.steps / el, "unit": "HomoAdd/s", "n_gpus": self.world, "rows": rows,
+                "value": (rows - 1) * a.steps / el, "unit": "HomoAdd/s", "n_gpus": a.gpus, "rows": rows,
                 "steps": a.steps, "ms_per_step": el / a.steps * 1e3, "scaling": "strong", "verified": ok,
                 "path": "dds_mcol_fold: shard folds on their GPUs, hipMemcpyPeerAsync of the partials, combine on GPU 0"}
 
@@ -1106,10 +1192,8 @@ class OrderWorkload(_Workload):
         want = np.concatenate([hold[np.argsort(~self.col[hold], kind="stable")], rest])
         return bool(np.array_equal(self.d_out.cpu().numpy().view(np.uint32), want))
 
-    def extra_distributed(self):
-        if self.world == 1 or not self.args.verify:
-            return {}
-        return {"verified": self.all_ranks_ok(self.local_ok())}
+    def verify_distributed(self):
+        return self.all_ranks_ok(self.local_ok())
 
     def report(self, res, elapsed):
         import numpy as np
@@ -1269,10 +1353,8 @@ class EntrySearchWorkload(_Workload):
         want_eq = np.nonzero(p[:, 3] == 11)[0]
         return bool(np.array_equal(res[0], want_or) and np.array_equal(res[1], want_eq))
 
-    def extra_distributed(self):
-        if self.world == 1 or not self.args.verify:
-            return {}
-        return {"verified": self.all_ranks_ok(self.local_ok(self.last_res))}
+    def verify_distributed(self):
+        return self.all_ranks_ok(self.local_ok(self.last_res))
 
     def report(self, res, elapsed):
         import numpy as np
@@ -1421,4 +1503,4 @@ def cpu_baseline(col, nsq, mb, seconds):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

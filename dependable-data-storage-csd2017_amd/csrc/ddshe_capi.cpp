@@ -429,15 +429,25 @@ int reduce_leaves(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const 
   if (spin) {
     // bounded: past 50 ms of spinning, or 60 s of naps (a loaded GPU, a fault), the stream
     // synchronisation decides
+    // synchronisation decides; a napping caller also asks the stream every ~2 ms, so a kernel that
+    // failed asynchronously (the word then never changes) is reported at once, not after 60 s
     const auto t0 = std::chrono::steady_clock::now();
     const auto limit = nap ? std::chrono::milliseconds(60000) : std::chrono::milliseconds(50);
+    int naps = 0;
     while (*dflag != seq) {
       if (std::chrono::steady_clock::now() - t0 > limit) {
         HIP_TRY(hipStreamSynchronize(st));
         break;
       }
-      if (nap) std::this_thread::sleep_for(std::chrono::microseconds(50));
-      else __builtin_ia32_pause();
+      if (nap) {
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (++naps % 40 == 0 && hipStreamQuery(st) != hipErrorNotReady) {
+          HIP_TRY(hipStreamSynchronize(st));  // done (the word is then set too) or an error to report
+          break;
+        }
+      } else {
+        __builtin_ia32_pause();
+      }
     }
     std::atomic_thread_fence(std::memory_order_acquire);
   } else {

@@ -80,9 +80,15 @@ std::shared_ptr<const bn::Barrett64> barrett_of(dds_ctx* ctx, const bn::Limbs& M
   return b;
 }
 
-void host_product(dds_ctx* ctx, const bn::Barrett64& bar, PairReq* req) {
+// never throws: an allocation failure becomes req->rc = DDS_E_NOMEM, so a caller that raised a queue's
+// host_busy around it always gets to lower it again
+void host_product(dds_ctx* ctx, const bn::Barrett64& bar, PairReq* req) noexcept {
   const uint64_t c0 = cpu_ns();
-  req->r = bn::barrett64_modmul(bar, req->a, req->b);
+  try {
+    req->r = bn::barrett64_modmul(bar, req->a, req->b);
+  } catch (...) {
+    req->rc = DDS_E_NOMEM;
+  }
   ctx->pair_cpu_ns[kCpuHost].fetch_add(cpu_ns() - c0);
   ctx->pair_host_calls.fetch_add(1);
 }
@@ -236,7 +242,7 @@ int modmul_coalesced(dds_ctx* ctx, const bn::Limbs& M, PairReq* req,
   const int policy = pair_policy(ctx);
   if (policy == DDS_PAIR_HOST) {
     host_product(ctx, *bar, req);
-    return DDS_OK;
+    return req->rc;
   }
   const uint64_t c_in = cpu_ns();
   uint64_t c_batch = 0;  // CPU of the batches this caller led (counted in their own phases)

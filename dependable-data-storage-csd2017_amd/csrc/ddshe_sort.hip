@@ -847,7 +847,7 @@ size_t rs_blocks(size_t n) { return (n + kRsTile - 1) / kRsTile; }
 size_t rs_scratch_bytes(size_t n) {
   // keys x2 (8 B), ids x1 extra (4 B; the other id buffer is the caller's output), histogram, OR/AND,
   // MSD bucket starts + control words + big-bucket list
-  return 2 * n * 8 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 1024 +
+  return 2 * n * 8 + 32 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 1024 +
          (size_t)kRsDigits * ((rs_blocks(n) + kScanTiles - 1) / kScanTiles) * 4 + 256 +
          16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows)) + 800 + (8 * (size_t)kMsdBuckets + 8) * 4;
 }
@@ -914,7 +914,10 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   if (n == 0) return hipSuccess;
   const size_t nb = rs_blocks(n);
   uint64_t* ka = (uint64_t*)scratch;
-  uint64_t* kb = ka + n;
+  // split keys keep their high words at word round_up(n, 4) of ka (16-byte aligned: the last histogram
+  // reads them four rows per uint4), so kb starts 16 bytes past an even row count
+  const size_t hi_word = (n + 3) & ~(size_t)3;
+  uint64_t* kb = ka + ((n + 1) & ~(size_t)1) + 2;
   uint32_t* ib = (uint32_t*)(kb + n);
   uint32_t* hist = (uint32_t*)(((uintptr_t)(ib + n) + 255) & ~(uintptr_t)255);
   uint32_t* dtot = hist + (size_t)kRsDigits * nb;
@@ -947,7 +950,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     const uint64_t* kin = (const uint64_t*)col;  // raw column before the first pass
     uint64_t* kout = ka;
     const MsdRuns none{};
-    uint32_t* hi = split ? reinterpret_cast<uint32_t*>(ka) + n : nullptr;  // ka = [low n words | high n words]
+    uint32_t* hi = split ? reinterpret_cast<uint32_t*>(ka) + hi_word : nullptr;  // ka = [low n words | high n words]
     for (int j = 0; j < np; ++j) {
       uint32_t* ids_out = ((np - 1 - j) % 2 == 0) ? fin : tmp;
       const bool last = j == np - 1;

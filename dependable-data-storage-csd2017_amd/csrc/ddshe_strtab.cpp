@@ -403,12 +403,13 @@ int str_scan(dds_strtab* t, size_t row0, size_t nrows, const char* const* values
                            d_needles, nd, flags, wl.st, true));
     const uint32_t req = mode == 2 ? (1u << nvalues) - 1u : 0u;  // AND: every needle's bit
     HIP_TRY(launch_byte_compact(flags, nrows, 0xFFu, w->misc.p, d_total, dst, wl.st, req, true));
-    w->sflags_zero = true;
   }
   record_time(ctx, w, wl.st, false, 2);
   HIP_TRY(hipStreamSynchronize(wl.st));
   const uint64_t total = *(volatile uint64_t*)hs;
   if (total > nrows) return fail(DDS_E_HIP, "scan count out of range");
+  // the count pass re-zeroed the flags it read: clean only once the stream finished and the count is sane
+  if (mode != 0) w->sflags_zero = true;
   if (total) memcpy(out_rows, hs + 64 + nbal, total * 4);
   if (ctx->timing.load()) {
     float ms = 0;

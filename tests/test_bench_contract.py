@@ -30,7 +30,9 @@ def test_bench_line_contract(path):
     d = json.loads(lines[0])
     assert TOP <= set(d), TOP - set(d)
     assert d["value"] > 0 and d["ms_per_step"] > 0 and d["steps"] >= 1
-    assert d["n_gpus"] == 1 and d["scaling"] in ("weak", "strong")
+    # n_gpus is the rank count the run was asked for (bench.py asserts it equals --gpus before printing)
+    assert d["n_gpus"] >= 1 and d["config"]["parallelism"] == f"rows-sharded x{d['n_gpus']}"
+    assert d["scaling"] in ("weak", "strong")
     assert d["higher_is_better"] is True
     assert "workload" in d["config"]
     assert ROOF <= set(d["roofline"]), ROOF - set(d["roofline"])

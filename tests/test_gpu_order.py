@@ -350,3 +350,27 @@ def test_order_speculative_plan_concurrent(eng):
     for x in th:
         x.join()
     assert not errors, errors
+
+
+@pytest.mark.parametrize("n", [65_536, 131_071, 131_072, 131_073, 131_074, 133_123])
+def test_order_msd_tile_edges(eng, n):
+    """Edges of the MSD path's indexing: row counts at and around a
+    multiple of the 2048-row tile and of the 64-tile scan chunk (131,072 = 64 tiles), every n % 4 (the
+    split keys' high words are read four rows per 16-byte load; their array starts 16-byte aligned), and
+    the buckets at both ends of the key span crowded, with the largest keys in the column's last rows, so
+    the last tile, the last scan chunk and the last MSD bucket all reach row n - 1. Each size is ordered
+    twice per direction: the second raw call runs the device-planned (speculative) MSD path."""
+    rng = np.random.default_rng(n)
+    span = 1 << 46
+    col = rng.integers(0, span, size=n, dtype=np.int64) - (1 << 45)
+    lo_rows = rng.choice(n - 600, size=700, replace=False)
+    col[lo_rows] = -(1 << 45) + rng.integers(0, 5, size=700)          # bucket 0: 5 keys, 700 rows
+    col[-600:] = (1 << 45) - 1 - rng.integers(0, 3, size=600)          # last bucket, at the column end
+    col[-1] = (1 << 45) - 1
+    valid = (rng.random(n) > 0.05).astype(np.uint8)
+    valid[-1] = 1
+    for desc in (True, False):
+        want = expected(col, valid, desc)
+        for _ in range(2):
+            assert np.array_equal(eng.ope_order(col, valid, desc), want), (n, desc)
+    assert np.array_equal(eng.ope_order(col, None, False), np.argsort(col, kind="stable"))
