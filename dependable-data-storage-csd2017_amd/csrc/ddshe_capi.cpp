@@ -295,6 +295,33 @@ int fold_level1(dds_ctx* ctx, Worker* w, hipStream_t st, ModConsts& mc, const ui
   size_t G = std::min(gmax, std::max<size_t>(1, count / 2));
   size_t ps = round_up(G, 64);
   HIP_TRY(w->p0.ensure((size_t)S2 * ps * 4));
+  // DDSHE_FOLD_INBLOCK=1 (A/B, off by default): level 1 with the in-block tree (k_fold InBlock), one
+  // row-major leaf per block straight to the reduction tree instead of the tail launches that take the
+  // G partials down to tree_switch_leaves(). Measured slower (profiles/r06_inblock_ab.txt: headline
+  // level 1 14.6 -> 15.7 ms, the strong-split share 1.75 -> 2.11 ms): the in-block products run in the
+  // throughput shape (4 lanes per bignum), whose per-product latency is ~4x the tail shape's.
+  static const int inblock = [] {
+    const char* e = getenv("DDSHE_FOLD_INBLOCK");
+    return e ? atoi(e) : 0;
+  }();
+  const size_t gpb = 256 / (size_t)pick_tpi(S);
+  const size_t Gb = G / gpb * gpb;  // whole blocks of live groups
+  if (inblock && use_tree() && !S1 && !d_ids && mc.dqm && S2 >= S && Gb > tree_switch_leaves()) {
+    G = Gb;
+    const size_t B = G / gpb;
+    record_time(ctx, w, st, true, 0);
+    HIP_TRY(launch_fold(S, X, xstride, count, mc.d, mc.dqm, mc.n0, w->p0.as<uint32_t>(), 1, G, S2, st, nullptr, 0,
+                        (size_t)S2));
+    record_time(ctx, w, st, false, 0);
+    if (ctx->timing.load()) {
+      w->timed_fold = true;
+      std::lock_guard<std::mutex> lk(ctx->tmu);
+      ctx->pending_modmuls = count - B;  // the row products and the in-block ones
+    }
+    *lv = Leaves{w->p0.as<uint32_t>(), 1, S2, mc.W, B, (int64_t)mc.W * S * ((int64_t)B - (int64_t)count), nullptr,
+                 (size_t)S2};
+    return DDS_OK;
+  }
   record_time(ctx, w, st, true, 0);
   HIP_TRY(launch_fold(S, X, xstride, count, mc.d, mc.dqm, mc.n0, w->p0.as<uint32_t>(), ps, G, S2, st, d_ids, S1));
   record_time(ctx, w, st, false, 0);

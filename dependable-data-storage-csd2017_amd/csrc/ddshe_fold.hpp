@@ -97,7 +97,14 @@ struct Grp {
 // level in the latency shape straight from the main-shape rows; the missing top limbs read as 0).
 // Partial g goes to P[l * pstride + g * pgs] (limb-major by default; row-major for a launch that hands
 // its partials to the reduction tree, whose blocks then read each leaf as one contiguous run).
-template <int S, int TPI, int W, bool QP = false, bool Idx = false, bool Narrow = false>
+// InBlock: the block's 256 / TPI partials are folded together before the kernel ends (a tree through
+// LDS: at each level the upper half of the live groups parks its values, the lower half multiplies them
+// in with mul_lds), and group 0 writes ONE partial per block, row-major with pgs words per leaf (limbs
+// S..pgs zeroed: the tree's leaf shape), at leaf blockIdx.x. Every group of every block must be live
+// (ngroups a multiple of 256 / TPI: the launcher checks). The block partial holds prod * R^(1 - c) with
+// c the block's rows, as a group's partial does (each in-block product contributes one R^-1 and one
+// more group). This replaces the tail launches between level 1 and the tree.
+template <int S, int TPI, int W, bool QP = false, bool Idx = false, bool Narrow = false, bool InBlock = false>
 __global__ void __launch_bounds__(256, 2) k_fold(const uint32_t* __restrict__ X, size_t xstride, size_t count,
                                               const uint32_t* __restrict__ consts, uint32_t n0,
                                               uint32_t* __restrict__ P, size_t pstride, size_t ngroups,
@@ -137,6 +144,31 @@ __global__ void __launch_bounds__(256, 2) k_fold(const uint32_t* __restrict__ X,
     }
   }
   M::normalize(a, g.bottom);
+  if constexpr (InBlock) {
+    constexpr int GPB = 256 / TPI;  // groups per block
+    __shared__ uint32_t slot[(GPB / 2) * S];
+    const int gi = (int)(threadIdx.x / TPI);
+    for (int h = GPB / 2; h >= 1; h >>= 1) {
+      if (gi >= h && gi < 2 * h) {
+        uint32_t* dst = slot + (gi - h) * S + g.r * L;
+#pragma unroll
+        for (int l = 0; l < L; ++l) dst[l] = a[l];
+      }
+      __syncthreads();
+      if (gi < h) {
+        M::mul_lds(a, n, slot + gi * S, n0, g.top, g.bottom);
+        M::normalize(a, g.bottom);
+      }
+      __syncthreads();  // the slots are rewritten by the next level
+    }
+    if (gi == 0) {
+      uint32_t* leaf = P + (size_t)blockIdx.x * pgs;
+#pragma unroll
+      for (int l = 0; l < L; ++l) leaf[g.r * L + l] = a[l];
+      for (size_t l = S + g.r; l < pgs; l += TPI) leaf[l] = 0u;
+    }
+    return;
+  }
   g.store_col(a, P, pstride, grp * pgs);  // pstride = 1, pgs = S: row-major partials (the tree's leaves)
 }
 

@@ -321,8 +321,21 @@ __global__ void __launch_bounds__(256, 2) k_modexp_pre(const uint32_t* __restric
 // idx + 1 == 0: squarings only. nsched == 0: E == 0 (x^0 = 1).
 // QP: every product but the last against N~ = N·n0 (values < 2N~); the last one, against N,
 // leaves the Montgomery form below 2N (R > 2N~) for the canonical reduction.
+// Occupancy: one S-word LDS slot per group (x^E·R is parked in the group's output row in HBM while
+// g^m is computed, not in a second slot) and at most 168 VGPRs, so three waves per SIMD hide the
+// squarings' serial parts (the LDS round trip of the operand, the settle/normalise carry chains);
+// DDSHE_LADDER_OCC2=1 builds the previous two-wave form (two slots, 172 VGPRs) for A/B.
+// Shapes of more than 29 limbs per lane keep two waves (a 168-VGPR bound spills them heavily).
+template <int S, int TPI>
+constexpr int ladder_waves() {
+#ifdef DDSHE_LADDER_OCC2
+  return 2;
+#else
+  return S / TPI <= 29 ? 3 : 2;
+#endif
+}
 template <int S, int TPI, int W, bool QP = false>
-__global__ void __launch_bounds__(256, 2) k_modexp_ladder(const uint32_t* __restrict__ Tab, size_t tstride,
+__global__ void __launch_bounds__(256, (ladder_waves<S, TPI>())) k_modexp_ladder(const uint32_t* __restrict__ Tab, size_t tstride,
                                                        const uint32_t* __restrict__ m, size_t count,
                                                        const uint32_t* __restrict__ consts,
                                                        const uint32_t* __restrict__ qp_mod,
@@ -336,8 +349,12 @@ __global__ void __launch_bounds__(256, 2) k_modexp_ladder(const uint32_t* __rest
   G g;
   const size_t grp = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / TPI;
   if (grp >= count) return;
+#ifdef DDSHE_LADDER_OCC2
   uint32_t* sq = lds + (size_t)(threadIdx.x / TPI) * 2 * S;  // group-private operand slots
   uint32_t* xs = sq + S;
+#else
+  uint32_t* sq = lds + (size_t)(threadIdx.x / TPI) * S;  // group-private operand slot
+#endif
   uint32_t n[L], acc[L];
   g.load_vec(n, QP ? qp_mod : consts + kConstN * S);
   if (nsched > 0) g.load_col(acc, Tab + (size_t)sched[0] * S * tstride, tstride, grp);
@@ -360,7 +377,14 @@ __global__ void __launch_bounds__(256, 2) k_modexp_ladder(const uint32_t* __rest
     uint32_t wb = mi ? 32u - (uint32_t)__builtin_clz(mi) : 0u;
     for (int off = 32; off >= 1; off >>= 1) wb = max(wb, (uint32_t)__shfl_xor((int)wb, off));
     M::normalize(acc, g.bottom);
+#ifdef DDSHE_LADDER_OCC2
     store_lds<S, TPI, W>(xs, acc, g.r);  // park x^E*R in xs; acc is reused for g^m
+#else
+    // park x^E*R in this group's output row (read back by mul_col below: other lanes' limbs, so the
+    // stores must have landed — workgroup fence: vmcnt(0), the write-through L1 serves the reloads)
+    g.store_col(acc, O, ostride, grp);
+    __threadfence_block();
+#endif
     g.load_vec(acc, consts + kConstRmod * S);
     for (int i = (int)wb - 1; i >= 0; --i) {
       M::normalize(acc, g.bottom);
@@ -372,7 +396,11 @@ __global__ void __launch_bounds__(256, 2) k_modexp_ladder(const uint32_t* __rest
       M::mul_lds(acc, n, sq, n0, g.top, g.bottom);
     }
     // acc = (g^m R) * (x^E R) * R^-1
+#ifdef DDSHE_LADDER_OCC2
     M::mul_lds(acc, n, xs, n0, g.top, g.bottom);
+#else
+    M::mul_col(acc, n, O, ostride, (uint32_t)grp, n0, g.top, g.bottom);
+#endif
   }
   if constexpr (QP) g.load_vec(n, consts + kConstN * S);
   Mont<S, TPI, W>::mul_col(acc, n, consts + kConstOne * S, 1, 0, n0, g.top, g.bottom);  // leave Montgomery form
@@ -1035,8 +1063,9 @@ hipError_t launch_reduce_rows(int S, uint32_t* X, size_t stride, size_t count, c
 
 hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, const uint32_t* consts,
                        const uint32_t* qp_mod, uint32_t n0, uint32_t* P, size_t pstride, size_t ngroups, int s_out,
-                       hipStream_t st, const uint32_t* ids, int lane1) {
+                       hipStream_t st, const uint32_t* ids, int lane1, size_t inblock_pgs) {
   if (ngroups == 0 || ngroups > count) return hipErrorInvalidValue;
+  if (inblock_pgs) s_out = 0;  // the kernel zeroes the leaves' upper limbs itself
   if (lane1 && !(fold1_shape(S) && (lane1 == S || (S == 76 && lane1 == 74)))) return hipErrorInvalidValue;
   const int sw = lane1 ? lane1 : S;  // limbs the kernel writes
   // limbs sw..s_out of the partials (tail shape is wider): zero, contiguous in the limb-major layout
@@ -1074,6 +1103,15 @@ hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, c
     return hipGetLastError();
   }
   const uint32_t* c = qp_mod ? qp_mod : consts;  // N~ = N·n0 in place of N (Mont QP): no v_mul_lo per CIOS step
+  if (inblock_pgs) {  // one partial per block (k_fold InBlock), row-major leaves of inblock_pgs words
+    if (!qp_mod || ids || lane1) return hipErrorInvalidValue;
+    DDSHE_SWITCH(S, {
+      if (ngroups % (256 / TPI) != 0 || inblock_pgs < (size_t)S) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((k_fold<S, TPI, W, true, false, false, true>), dim3(grid_for(ngroups * TPI)), dim3(256), 0,
+                         st, X, xstride, count, c, n0, P, 1, ngroups, nullptr, S, inblock_pgs);
+    });
+    return hipGetLastError();
+  }
   if (qp_mod && ids) {
     DDSHE_SWITCH(S, hipLaunchKernelGGL((k_fold<S, TPI, W, true, true>), dim3(grid_for(ngroups * TPI)), dim3(256), 0, st, X, xstride, count, c,
                                        n0, P, pstride, ngroups, ids));
@@ -1308,6 +1346,11 @@ hipError_t launch_modexp_pre(int S, const uint32_t* Xcol, size_t xstride, size_t
   return hipGetLastError();
 }
 
+#ifdef DDSHE_LADDER_OCC2
+constexpr int kLadderSlots = 2;
+#else
+constexpr int kLadderSlots = 1;
+#endif
 hipError_t launch_modexp_ladder(int S, const uint32_t* Tab, size_t tstride, const uint32_t* m, size_t count,
                                 const uint32_t* consts, const uint32_t* qp_mod, const uint32_t* gR,
                                 const uint32_t* sched, int nsched, uint32_t n0, uint32_t* O, size_t ostride,
@@ -1315,11 +1358,11 @@ hipError_t launch_modexp_ladder(int S, const uint32_t* Tab, size_t tstride, cons
   if (count == 0) return hipSuccess;
   if (qp_mod) {
     DDSHE_SWITCH(S, hipLaunchKernelGGL((k_modexp_ladder<S, TPI, W, true>), dim3(grid_for(count * TPI)), dim3(256),
-                                       (256 / TPI) * 2 * S * 4, st, Tab, tstride, m, count, consts, qp_mod, gR, sched,
+                                       (256 / TPI) * kLadderSlots * S * 4, st, Tab, tstride, m, count, consts, qp_mod, gR, sched,
                                        nsched, n0, O, ostride));
   } else {
     DDSHE_SWITCH(S, hipLaunchKernelGGL((k_modexp_ladder<S, TPI, W>), dim3(grid_for(count * TPI)), dim3(256),
-                                       (256 / TPI) * 2 * S * 4, st, Tab, tstride, m, count, consts, nullptr, gR, sched,
+                                       (256 / TPI) * kLadderSlots * S * 4, st, Tab, tstride, m, count, consts, nullptr, gR, sched,
                                        nsched, n0, O, ostride));
   }
   return hipGetLastError();

@@ -44,7 +44,8 @@ hipError_t launch_fold(int S, const uint32_t* X, size_t xstride, size_t count, c
                        const uint32_t* qp_mod, uint32_t n0,
                        uint32_t* P, size_t pstride, size_t ngroups, int s_out, hipStream_t st,
                        const uint32_t* ids = nullptr,  // ids: fold rows ids[0..count) (device, u32)
-                       int lane1 = 0);  // != 0: one bignum per lane (k_fold1) at lane1 = fold1_limbs(S, bits) limbs
+                       int lane1 = 0,  // != 0: one bignum per lane (k_fold1) at lane1 = fold1_limbs(S, bits) limbs
+                       size_t inblock_pgs = 0);  // != 0: k_fold InBlock, one row-major leaf of this many words per block
 bool fold_qp_enabled();
 // k_fold1 (one bignum per lane) exists for S (40, 76) and is worth its longer per-product latency for
 // folds of at least fold1_min_rows(S) rows (DDSHE_FOLD1=0 disables it, DDSHE_FOLD1_MIN=<rows> overrides)
