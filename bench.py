@@ -146,7 +146,7 @@ def main():
     ap.add_argument("--strong-rows", type=int, default=10_000_000,
                     help="rows of the strong-scaling and one-process multi-GPU lines (the north-star config)")
     args = ap.parse_args()
-    dflt = {"sum": (10_000_000, 20, 3, 2), "product_filter": (10_000_000, 10, 2, 3),
+    dflt = {"sum": (10_000_000, 20, 3, 2), "product_filter": (10_000_000, 10, 5, 3),
             "encrypt_sum": (1_000_000, 2, 1, 4), "order": (10_000_000, 10, 2, 3),
             "entry_search": (10_000_000, 10, 2, 5)}[args.workload]
     args.rows = dflt[0] if args.rows is None else args.rows
@@ -425,14 +425,9 @@ class SumWorkload(_Workload):
         if traffic is not None:
             traffic *= self.mine / 1e7
         roof.update(traffic=traffic, traffic_unit=f"HBM bytes per launch (PMC, profiles/{PMC_FILE})")
-        for vname in ("r04_pmc_valu_fold.json", "r03_pmc_valu_fold.json", "r01_pmc_valu_fold.json"):
-            vf = os.path.join(ROOT, "profiles", vname)
-            if os.path.exists(vf):  # rocprofv3 VALU counters of the same kernel (north star: VALU-roofline fraction)
-                dv = json.load(open(vf))["derived"]
-                roof["valu_pmc"] = {"mad_issue_frac_at_measured_clock": dv["mad_issue_frac_of_half_rate_peak_at_measured_clock"],
-                                    "int64_share_of_valu": dv.get("valu_int64_share_of_valu", dv.get("mad_share_of_valu")),
-                                    "clock_GHz": dv["clock_GHz_est"], "source": "profiles/" + vname}
-                break
+        vp = valu_pmc(("r06_pmc_valu_fold.json", "r04_pmc_valu_fold.json", "r03_pmc_valu_fold.json"))
+        if vp:  # rocprofv3 VALU counters of the same kernel (north star: VALU-roofline fraction)
+            roof["valu_pmc"] = vp
         cpu = None
         if self.world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(self.col, nsq, (nsq.bit_length() + 7) // 8, a.cpu_seconds)
@@ -787,7 +782,8 @@ def run_extra_configs(main_wl):
     headline line so the driver's BENCH record carries them."""
     import copy
     out = {}
-    for name, cls, rows, steps, warmup, seed in (("config3_product_filter", ProductFilterWorkload, 10_000_000, 10, 2, 3),
+    # config 3 warms up 5 steps: its first k_fold1 launches run while the clock ramps (profiles/r06_pf_fold1_dispatches.json)
+    for name, cls, rows, steps, warmup, seed in (("config3_product_filter", ProductFilterWorkload, 10_000_000, 10, 5, 3),
                                                  ("config4_encrypt_sum", EncryptSumWorkload, 1_000_000, 2, 1, 4)):
         a = copy.copy(main_wl.args)
         a.rows, a.steps, a.warmup, a.seed, a.strong = rows, steps, warmup, seed, False
@@ -864,6 +860,33 @@ def pmc_entry(workloads, kernel):
         if d is not None:
             return d["hbm_bytes_per_dispatch"], d["dispatches"]
     return None
+
+
+def valu_pmc(names):
+    """The first committed rocprofv3 SQ/GRBM pass summary (tools/pmc_valu_summary.py) among `names`: the
+    kernel's 64-bit VALU issue rate against the half-rate v_mad_u64_u32 peak at the clock measured in that
+    run, and its 64-bit instructions per expected lane mad (1.0 = nothing but the Montgomery mads)."""
+    for vname in names:
+        vf = os.path.join(ROOT, "profiles", vname)
+        if os.path.exists(vf):
+            dv = json.load(open(vf))["derived"]
+            out = {"mad_issue_frac_at_measured_clock": dv["mad_issue_frac_of_half_rate_peak_at_measured_clock"],
+                   "int64_share_of_valu": dv.get("valu_int64_share_of_valu", dv.get("mad_share_of_valu")),
+                   "clock_GHz": dv["clock_GHz_est"], "source": "profiles/" + vname}
+            for k in ("int64_instr_per_expected_mad", "issue_stall_share", "waitcnt_share"):
+                if k in dv:
+                    out[k] = dv[k]
+            return out
+    return None
+
+
+def engine_shape(bits: int):
+    """(S, W) of the engine's lane-group shape for a modulus of `bits` bits (kShapes, ddshe_shapes.hpp:
+    the first with S*W >= bits + 2)."""
+    for S, W in ((40, 28), (76, 28), (112, 28), (148, 28), (232, 27), (320, 27), (640, 27)):
+        if S * W >= bits + 2:
+            return S, W
+    raise ValueError(bits)
 
 
 def load_keyset(name):
@@ -945,12 +968,10 @@ class ProductFilterWorkload(_Workload):
             kname = "k_fold<76, 2, 28, true>"
         roof["traffic"] = pmc_traffic("product_filter", (kname,))
         roof["traffic_unit"] = f"HBM bytes per launch (PMC, profiles/{PMC_FILE})"
-        vf = os.path.join(ROOT, "profiles", "r02_pmc_valu_fold1.json")
-        if kname.startswith("k_fold1<74") and os.path.exists(vf):  # VALU counters of the same kernel
-            dv = json.load(open(vf))["derived"]
-            roof["valu_pmc"] = {"mad_issue_frac_at_measured_clock": dv["mad_issue_frac_of_half_rate_peak_at_measured_clock"],
-                                "mad_share_of_valu": dv["mad_share_of_valu"], "clock_GHz": dv["clock_GHz_est"],
-                                "source": "profiles/r02_pmc_valu_fold1.json"}
+        if kname.startswith("k_fold1<74"):  # VALU counters of the same kernel
+            vp = valu_pmc(("r06_pmc_valu_fold1.json", "r02_pmc_valu_fold1.json"))
+            if vp:
+                roof["valu_pmc"] = vp
         _, _, filt_dev_ms, _ = self.eng.timing()  # HIP events around the filter launches (device time)
         filt_s = filt_dev_ms / 1e3 / (4 * a.steps)
         matches = sum(counts.values()) / 4
@@ -1123,11 +1144,19 @@ class EncryptSumWorkload(_Workload):
             per_enc = [(sq + mul + tab + m_ops + 3, s32)] * 2
         mac_issued = sum(cnt * (2 * s * s + s) for cnt, s in per_enc)
         achieved = mac_issued * self.mine / enc_s / 1e12
+        # the same products in the engine's own limbs (28- or 27-bit: what the VALU actually issues)
+        mod_bits = k["nsquare"].bit_length() if a.public else 2 * k["p"].bit_length()
+        S_eng, W_eng = engine_shape(mod_bits)
+        lane_mads = sum(cnt for cnt, _ in per_enc) * (2 * S_eng * S_eng + S_eng)
         s_full = (k["nsquare"].bit_length() + 31) // 32
         binary_mac = binary_ladder_modmuls(n) * (2 * s_full * s_full + s_full)
         roof = {"bound": "valu-int", "kernel": "k_modexp_ladder (encrypt phase: pre + ladder + CRT kernels)",
                 "achieved": achieved, "peak": PEAK_TMAC, "unit": "TMAC/s", "frac": achieved / PEAK_TMAC,
-                "mac_per_encrypt_issued": mac_issued, "mac_per_encrypt_binary_ladder_n2": binary_mac,
+                "mac_per_encrypt_issued": mac_issued,
+                "mac_unit": "32x32-bit MACs of the products the ladder issues, 2s^2+s with s = 32-bit limbs of the modulus",
+                "lane_mads_per_encrypt": lane_mads, "engine_shape": [S_eng, W_eng],
+                "lane_mad_frac": lane_mads * self.mine / enc_s / 1e12 / PEAK_TMAC,
+                "mac_per_encrypt_binary_ladder_n2": binary_mac,
                 "effective_vs_binary_ladder_n2": binary_mac * self.mine / enc_s / 1e12,
                 "avg_encrypt_ms": enc_s * 1e3, "traffic": None}
         if not a.public:  # the ladder's HBM bytes (PMC), per dispatch: one dispatch per CRT half and 1M-row chunk
@@ -1137,13 +1166,9 @@ class EncryptSumWorkload(_Workload):
                 roof["traffic_unit"] = (f"HBM bytes per k_modexp_ladder<112,4,28> dispatch (PMC, profiles/{PMC_FILE});"
                                         " the per-row window tables are streamed from HBM")
                 roof["traffic_rows_per_dispatch"] = self.mine
-            sf = os.path.join(ROOT, "profiles", "r05_pmc_enc_ladder.json")
-            if os.path.exists(sf):  # the same kernel's wait counters: what the ladder waits on
-                dv = json.load(open(sf))["dispatches"][0]["derived"]
-                roof["stall_pmc"] = {k: dv[k] for k in ("hbm_GBps", "waitcnt_share_of_wave_cycles",
-                                                        "issue_stall_share_of_wave_cycles",
-                                                        "valu_active_share_of_wave_cycles")}
-                roof["stall_pmc"]["source"] = "profiles/r05_pmc_enc_ladder.json"
+            vp = valu_pmc(("r06_pmc_valu_ladder.json",))
+            if vp:  # the ladder's own SQ/GRBM pass: 64-bit VALU issue rate, waits
+                roof["valu_pmc"] = vp
         cpu = None
         if self.world == 1 and not a.no_cpu_baseline:
             cpu = cpu_encrypt_baseline(k, self.rcol, self.ms, a.cpu_seconds, self.out)

@@ -12,6 +12,7 @@ P=gpurun_out/prof6
 B="python3 bench.py --no-cpu-baseline --no-e2e"
 V="SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 GRBM_GUI_ACTIVE"
 KS=(
+  "300 order_keys2_0 env DDSHE_ORDER_KEYS2=0 python -u -m pytest tests/test_gpu_order.py -x -q --timeout 200 --timeout-method thread"
   "120 ubench tools/microbench/ubench"
   "300 ks_sum rocprofv3 --kernel-trace --stats --output-format csv -d $P/sum -o run -- $B --no-extras --steps 10"
   "300 ks_pf rocprofv3 --kernel-trace --stats --output-format csv -d $P/pf -o run -- $B --workload product_filter --steps 10"

@@ -34,6 +34,7 @@ def main(path, kern, products, s, out):
         "valu_int64_share_of_valu": i64 / c["SQ_INSTS_VALU"],
         "mad_lane_ops_per_clk_per_CU": mad_ops,
         "mad_issue_frac_of_half_rate_peak_at_measured_clock": mad_ops / 64,
+        "int64_instr_per_expected_mad": i64 / (products * (2 * s * s + s) / 64),
         "valu_wave_instr_per_clk_per_SIMD": c["SQ_INSTS_VALU"] / (cycles * N_SIMD),
         "issue_stall_share": c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"],
         "waitcnt_share": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
