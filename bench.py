@@ -837,9 +837,15 @@ def pmc_traffic(workload, kernels, per_step=False, largest=False):
 
 
 def order_pmc_traffic():
-    """HBM bytes of one OrderLS call on raw arrays from the PMC pass of the order bench: that pass runs
-    one raw call (k_rs_prep + k_rs_red once) and the resident line's calls (no prep), so the other
-    kernels' bytes are divided by the calls (one k_msd_bounds dispatch per call)."""
+    """HBM bytes of one OrderLS call on raw arrays: the last raw call (the carried plan: no min / max pass)
+    of the per-call PMC split (tools/order_call_traffic.py -> profiles/r06_order_call_traffic.json; the
+    order bench's FETCH_SIZE / WRITE_SIZE passes with one warmup and two steps); older rounds: one raw call
+    with k_rs_prep + k_rs_red and the resident line's calls averaged."""
+    cf = os.path.join(ROOT, "profiles", "r06_order_call_traffic.json")
+    if os.path.exists(cf):
+        raw = [c for c in json.load(open(cf))["calls"] if "__amd_rocclr_copyBuffer" not in c["kernels"]]
+        if raw:
+            return raw[-1]["hbm_bytes"]
     once = pmc_traffic("order", ("k_rs_prep", "k_rs_red"), per_step=True)
     rest = pmc_traffic("order", ("k_rs_hist<256>", "k_rs_scan_tiles", "k_rs_scan_chunks", "k_rs_scatter<256>", "k_msd_local", "k_msd_big"),
                        per_step=True)
@@ -1230,16 +1236,17 @@ class OrderWorkload(_Workload):
                 print("VERIFY FAILED", file=sys.stderr)
         step_s = elapsed / a.steps
         alg = 13 * self.mine  # read key + valid byte, write one row id
-        roof = {"bound": "hbm", "kernel": "k_rs_prep + 2 LSD passes over the top 16 bits of the key span (k_rs_hist/k_rs_scan_tiles/k_rs_scan_chunks/"
+        roof = {"bound": "hbm", "kernel": "2 LSD passes over the top 16 bits of the key span (k_rs_hist/k_rs_scan_tiles/k_rs_scan_chunks/"
                 "k_rs_scatter; the last scatter also fills the bucket table) + k_msd_local/k_msd_big (in-bucket order "
-                "of the buckets holding two distinct keys)",
+                "of the buckets holding two distinct keys); the previous call's plan carried (its first histogram also takes "
+                "the bounds, k_rs_red checks the plan: no k_rs_prep pass)",
                 "achieved": alg / step_s / 1e9, "peak": 8000.0, "unit": "GB/s", "frac": alg / step_s / 1e9 / 8000.0,
                 "algorithmic_bytes": alg,
-                # prep 9 + pass 1 (hist 9 + scatter 9 + 12) + pass 2 (hist 8 + scatter 12 + 4) (+ the multi-key
-                # buckets' key gathers and rounds)
-                "issued_bytes_est": self.mine * (9 + 30 + 24),
+                # pass 1 (hist 9 + scatter 9 + 12) + pass 2 (hist 4 + scatter 12 + 12) (+ the multi-key
+                # buckets' copies and rounds)
+                "issued_bytes_est": self.mine * (30 + 28),
                 "traffic": order_pmc_traffic(),
-                "traffic_unit": "HBM bytes per OrderLS call (PMC, profiles/" + PMC_FILE + ")"}
+                "traffic_unit": "HBM bytes per raw OrderLS call (PMC, profiles/r06_order_call_traffic.json)"}
         roof["issued_GBps"] = roof["issued_bytes_est"] / step_s / 1e9  # what the MSD-split design moves
         roof["issued_frac"] = roof["issued_GBps"] / 8000.0
         cpu = None

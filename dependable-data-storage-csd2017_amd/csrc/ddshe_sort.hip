@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
 
 #include "ddshe_launch.hpp"
 
@@ -150,9 +151,12 @@ __global__ void __launch_bounds__(256) k_rs_prep(const int64_t* __restrict__ col
 // red[2] = kmin, red[3] = s1 (the first pass's shift, span bits - 16) when the span has spec_lo..spec_hi
 // bits, else kRsNoPlan (every later kernel of the call then returns at once).
 constexpr uint64_t kRsNoPlan = ~0ull;
+// carry (ckmin, cs1 >= 0): a carried plan (launch_ope_order's prep-free path) is checked instead of one
+// being made: it stands (red[2..3] = ckmin, cs1) iff every holder's key lies in [ckmin, ckmin + 2^(cs1+16))
+// and the top bit of that range is used (the MSD split's top digit is not wasted); else kRsNoPlan.
 __global__ void __launch_bounds__(1024) k_rs_red(const uint64_t* __restrict__ part, size_t nparts,
                                                  uint64_t* __restrict__ red, int spec_lo, int spec_hi,
-                                                 uint64_t* __restrict__ hout) {
+                                                 uint64_t* __restrict__ hout, uint64_t ckmin = 0, int cs1 = -1) {
   uint64_t lo = ~0ull, hi = 0;
   for (size_t i = threadIdx.x; i < nparts; i += 1024) {
     lo = min(lo, part[2 * i]);
@@ -165,7 +169,12 @@ __global__ void __launch_bounds__(1024) k_rs_red(const uint64_t* __restrict__ pa
       hout[0] = mn;
       hout[1] = mx;
     }
-    if (spec_lo <= spec_hi) {
+    if (cs1 >= 0) {
+      const uint64_t span = mn <= mx && mn >= ckmin ? mx - ckmin : ~0ull;
+      const int sb = span ? 64 - __builtin_clzll(span) : 0;
+      red[2] = ckmin;
+      red[3] = (mn <= mx && mn >= ckmin && sb == cs1 + kMsdBits) ? (uint64_t)cs1 : kRsNoPlan;
+    } else if (spec_lo <= spec_hi) {
       const uint64_t span = mn <= mx ? mx - mn : 0ull;
       const int sb = span ? 64 - __builtin_clzll(span) : 0;
       red[2] = mn <= mx ? mn : 0ull;
@@ -239,7 +248,8 @@ __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ key
                                                      uint32_t* __restrict__ hist, size_t nblocks,
                                                      uint32_t* __restrict__ clr, uint32_t nclr, bool pairs,
                                                      const uint32_t* __restrict__ khi,
-                                                     const uint64_t* __restrict__ plan, bool rowatom) {
+                                                     const uint64_t* __restrict__ plan, bool rowatom,
+                                                     uint64_t* __restrict__ mm = nullptr) {
   if (plan) {  // speculative call: kmin and the shift (relative to s1) from k_rs_red's plan
     const uint64_t s1 = plan[1];
     if (s1 == kRsNoPlan) return;
@@ -267,6 +277,7 @@ __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ key
   uint64_t key[kIt];
   uint32_t id[kIt];
   size_t rix[kIt];
+  uint64_t mlo = ~0ull, mhi = 0;  // mm: the block's holder-key bounds
   if (khi) {
     // split keys (the MSD path's last pass, digit and validity bits >= 32): only the high words, four rows
     // per 16-byte load; an unaligned tail row by row
@@ -306,6 +317,18 @@ __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ key
       key[2 * k] = ids ? kv.x : (hv & 0xFFu) ? rs_ukey(kv.x, desc) - kmin : (kbit ? kRsNoHold : 0ull);
       key[2 * k + 1] = ids ? kv.y : (hv >> 8) ? rs_ukey(kv.y, desc) - kmin : (kbit ? kRsNoHold : 0ull);
       id[2 * k] = id[2 * k + 1] = 0u;
+      if (mm) {  // the raw keys' bounds (before kmin): holders among the in-range rows only
+        if (rix[2 * k] < n && (hv & 0xFFu)) {
+          const uint64_t u = rs_ukey(kv.x, desc);
+          mlo = min(mlo, u);
+          mhi = max(mhi, u);
+        }
+        if (rix[2 * k + 1] < n && (hv >> 8)) {
+          const uint64_t u = rs_ukey(kv.y, desc);
+          mlo = min(mlo, u);
+          mhi = max(mhi, u);
+        }
+      }
     }
   } else {
 #pragma unroll
@@ -315,8 +338,14 @@ __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ key
       key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc, kmin, kbit);  // first pass: keys = the column
       id[k] = need_id ? rs_load_id(ids, i, valid, vbit) : 0u;
       rix[k] = r;
+      if (mm && r < n && (!valid || valid[i])) {
+        const uint64_t u = rs_ukey(keys[i], desc);
+        mlo = min(mlo, u);
+        mhi = max(mhi, u);
+      }
     }
   }
+  if (mm) rs_minmax_block(mlo, mhi, mm + 2 * blockIdx.x);
   if (rowatom) {
     uint32_t* mine = &wcnt[threadIdx.x >> 6][0];
 #pragma unroll
@@ -849,7 +878,8 @@ size_t rs_scratch_bytes(size_t n) {
   // MSD bucket starts + control words + big-bucket list
   return 2 * n * 8 + 32 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 1024 +
          (size_t)kRsDigits * ((rs_blocks(n) + kScanTiles - 1) / kScanTiles) * 4 + 256 +
-         16 * ((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows)) + 800 + (8 * (size_t)kMsdBuckets + 8) * 4;
+         16 * std::max((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows), rs_blocks(n)) + 800 +
+         (8 * (size_t)kMsdBuckets + 8) * 4;
 }
 
 // the MSD path pays off from 4 LSD passes on (a span of > 24 bits) and enough rows to fill the buckets
@@ -876,11 +906,23 @@ static int order_xcd() {
 // one LSD pass: per-tile digit counts, their scan over tiles, the stable scatter (tiles of BLK x kRsItems
 // rows; 256 threads measured fastest: 512 / 1024-thread tiles lengthen the write-out's digit runs but
 // cut the blocks per CU, +0 / +10 us on the first pass of 10M rows)
+// First pass of a carried plan (launch_ope_order's prep-free path): the histogram runs with the carried
+// kmin and shift (absolute) and leaves the blocks' holder-key bounds in mm; k_rs_red then checks the plan
+// against them before the scatter (which, like every later kernel, reads the plan from red + 2).
+struct CarryPass {
+  uint64_t* mm = nullptr;  // nullptr: no carried plan
+  uint64_t* red = nullptr;
+  uint64_t* hout = nullptr;
+  uint64_t kmin = 0;
+  int s1 = -1;
+};
+
 template <int BLK>
 static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in, const uint8_t* valid, size_t n,
                     int shift, bool last, int desc, bool vbit, bool kbit, uint64_t kmin, uint32_t* hist,
                     uint32_t* ctot, uint32_t* dtot, uint64_t* kout, uint32_t* ids_out, uint32_t* clr,
-                    const MsdRuns& runs, const uint32_t* khi, uint32_t* khi_out, const uint64_t* plan) {
+                    const MsdRuns& runs, const uint32_t* khi, uint32_t* khi_out, const uint64_t* plan,
+                    const CarryPass& cp = CarryPass{}) {
   const size_t nb = (n + RsTile<BLK>::kRows - 1) / RsTile<BLK>::kRows;
   // 16-byte key pairs for the counts: aligned keys (and valid bytes when the first pass reads them), no
   // id read (DDSHE_ORDER_HPAIR=0: one row per lane, A/B)
@@ -891,9 +933,16 @@ static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in,
   // digit of a wave, found by 9 ballots, A/B): same box, 10M rows, raw call 0.318 -> 0.287 ms on the bench's
   // OPE column, 0.675 -> 0.652 on uniform 54-bit keys, 0.265 -> 0.275 with every wave's digits equal
   static const int hatom = order_env("DDSHE_ORDER_HATOM", 1);
-  hipLaunchKernelGGL((k_rs_hist<BLK, BLK>), dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, last,
-                     desc, vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs && !khi, khi, plan,
-                     hatom != 0);
+  if (cp.mm) {
+    hipLaunchKernelGGL((k_rs_hist<BLK, BLK>), dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n,
+                       shift + cp.s1, last, desc, vbit, kbit, cp.kmin, hist, nb, clr, clr ? kMsdTableWords : 0u,
+                       pairs && !khi, khi, nullptr, hatom != 0, cp.mm);
+    hipLaunchKernelGGL(k_rs_red, dim3(1), dim3(1024), 0, st, cp.mm, nb, cp.red, 1, 0, cp.hout, cp.kmin, cp.s1);
+  } else {
+    hipLaunchKernelGGL((k_rs_hist<BLK, BLK>), dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, last,
+                       desc, vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs && !khi, khi, plan,
+                       hatom != 0);
+  }
   const size_t nch = (nb + kScanTiles - 1) / kScanTiles;
   hipLaunchKernelGGL(k_rs_scan_tiles, dim3((unsigned)nch), dim3(kScanThreads), 0, st, hist, nb, ctot);
   hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nch, dtot);
@@ -908,6 +957,27 @@ static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in,
 // call continues on the host-planned path from the bounds the same pass stored to host memory).
 constexpr int kSpecLo = 40, kSpecHi = 56;
 static std::atomic<int> g_order_spec{0};
+// The plan of the last raw call that ran the MSD path (kmin, s1, direction), carried to the next raw call:
+// that call skips the min / max pass (k_rs_prep + k_rs_red before the passes) — its first histogram uses
+// the carried plan and collects the bounds, k_rs_red checks the plan against them before the first
+// scatter, and a plan that no longer fits (keys below kmin or a span of another bit length) makes every
+// later kernel return; the call then goes on host-planned from the bounds the check stored. Shared by
+// every caller (a race only costs a failed check). DDSHE_ORDER_CARRY=0: the prep pass every call (A/B).
+struct CarriedPlan {
+  uint64_t kmin;
+  int s1;   // -1: none
+  int desc;
+};
+static std::mutex g_carry_mu;
+static CarriedPlan g_carry{0, -1, 0};
+static CarriedPlan carry_get() {
+  std::lock_guard<std::mutex> lk(g_carry_mu);
+  return g_carry;
+}
+static void carry_set(CarriedPlan p) {
+  std::lock_guard<std::mutex> lk(g_carry_mu);
+  g_carry = p;
+}
 
 hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, int desc, void* scratch,
                             uint32_t* out_ids, hipStream_t st, const uint64_t* ubounds, const MappedWords* hw) {
@@ -926,8 +996,9 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   uint64_t* red = (uint64_t*)(((uintptr_t)(ctot + (size_t)kRsDigits * nch) + 15) & ~(uintptr_t)15);
   uint64_t* part = red + 4;  // red[0..1] min / max, red[2..3] the speculative plan
   const size_t pb = (n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows);
-  // MSD bucket table (MsdRuns layout), then the control words and the big-bucket list
-  uint32_t* mtab = (uint32_t*)(((uintptr_t)(part + 2 * pb) + 255) & ~(uintptr_t)255);
+  // MSD bucket table (MsdRuns layout), then the control words and the big-bucket list (part: the prep
+  // blocks' bounds, or the first histogram's under a carried plan)
+  uint32_t* mtab = (uint32_t*)(((uintptr_t)(part + 2 * std::max(pb, nb)) + 255) & ~(uintptr_t)255);
   MsdRuns runs{mtab, (unsigned long long*)(mtab + kMsdBuckets), mtab + 3 * kMsdBuckets,
                (unsigned long long*)(mtab + 4 * kMsdBuckets), mtab + 6 * kMsdBuckets, 0};
   uint32_t* mctl = mtab + 7 * kMsdBuckets;
@@ -945,7 +1016,8 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   // set the first pass clears the bucket table and the last fills it. plan: shifts relative to s1, kmin
   // and s1 from the device
   auto run_passes = [&](const int* shifts, int np, uint32_t* fin, uint32_t* tmp, const MsdRuns& msd, bool split,
-                        bool kbit, bool vbit, uint64_t kmin, const uint64_t* plan) {
+                        bool kbit, bool vbit, uint64_t kmin, const uint64_t* plan,
+                        const CarryPass& cp = CarryPass{}) {
     const uint32_t* ids_in = nullptr;  // identity before the first pass
     const uint64_t* kin = (const uint64_t*)col;  // raw column before the first pass
     uint64_t* kout = ka;
@@ -956,7 +1028,8 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
       const bool last = j == np - 1;
       rs_pass<256>(st, kin, ids_in, valid, n, shifts[j], last, desc, vbit, kbit, kmin, hist, ctot, dtot,
                    last ? (msd.first && keys2 ? kout : nullptr) : kout, ids_out, j == 0 ? msd.first : nullptr,
-                   last ? msd : none, j == 1 ? hi : nullptr, j == 0 ? hi : nullptr, plan);
+                   last ? msd : none, j == 1 ? hi : nullptr, j == 0 ? hi : nullptr, plan,
+                   j == 0 ? cp : CarryPass{});
       kin = kout;
       kout = kout == ka ? kb : ka;
       ids_in = ids_out;
@@ -989,6 +1062,27 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     hred[0] = ubounds[0] <= ubounds[1] ? (desc ? ~ubounds[1] : ubounds[0]) : 1;
     hred[1] = ubounds[0] <= ubounds[1] ? (desc ? ~ubounds[0] : ubounds[1]) : 0;
   } else {
+    static const int carry_env = order_env("DDSHE_ORDER_CARRY", 1);
+    const CarriedPlan cpl = carry_get();
+    if (hw && carry_env && spec_env && split_env && msd_enabled(n, kSpecLo) && cpl.s1 >= 0 && cpl.desc == desc) {
+      const uint64_t* plan = red + 2;
+      CarryPass cp;
+      cp.mm = part;
+      cp.red = red;
+      cp.hout = hw->d;
+      cp.kmin = cpl.kmin;
+      cp.s1 = cpl.s1;
+      const int rel[2] = {0, 8};
+      run_passes(rel, 2, out_ids, ib, runs, true, valid != nullptr, false, 0, plan, cp);
+      msd_tail(0, plan);
+      uint64_t ovf = 0, pl = 0;
+      if ((e = read_ctl(plan, &ovf, &pl)) != hipSuccess) return e;
+      if (pl != kRsNoPlan && !ovf) return hipGetLastError();  // the carried plan stands for the next call too
+      carry_set(CarriedPlan{0, -1, 0});
+      if (pl != kRsNoPlan) skip_msd = true;  // a crowded bucket overflowed: straight to the LSD passes
+      hred[0] = hw->h[0];
+      hred[1] = hw->h[1];
+    } else {
     const bool spec = hw && spec_env && split_env && msd_enabled(n, kSpecLo) && g_order_spec.load(std::memory_order_relaxed);
     if (((uintptr_t)col & 15) == 0 && ((uintptr_t)valid & 1) == 0)
       hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
@@ -1016,6 +1110,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
       if ((e = hipMemcpyAsync(hred, red, sizeof(hred), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
       if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
     }
+    }
   }
   // the bytes of max - min (at least one pass when rows may lack the position: its last pass buckets them)
   const uint64_t kmin = hred[0] <= hred[1] ? hred[0] : 0ull;
@@ -1023,7 +1118,14 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   const int sb = span ? 64 - __builtin_clzll(span) : 0;  // bits of the span
   const bool kbit = valid && sb <= 56;                    // validity in key bit 63 (every shift <= 48)
   const bool vbit = valid && !kbit && n <= (size_t)kRsLack;
-  if (!ubounds && hw) g_order_spec.store(sb >= kSpecLo && sb <= kSpecHi, std::memory_order_relaxed);
+  if (!ubounds && hw) {
+    g_order_spec.store(sb >= kSpecLo && sb <= kSpecHi, std::memory_order_relaxed);
+    // the next raw call may carry this plan (the MSD path below runs it with split keys and, with a
+    // valid array, the key-bit validity: what the carried path runs)
+    const bool carriable = sb >= kSpecLo && sb <= kSpecHi && !skip_msd && msd_enabled(n, sb) && split_env &&
+                           (!valid || sb <= 56);
+    carry_set(carriable ? CarriedPlan{kmin, sb - kMsdBits, desc} : CarriedPlan{0, -1, 0});
+  }
   if (!skip_msd && msd_enabled(n, sb)) {
     runs.s1 = sb - kMsdBits;
     const int shifts[2] = {runs.s1, sb - 8};

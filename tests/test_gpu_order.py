@@ -203,6 +203,34 @@ def test_order_speculative_plan_sequence(eng):
                               expected(col, np.ones(n, np.uint8), not desc)), k
 
 
+def test_order_carried_plan_sequence(eng):
+    """A raw call after one that ran the MSD path carries that call's plan (kmin, shift) and skips the
+    min / max pass: its first histogram collects the bounds and k_rs_red checks the plan before the first
+    scatter. Same direction throughout, so every call after the first tries the carried plan: keys below
+    the carried kmin, a range shifted past its top, a span of fewer bits, a crowded bucket (LSD fallback),
+    another row count, rows without a valid array and a direction flip must all sort as numpy does."""
+    rng = np.random.default_rng(57)
+    ope_map = np.cumsum(rng.integers(1, 1 << 40, size=10001, dtype=np.int64)) - (1 << 52)
+
+    def ope(n, lo=1, hi=10001, shift=0):
+        return ope_map[rng.integers(lo, hi, size=n)] + shift
+
+    def crowded(n):
+        c = ope(n)
+        rows = rng.choice(n, size=20_000, replace=False)     # > 8192 rows, > 16 keys in one 16-bit bucket
+        c[rows] = ope_map[5000] + rng.integers(0, 1 << 30, size=20_000)
+        return c
+
+    n = 300_001
+    seq = [(ope(n), True), (ope(n), True), (ope(n, shift=-(1 << 44)), True), (ope(n, shift=-(1 << 44)), True),
+           (ope(n, shift=1 << 50), True), (ope(n, 1, 2000), True), (ope(n, 1, 2000), True), (crowded(n), True),
+           (ope(n), True), (ope(150_007), True), (ope(n), False), (ope(n), False), (ope(n), True)]
+    for k, (col, desc) in enumerate(seq):
+        valid = (rng.random(len(col)) > 0.05).astype(np.uint8) if k % 3 else None
+        v = valid if valid is not None else np.ones(len(col), np.uint8)
+        assert np.array_equal(eng.ope_order(col, valid, desc), expected(col, v, desc)), k
+
+
 @pytest.mark.parametrize("offset", [0, 1])
 def test_order_device_pointers(eng, offset):
     """dds_ope_order_device on caller-owned device buffers: the min/max prep reads 16-byte key pairs
