@@ -770,11 +770,61 @@ __device__ __forceinline__ void msd_wave_sort(const uint64_t* __restrict__ keys,
   }
 }
 
+// One wave's work on multi-key bucket b (rows [lo, lo + m)): copy its ids (and, gather mode, its keys)
+// to the side buffers, then the stable partition, or the in-register network, or the big-bucket list.
+__device__ __forceinline__ void msd_bucket(const int64_t* __restrict__ col, int desc, uint64_t kmin,
+                                           uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
+                                           uint32_t* __restrict__ ids, uint32_t b, uint32_t lo, uint32_t m, int s1,
+                                           uint32_t* __restrict__ ctl, uint32_t* __restrict__ big, int lane) {
+  // this bucket's grouped ids to the side buffer (free after the last pass), and (gather mode) their keys
+  // gathered from the column by id, read from there below
+  for (uint32_t p0 = 0; p0 < m; p0 += 512) {  // 8 loads in flight per lane, then their stores
+    uint32_t v[8];
+    int64_t c[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const uint32_t p = p0 + (uint32_t)(r * 64 + lane);
+      v[r] = ids[lo + min(p, m - 1)];
+    }
+    if (col) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) c[r] = col[v[r]];
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const uint32_t p = p0 + (uint32_t)(r * 64 + lane);
+      if (p < m) {
+        src[lo + p] = v[r];
+        if (col) keys[lo + p] = rs_ukey((uint64_t)c[r], desc) - kmin;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's copies land before its lanes read them
+  if (msd_wave_partition(keys, src, ids, lo, m, lane, m <= kMsdWaveMax ? 2 : 16)) return;
+  if (m > kMsdWaveMax) {
+    if (lane == 0) big[atomicAdd(&ctl[kMsdCtlBig], 1u)] = b;
+    return;
+  }
+  const uint64_t rmask = (1ull << s1) - 1ull;
+  if (m <= 64) msd_wave_sort<1, 6>(keys, src, ids, lo, m, rmask, lane);
+  else if (m <= 128) msd_wave_sort<2, 7>(keys, src, ids, lo, m, rmask, lane);
+  else if (m <= 256) msd_wave_sort<4, 8>(keys, src, ids, lo, m, rmask, lane);
+  else msd_wave_sort<8, 9>(keys, src, ids, lo, m, rmask, lane);
+}
+
+// One wave per `per_wave` consecutive buckets: the wave's first lanes read their buckets' table entries
+// together, a ballot marks the buckets holding two distinct keys, and the wave orders those one after
+// another (bucket bounds made wave-uniform, so its addressing stays scalar). Round 5 ran one wave per
+// bucket: 65,536 waves, most reading one word and exiting. Same box, k_msd_local per 10M-row call on the
+// bench's OPE column (profiles/r06_msdwave_ab.txt): 1 bucket per wave 42.8 us, 2: 39.9, 4: 45.0, 8: ~51
+// (neighbouring multi-key buckets serialise); uniform 54-bit keys (every bucket multi-key): call 0.709 ->
+// 0.683 ms at 2.
+// (per_wave: DDSHE_ORDER_MSDWAVE, 2 by default; 1 is round 5's one wave per bucket, A/B; a power of 2 <= 64)
 __global__ void __launch_bounds__(256) k_msd_local(const int64_t* __restrict__ col, int desc, uint64_t kmin,
                                                    uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
                                                    uint32_t* __restrict__ ids, MsdRuns runs,
                                                    uint32_t* __restrict__ ctl, uint32_t* __restrict__ big,
-                                                   const uint64_t* __restrict__ plan) {
+                                                   const uint64_t* __restrict__ plan, uint32_t per_wave) {
   if (plan) {
     const uint64_t s1 = plan[1];
     if (s1 == kRsNoPlan) return;
@@ -782,47 +832,20 @@ __global__ void __launch_bounds__(256) k_msd_local(const int64_t* __restrict__ c
     runs.s1 = (int)s1;
   }
   const int lane = threadIdx.x & 63;
-  {  // one wave per bucket (a grid-stride loop over the buckets measured 34 -> 56 us: the multi-key
-     // buckets' rounds serialise within a wave)
-    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const uint32_t lo = runs.first[b];
-    if (lo == ~0u) return;  // empty
-    if (!runs.multi[b] && runs.kmin[b] == runs.kmax[b]) return;  // one key: the last pass put its rows in place
-    const uint32_t m = runs.end[b] - lo;
-    // this bucket's grouped ids to the side buffer (free after the last pass), and their keys gathered
-    // from the column by id (the last pass does not write the keys out), read from there below
-    for (uint32_t p0 = 0; p0 < m; p0 += 512) {  // 8 loads in flight per lane, then their stores
-      uint32_t v[8];
-      int64_t c[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const uint32_t p = p0 + (uint32_t)(r * 64 + lane);
-        v[r] = ids[lo + min(p, m - 1)];
-      }
-      if (col) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) c[r] = col[v[r]];
-      }
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const uint32_t p = p0 + (uint32_t)(r * 64 + lane);
-        if (p < m) {
-          src[lo + p] = v[r];
-          if (col) keys[lo + p] = rs_ukey((uint64_t)c[r], desc) - kmin;
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's copies land before its lanes read them
-    if (msd_wave_partition(keys, src, ids, lo, m, lane, m <= kMsdWaveMax ? 2 : 16)) return;
-    if (m > kMsdWaveMax) {
-      if (lane == 0) big[atomicAdd(&ctl[kMsdCtlBig], 1u)] = b;
-      return;
-    }
-    const uint64_t rmask = (1ull << runs.s1) - 1ull;
-    if (m <= 64) msd_wave_sort<1, 6>(keys, src, ids, lo, m, rmask, lane);
-    else if (m <= 128) msd_wave_sort<2, 7>(keys, src, ids, lo, m, rmask, lane);
-    else if (m <= 256) msd_wave_sort<4, 8>(keys, src, ids, lo, m, rmask, lane);
-    else msd_wave_sort<8, 9>(keys, src, ids, lo, m, rmask, lane);
+  const uint32_t b0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * per_wave;
+  const uint32_t bl = b0 + ((uint32_t)lane & (per_wave - 1));
+  const uint32_t lo_l = runs.first[bl];
+  const bool need = lane < (int)per_wave && lo_l != ~0u &&
+                    (runs.multi[bl] != 0u || runs.kmin[bl] != runs.kmax[bl]);
+  const uint32_t m_l = need ? runs.end[bl] - lo_l : 0u;
+  uint64_t mask = __ballot(need);
+  while (mask) {
+    const int j = __builtin_ctzll(mask);
+    mask &= mask - 1ull;
+    // wave-uniform (SGPRs): the bucket's addressing stays scalar in msd_bucket
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)lo_l, j));
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)m_l, j));
+    msd_bucket(col, desc, kmin, keys, src, ids, b0 + (uint32_t)j, lo, m, runs.s1, ctl, big, lane);
   }
 }
 
@@ -1036,8 +1059,12 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     }
   };
   auto msd_tail = [&](uint64_t kmin, const uint64_t* plan) {
-    hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / 4), dim3(256), 0, st, keys2 ? nullptr : col, desc, kmin, kb, ib,
-                       out_ids, runs, mctl, mbig, plan);
+    static const uint32_t per_wave = [] {
+      const int v = order_env("DDSHE_ORDER_MSDWAVE", 2);
+      return (v >= 1 && v <= 64 && (v & (v - 1)) == 0) ? (uint32_t)v : 2u;
+    }();
+    hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / (4 * per_wave)), dim3(256), 0, st, keys2 ? nullptr : col, desc,
+                       kmin, kb, ib, out_ids, runs, mctl, mbig, plan, per_wave);
     hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, kb, ib, out_ids, runs, mctl, mbig, plan);
   };
   // words 2..3 of hw after the call's device work: overflow flag, plan
