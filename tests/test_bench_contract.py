@@ -10,7 +10,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FILES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r01_bench_*.json"))) + [
     os.path.join(ROOT, "profiles", "r02_bench_default_final.json")] + [
-    os.path.join(ROOT, "profiles", f"r05_{w}.json") for w in ("default", "pf", "order", "es")]
+    os.path.join(ROOT, "profiles", f"r0{r}_{w}.json") for r in (5, 6) for w in ("default", "pf", "order", "es")]
 
 TOP = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
        "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
@@ -82,3 +82,17 @@ def test_round5_default_line_boundary_and_latency():
     assert big["host_cpu_ms"] < 0.1 * big["wall_ms"]  # the long fold's caller sleeps, it does not spin
     n = d["latency"]["pair_sum_route_native_threads_2048bit"]
     assert n["errors"] == 0 and n["matches"] is True
+
+
+def test_round6_default_line_and_rehearsal():
+    """The round-6 default line: configs 3 and 4 verified with their VALU PMC sources, the strong split's
+    combine equal to the fold; the two-rank gloo rehearsal through the launcher reports n_gpus 2, verified."""
+    d = json.loads(open(os.path.join(ROOT, "profiles", "r06_default.json")).read())
+    assert d["roofline"]["valu_pmc"]["source"] == "profiles/r06_pmc_valu_fold.json"
+    for name in ("config3_product_filter", "config4_encrypt_sum"):
+        c = d["configs"][name]
+        assert c.get("verified") is True and c["roofline"]["valu_pmc"]["source"].startswith("profiles/r06_"), name
+    assert 0 < d["configs"]["config4_encrypt_sum"]["roofline"]["lane_mad_frac"] <= 1
+    assert d["strong_split_1gpu"]["combined_equals_full_fold"] is True
+    g = json.loads(open(os.path.join(ROOT, "profiles", "r06_gloo2_rehearsal.json")).read())
+    assert g["n_gpus"] == 2 and g["verified"] is True and g["config"]["parallelism"] == "rows-sharded x2"
