@@ -151,12 +151,9 @@ __global__ void __launch_bounds__(256) k_rs_prep(const int64_t* __restrict__ col
 // red[2] = kmin, red[3] = s1 (the first pass's shift, span bits - 16) when the span has spec_lo..spec_hi
 // bits, else kRsNoPlan (every later kernel of the call then returns at once).
 constexpr uint64_t kRsNoPlan = ~0ull;
-// carry (ckmin, cs1 >= 0): a carried plan (launch_ope_order's prep-free path) is checked instead of one
-// being made: it stands (red[2..3] = ckmin, cs1) iff every holder's key lies in [ckmin, ckmin + 2^(cs1+16))
-// and the top bit of that range is used (the MSD split's top digit is not wasted); else kRsNoPlan.
 __global__ void __launch_bounds__(1024) k_rs_red(const uint64_t* __restrict__ part, size_t nparts,
                                                  uint64_t* __restrict__ red, int spec_lo, int spec_hi,
-                                                 uint64_t* __restrict__ hout, uint64_t ckmin = 0, int cs1 = -1) {
+                                                 uint64_t* __restrict__ hout) {
   uint64_t lo = ~0ull, hi = 0;
   for (size_t i = threadIdx.x; i < nparts; i += 1024) {
     lo = min(lo, part[2 * i]);
@@ -169,12 +166,7 @@ __global__ void __launch_bounds__(1024) k_rs_red(const uint64_t* __restrict__ pa
       hout[0] = mn;
       hout[1] = mx;
     }
-    if (cs1 >= 0) {
-      const uint64_t span = mn <= mx && mn >= ckmin ? mx - ckmin : ~0ull;
-      const int sb = span ? 64 - __builtin_clzll(span) : 0;
-      red[2] = ckmin;
-      red[3] = (mn <= mx && mn >= ckmin && sb == cs1 + kMsdBits) ? (uint64_t)cs1 : kRsNoPlan;
-    } else if (spec_lo <= spec_hi) {
+    if (spec_lo <= spec_hi) {
       const uint64_t span = mn <= mx ? mx - mn : 0ull;
       const int sb = span ? 64 - __builtin_clzll(span) : 0;
       red[2] = mn <= mx ? mn : 0ull;
@@ -277,7 +269,7 @@ __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ key
   uint64_t key[kIt];
   uint32_t id[kIt];
   size_t rix[kIt];
-  uint64_t mlo = ~0ull, mhi = 0;  // mm: the block's holder-key bounds
+  uint64_t mhi = 0;  // mm: the block's largest holder key (offset by the carried kmin)
   if (khi) {
     // split keys (the MSD path's last pass, digit and validity bits >= 32): only the high words, four rows
     // per 16-byte load; an unaligned tail row by row
@@ -317,17 +309,9 @@ __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ key
       key[2 * k] = ids ? kv.x : (hv & 0xFFu) ? rs_ukey(kv.x, desc) - kmin : (kbit ? kRsNoHold : 0ull);
       key[2 * k + 1] = ids ? kv.y : (hv >> 8) ? rs_ukey(kv.y, desc) - kmin : (kbit ? kRsNoHold : 0ull);
       id[2 * k] = id[2 * k + 1] = 0u;
-      if (mm) {  // the raw keys' bounds (before kmin): holders among the in-range rows only
-        if (rix[2 * k] < n && (hv & 0xFFu)) {
-          const uint64_t u = rs_ukey(kv.x, desc);
-          mlo = min(mlo, u);
-          mhi = max(mhi, u);
-        }
-        if (rix[2 * k + 1] < n && (hv >> 8)) {
-          const uint64_t u = rs_ukey(kv.y, desc);
-          mlo = min(mlo, u);
-          mhi = max(mhi, u);
-        }
+      if (mm) {  // the largest offset key of a holder (k_rs_scan_chunks checks the carried plan with it)
+        if (rix[2 * k] < n && (hv & 0xFFu)) mhi = max(mhi, key[2 * k]);
+        if (rix[2 * k + 1] < n && (hv >> 8)) mhi = max(mhi, key[2 * k + 1]);
       }
     }
   } else {
@@ -338,14 +322,20 @@ __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ key
       key[k] = ids ? keys[i] : rs_key_of(keys[i], valid, i, desc, kmin, kbit);  // first pass: keys = the column
       id[k] = need_id ? rs_load_id(ids, i, valid, vbit) : 0u;
       rix[k] = r;
-      if (mm && r < n && (!valid || valid[i])) {
-        const uint64_t u = rs_ukey(keys[i], desc);
-        mlo = min(mlo, u);
-        mhi = max(mhi, u);
-      }
+      if (mm && r < n && (!valid || valid[i])) mhi = max(mhi, key[k]);
     }
   }
-  if (mm) rs_minmax_block(mlo, mhi, mm + 2 * blockIdx.x);
+  if (mm) {  // block max -> mm[blockIdx.x]
+    for (int off = 32; off >= 1; off >>= 1) mhi = max(mhi, (uint64_t)__shfl_xor((long long)mhi, off));
+    __shared__ uint64_t smax[kW];
+    if (lane == 0) smax[threadIdx.x >> 6] = mhi;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t v = smax[0];
+      for (int w = 1; w < kW; ++w) v = max(v, smax[w]);
+      mm[blockIdx.x] = v;
+    }
+  }
   if (rowatom) {
     uint32_t* mine = &wcnt[threadIdx.x >> 6][0];
 #pragma unroll
@@ -413,8 +403,31 @@ __global__ void __launch_bounds__(kScanThreads) k_rs_scan_tiles(uint32_t* __rest
   ctot[(size_t)blockIdx.x * kRsDigits + d] = run;
 }
 
+// Carried plan (mm != nullptr, the first pass of launch_ope_order's prep-free path): the block also takes
+// the max of the first histogram's per-block holder maxima (keys offset by the carried kmin) and keeps the
+// plan (plan[0..1] = kmin, s1) iff it fits: every holder key in [kmin, kmin + 2^(s1+16)) with the top
+// bit used, i.e. 2^(s1+15) <= max < 2^(s1+16) and max <= ~kmin (a key below kmin wraps to at least
+// 2^64 - kmin = ~kmin + 1); else plan[1] = kRsNoPlan and every later kernel of the call returns.
 __global__ void __launch_bounds__(kScanThreads) k_rs_scan_chunks(uint32_t* __restrict__ ctot, size_t nchunks,
-                                                                 uint32_t* __restrict__ dtot) {
+                                                                 uint32_t* __restrict__ dtot,
+                                                                 const uint64_t* __restrict__ mm = nullptr,
+                                                                 size_t nmm = 0, uint64_t* __restrict__ plan = nullptr,
+                                                                 uint64_t ckmin = 0, int cs1 = -1) {
+  if (mm) {
+    uint64_t v = 0;
+    for (size_t i = threadIdx.x; i < nmm; i += kScanThreads) v = max(v, mm[i]);
+    for (int off = 32; off >= 1; off >>= 1) v = max(v, (uint64_t)__shfl_xor((long long)v, off));
+    __shared__ uint64_t sm[(kScanThreads + 63) / 64];
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < (kScanThreads + 63) / 64; ++w) v = max(v, sm[w]);
+      v = max(v, sm[0]);
+      const bool ok = v <= ~ckmin && (v >> (cs1 + kMsdBits)) == 0 && (v >> (cs1 + kMsdBits - 1)) == 1;
+      plan[0] = ckmin;
+      plan[1] = ok ? (uint64_t)cs1 : kRsNoPlan;
+    }
+  }
   const int d = threadIdx.x;
   if (d >= kRsDigits) return;
   uint32_t run = 0;
@@ -640,7 +653,8 @@ constexpr uint32_t kMsdWaveMax = 512;
 constexpr uint32_t kMsdBlockMax = 8192;
 constexpr int kMsdBigBlocks = 256;  // grid of the block path (grid-stride over the big buckets; one per CU:
                                      // a launch that finds no big bucket costs its dispatch, 13 us at 512)
-enum { kMsdCtlBig = 0, kMsdCtlOverflow = 1 };
+enum { kMsdCtlBig = 0, kMsdCtlOverflow = 1, kMsdCtlTicket = 2 };
+static_assert(kMsdBigBlocks < (1 << 16), "k_msd_big ticket: block count in 16 bits");
 
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
   const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
@@ -870,28 +884,54 @@ __device__ __forceinline__ void msd_block_sort(const uint64_t* __restrict__ keys
 
 // buckets of 513..8192 rows with more distinct keys than k_msd_local's partition rounds: one
 // workgroup each (grid-stride over the list); larger ones: overflow flag (host falls back to LSD)
+// hout (nullable): the call's read-back words (overflow flag, plan) stored to the host-mapped words by the
+// last block to finish (a ticket in ctl, cleared with the table by the call's first histogram), instead
+// of a k_rs_publish launch after it (DDSHE_ORDER_PUBLISH=1, A/B). kMsdBigBlocks < 2^16 (ticket bits).
 __global__ void __launch_bounds__(1024) k_msd_big(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ src,
                                                   uint32_t* __restrict__ ids, MsdRuns runs, uint32_t* __restrict__ ctl,
-                                                  const uint32_t* __restrict__ big, const uint64_t* __restrict__ plan) {
+                                                  const uint32_t* __restrict__ big, const uint64_t* __restrict__ plan,
+                                                  uint64_t* __restrict__ hout) {
+  bool planned = true;
   if (plan) {
     const uint64_t s1 = plan[1];
-    if (s1 == kRsNoPlan) return;
-    runs.s1 = (int)s1;
+    planned = s1 != kRsNoPlan;
+    runs.s1 = planned ? (int)s1 : 0;
   }
   __shared__ uint64_t xch[kMsdBlockMax];
-  const uint32_t nbig = ctl[kMsdCtlBig];
+  const uint32_t nbig = planned ? ctl[kMsdCtlBig] : 0u;
   const uint64_t rmask = (1ull << runs.s1) - 1ull;
+  bool ovf_blk = false;  // this block raised the overflow flag
   for (uint32_t q = blockIdx.x; q < nbig; q += gridDim.x) {
     const uint32_t b = big[q];
     const uint32_t lo = runs.first[b], m = runs.end[b] - lo;
     if (m > kMsdBlockMax) {
       if (threadIdx.x == 0) atomicOr(&ctl[kMsdCtlOverflow], 1u);
+      ovf_blk = true;
       continue;
     }
     if (m <= 2048) msd_block_sort<2, 11>(keys, src, ids, lo, m, rmask, xch);
     else if (m <= 4096) msd_block_sort<4, 12>(keys, src, ids, lo, m, rmask, xch);
     else msd_block_sort<8, 13>(keys, src, ids, lo, m, rmask, xch);
     __syncthreads();  // xch is free for the next bucket
+  }
+  if (hout && threadIdx.x == 0) {
+    if (!planned) {  // nothing ran (the table was not cleared this call): block 0 reports the missing plan
+      if (blockIdx.x == 0) {
+        hout[2] = 0ull;
+        hout[3] = kRsNoPlan;
+      }
+      return;
+    }
+    // planned: the call's first histogram cleared the ticket with the table. One atomic per block carries
+    // both the ticket (low 16 bits) and whether the block overflowed (bits 16+), so the last block reads
+    // the overflow verdict from its own atomic's result: no fence, no second word to order against.
+    const uint32_t add = 1u + (ovf_blk ? 0x10000u : 0u);
+    const uint32_t v = atomicAdd(&ctl[kMsdCtlTicket], add) + add;
+    if ((v & 0xFFFFu) == gridDim.x) {  // every other block is done
+      hout[2] = (v >> 16) != 0u ? 1ull : 0ull;
+      hout[3] = plan ? plan[1] : 0ull;
+      ctl[kMsdCtlTicket] = 0u;
+    }
   }
 }
 
@@ -930,12 +970,11 @@ static int order_xcd() {
 // rows; 256 threads measured fastest: 512 / 1024-thread tiles lengthen the write-out's digit runs but
 // cut the blocks per CU, +0 / +10 us on the first pass of 10M rows)
 // First pass of a carried plan (launch_ope_order's prep-free path): the histogram runs with the carried
-// kmin and shift (absolute) and leaves the blocks' holder-key bounds in mm; k_rs_red then checks the plan
-// against them before the scatter (which, like every later kernel, reads the plan from red + 2).
+// kmin and shift (absolute) and leaves each block's largest holder key in mm; k_rs_scan_chunks then checks
+// the plan against them before the scatter (which, like every later kernel, reads the plan from red + 2).
 struct CarryPass {
-  uint64_t* mm = nullptr;  // nullptr: no carried plan
-  uint64_t* red = nullptr;
-  uint64_t* hout = nullptr;
+  uint64_t* mm = nullptr;  // nullptr: no carried plan; else the first histogram's per-block holder maxima
+  uint64_t* red = nullptr;  // the plan goes to red + 2
   uint64_t kmin = 0;
   int s1 = -1;
 };
@@ -956,11 +995,10 @@ static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in,
   // digit of a wave, found by 9 ballots, A/B): same box, 10M rows, raw call 0.318 -> 0.287 ms on the bench's
   // OPE column, 0.675 -> 0.652 on uniform 54-bit keys, 0.265 -> 0.275 with every wave's digits equal
   static const int hatom = order_env("DDSHE_ORDER_HATOM", 1);
-  if (cp.mm) {
+  if (cp.mm) {  // carried plan: checked by k_rs_scan_chunks, before the scatter reads it
     hipLaunchKernelGGL((k_rs_hist<BLK, BLK>), dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n,
                        shift + cp.s1, last, desc, vbit, kbit, cp.kmin, hist, nb, clr, clr ? kMsdTableWords : 0u,
                        pairs && !khi, khi, nullptr, hatom != 0, cp.mm);
-    hipLaunchKernelGGL(k_rs_red, dim3(1), dim3(1024), 0, st, cp.mm, nb, cp.red, 1, 0, cp.hout, cp.kmin, cp.s1);
   } else {
     hipLaunchKernelGGL((k_rs_hist<BLK, BLK>), dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, last,
                        desc, vbit, kbit, kmin, hist, nb, clr, clr ? kMsdTableWords : 0u, pairs && !khi, khi, plan,
@@ -968,7 +1006,12 @@ static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in,
   }
   const size_t nch = (nb + kScanTiles - 1) / kScanTiles;
   hipLaunchKernelGGL(k_rs_scan_tiles, dim3((unsigned)nch), dim3(kScanThreads), 0, st, hist, nb, ctot);
-  hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nch, dtot);
+  if (cp.mm)
+    hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nch, dtot, cp.mm, nb, cp.red + 2,
+                       cp.kmin, cp.s1);
+  else
+    hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nch, dtot, nullptr, (size_t)0,
+                       nullptr, 0ull, -1);
   hipLaunchKernelGGL(k_rs_scatter<BLK>, dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, desc, vbit,
                      kbit, last, kmin, hist, ctot, dtot, nb, kout, ids_out, order_xcd(), runs, khi, khi_out, plan);
 }
@@ -982,10 +1025,11 @@ constexpr int kSpecLo = 40, kSpecHi = 56;
 static std::atomic<int> g_order_spec{0};
 // The plan of the last raw call that ran the MSD path (kmin, s1, direction), carried to the next raw call:
 // that call skips the min / max pass (k_rs_prep + k_rs_red before the passes) — its first histogram uses
-// the carried plan and collects the bounds, k_rs_red checks the plan against them before the first
-// scatter, and a plan that no longer fits (keys below kmin or a span of another bit length) makes every
-// later kernel return; the call then goes on host-planned from the bounds the check stored. Shared by
-// every caller (a race only costs a failed check). DDSHE_ORDER_CARRY=0: the prep pass every call (A/B).
+// the carried plan and takes each block's largest holder key, k_rs_scan_chunks checks the plan with them
+// before the first scatter, and a plan that no longer fits (keys below kmin, or a span of another bit
+// length) makes every later kernel return; the call then runs the min / max pass and goes on as a call
+// without a carried plan. Shared by every caller (a race only costs a failed check).
+// DDSHE_ORDER_CARRY=0: the min / max pass every call (A/B).
 struct CarriedPlan {
   uint64_t kmin;
   int s1;   // -1: none
@@ -1058,6 +1102,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
       ids_in = ids_out;
     }
   };
+  static const int publish_env = order_env("DDSHE_ORDER_PUBLISH", 0);  // 1: k_rs_publish launch (A/B)
   auto msd_tail = [&](uint64_t kmin, const uint64_t* plan) {
     static const uint32_t per_wave = [] {
       const int v = order_env("DDSHE_ORDER_MSDWAVE", 2);
@@ -1065,12 +1110,13 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     }();
     hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / (4 * per_wave)), dim3(256), 0, st, keys2 ? nullptr : col, desc,
                        kmin, kb, ib, out_ids, runs, mctl, mbig, plan, per_wave);
-    hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, kb, ib, out_ids, runs, mctl, mbig, plan);
+    hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, kb, ib, out_ids, runs, mctl, mbig, plan,
+                       (hw && !publish_env) ? hw->d : nullptr);
   };
   // words 2..3 of hw after the call's device work: overflow flag, plan
   auto read_ctl = [&](const uint64_t* plan, uint64_t* ovf, uint64_t* pl) -> hipError_t {
     if (hw) {
-      hipLaunchKernelGGL(k_rs_publish, dim3(1), dim3(1), 0, st, mctl, plan, hw->d);
+      if (publish_env) hipLaunchKernelGGL(k_rs_publish, dim3(1), dim3(1), 0, st, mctl, plan, hw->d);
       hipError_t r = hipStreamSynchronize(st);
       *ovf = hw->h[2];
       *pl = hw->h[3];
@@ -1091,12 +1137,12 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   } else {
     static const int carry_env = order_env("DDSHE_ORDER_CARRY", 1);
     const CarriedPlan cpl = carry_get();
+    bool carried = false;  // a carried plan ran and did not stand: the bounds come from the min / max pass now
     if (hw && carry_env && spec_env && split_env && msd_enabled(n, kSpecLo) && cpl.s1 >= 0 && cpl.desc == desc) {
       const uint64_t* plan = red + 2;
       CarryPass cp;
       cp.mm = part;
       cp.red = red;
-      cp.hout = hw->d;
       cp.kmin = cpl.kmin;
       cp.s1 = cpl.s1;
       const int rel[2] = {0, 8};
@@ -1107,10 +1153,10 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
       if (pl != kRsNoPlan && !ovf) return hipGetLastError();  // the carried plan stands for the next call too
       carry_set(CarriedPlan{0, -1, 0});
       if (pl != kRsNoPlan) skip_msd = true;  // a crowded bucket overflowed: straight to the LSD passes
-      hred[0] = hw->h[0];
-      hred[1] = hw->h[1];
-    } else {
-    const bool spec = hw && spec_env && split_env && msd_enabled(n, kSpecLo) && g_order_spec.load(std::memory_order_relaxed);
+      carried = true;
+    }
+    const bool spec = !carried && hw && spec_env && split_env && msd_enabled(n, kSpecLo) &&
+                      g_order_spec.load(std::memory_order_relaxed);
     if (((uintptr_t)col & 15) == 0 && ((uintptr_t)valid & 1) == 0)
       hipLaunchKernelGGL(k_rs_prep, dim3((unsigned)pb), dim3(256), 0, st, col, valid, n, desc, part);
     else
@@ -1136,7 +1182,6 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     } else {
       if ((e = hipMemcpyAsync(hred, red, sizeof(hred), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
       if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-    }
     }
   }
   // the bytes of max - min (at least one pass when rows may lack the position: its last pass buckets them)
