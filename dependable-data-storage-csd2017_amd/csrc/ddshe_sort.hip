@@ -151,6 +151,7 @@ __global__ void __launch_bounds__(256) k_rs_prep(const int64_t* __restrict__ col
 // red[2] = kmin, red[3] = s1 (the first pass's shift, span bits - 16) when the span has spec_lo..spec_hi
 // bits, else kRsNoPlan (every later kernel of the call then returns at once).
 constexpr uint64_t kRsNoPlan = ~0ull;
+constexpr int kCarryWords = 64;  // the carried plan's max words (k_rs_hist atomicMax, k_rs_scan_chunks check)
 __global__ void __launch_bounds__(1024) k_rs_red(const uint64_t* __restrict__ part, size_t nparts,
                                                  uint64_t* __restrict__ red, int spec_lo, int spec_hi,
                                                  uint64_t* __restrict__ hout) {
@@ -325,7 +326,7 @@ __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ key
       if (mm && r < n && (!valid || valid[i])) mhi = max(mhi, key[k]);
     }
   }
-  if (mm) {  // block max -> mm[blockIdx.x]
+  if (mm) {  // block max, folded into mm[block % kCarryWords] (k_rs_scan_chunks reads and re-zeroes them)
     for (int off = 32; off >= 1; off >>= 1) mhi = max(mhi, (uint64_t)__shfl_xor((long long)mhi, off));
     __shared__ uint64_t smax[kW];
     if (lane == 0) smax[threadIdx.x >> 6] = mhi;
@@ -333,7 +334,7 @@ __global__ void __launch_bounds__(HB) k_rs_hist(const uint64_t* __restrict__ key
     if (threadIdx.x == 0) {
       uint64_t v = smax[0];
       for (int w = 1; w < kW; ++w) v = max(v, smax[w]);
-      mm[blockIdx.x] = v;
+      atomicMax(reinterpret_cast<unsigned long long*>(mm) + (blockIdx.x % kCarryWords), (unsigned long long)v);
     }
   }
   if (rowatom) {
@@ -403,26 +404,25 @@ __global__ void __launch_bounds__(kScanThreads) k_rs_scan_tiles(uint32_t* __rest
   ctot[(size_t)blockIdx.x * kRsDigits + d] = run;
 }
 
-// Carried plan (mm != nullptr, the first pass of launch_ope_order's prep-free path): the block also takes
-// the max of the first histogram's per-block holder maxima (keys offset by the carried kmin) and keeps the
-// plan (plan[0..1] = kmin, s1) iff it fits: every holder key in [kmin, kmin + 2^(s1+16)) with the top
-// bit used, i.e. 2^(s1+15) <= max < 2^(s1+16) and max <= ~kmin (a key below kmin wraps to at least
-// 2^64 - kmin = ~kmin + 1); else plan[1] = kRsNoPlan and every later kernel of the call returns.
+// Carried plan (mm != nullptr, the first pass of launch_ope_order's prep-free path): thread 0 also reads
+// the largest holder key of the first histogram (keys offset by the carried kmin, atomicMax'ed by its
+// blocks into kCarryWords words: one word for all 4,883 blocks of 10M rows serialised the atomics, 23 ->
+// 64 us), re-zeroes the words for the next call, and keeps the plan (plan[0..1] = kmin, s1) iff it
+// fits: every holder key in [kmin, kmin + 2^(s1+16)) with the top bit used, i.e. 2^(s1+15) <= max <
+// 2^(s1+16) and max <= ~kmin (a key below kmin wraps to at least 2^64 - kmin = ~kmin + 1); else plan[1]
+// = kRsNoPlan and every later kernel of the call returns. A word that was not zero before the call (a
+// fresh buffer, a scratch layout of another row count) only raises the max: the check then fails, or
+// passes for a range that still holds every key.
 __global__ void __launch_bounds__(kScanThreads) k_rs_scan_chunks(uint32_t* __restrict__ ctot, size_t nchunks,
                                                                  uint32_t* __restrict__ dtot,
-                                                                 const uint64_t* __restrict__ mm = nullptr,
-                                                                 size_t nmm = 0, uint64_t* __restrict__ plan = nullptr,
+                                                                 uint64_t* __restrict__ mm = nullptr,
+                                                                 uint64_t* __restrict__ plan = nullptr,
                                                                  uint64_t ckmin = 0, int cs1 = -1) {
-  if (mm) {
-    uint64_t v = 0;
-    for (size_t i = threadIdx.x; i < nmm; i += kScanThreads) v = max(v, mm[i]);
+  if (mm && threadIdx.x < 64) {  // wave 0: the kCarryWords maxima
+    uint64_t v = threadIdx.x < kCarryWords ? mm[threadIdx.x] : 0ull;
+    if (threadIdx.x < kCarryWords) mm[threadIdx.x] = 0ull;
     for (int off = 32; off >= 1; off >>= 1) v = max(v, (uint64_t)__shfl_xor((long long)v, off));
-    __shared__ uint64_t sm[(kScanThreads + 63) / 64];
-    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
-    __syncthreads();
     if (threadIdx.x == 0) {
-      for (int w = 1; w < (kScanThreads + 63) / 64; ++w) v = max(v, sm[w]);
-      v = max(v, sm[0]);
       const bool ok = v <= ~ckmin && (v >> (cs1 + kMsdBits)) == 0 && (v >> (cs1 + kMsdBits - 1)) == 1;
       plan[0] = ckmin;
       plan[1] = ok ? (uint64_t)cs1 : kRsNoPlan;
@@ -941,7 +941,7 @@ size_t rs_scratch_bytes(size_t n) {
   // MSD bucket starts + control words + big-bucket list
   return 2 * n * 8 + 32 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 1024 +
          (size_t)kRsDigits * ((rs_blocks(n) + kScanTiles - 1) / kScanTiles) * 4 + 256 +
-         16 * std::max((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows), rs_blocks(n)) + 800 +
+         16 * std::max((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows), rs_blocks(n)) + 8 * kCarryWords + 800 +
          (8 * (size_t)kMsdBuckets + 8) * 4;
 }
 
@@ -970,10 +970,10 @@ static int order_xcd() {
 // rows; 256 threads measured fastest: 512 / 1024-thread tiles lengthen the write-out's digit runs but
 // cut the blocks per CU, +0 / +10 us on the first pass of 10M rows)
 // First pass of a carried plan (launch_ope_order's prep-free path): the histogram runs with the carried
-// kmin and shift (absolute) and leaves each block's largest holder key in mm; k_rs_scan_chunks then checks
-// the plan against them before the scatter (which, like every later kernel, reads the plan from red + 2).
+// kmin and shift (absolute) and atomicMax's each block's largest holder key into *mm; k_rs_scan_chunks checks
+// the plan with it before the scatter (which, like every later kernel, reads the plan from red + 2).
 struct CarryPass {
-  uint64_t* mm = nullptr;  // nullptr: no carried plan; else the first histogram's per-block holder maxima
+  uint64_t* mm = nullptr;  // nullptr: no carried plan; else the word the first histogram's blocks atomicMax into
   uint64_t* red = nullptr;  // the plan goes to red + 2
   uint64_t kmin = 0;
   int s1 = -1;
@@ -1007,11 +1007,11 @@ static void rs_pass(hipStream_t st, const uint64_t* kin, const uint32_t* ids_in,
   const size_t nch = (nb + kScanTiles - 1) / kScanTiles;
   hipLaunchKernelGGL(k_rs_scan_tiles, dim3((unsigned)nch), dim3(kScanThreads), 0, st, hist, nb, ctot);
   if (cp.mm)
-    hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nch, dtot, cp.mm, nb, cp.red + 2,
+    hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nch, dtot, cp.mm, cp.red + 2,
                        cp.kmin, cp.s1);
   else
-    hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nch, dtot, nullptr, (size_t)0,
-                       nullptr, 0ull, -1);
+    hipLaunchKernelGGL(k_rs_scan_chunks, dim3(1), dim3(kScanThreads), 0, st, ctot, nch, dtot, nullptr, nullptr, 0ull,
+                       -1);
   hipLaunchKernelGGL(k_rs_scatter<BLK>, dim3((unsigned)nb), dim3(BLK), 0, st, kin, ids_in, valid, n, shift, desc, vbit,
                      kbit, last, kmin, hist, ctot, dtot, nb, kout, ids_out, order_xcd(), runs, khi, khi_out, plan);
 }
@@ -1025,7 +1025,7 @@ constexpr int kSpecLo = 40, kSpecHi = 56;
 static std::atomic<int> g_order_spec{0};
 // The plan of the last raw call that ran the MSD path (kmin, s1, direction), carried to the next raw call:
 // that call skips the min / max pass (k_rs_prep + k_rs_red before the passes) — its first histogram uses
-// the carried plan and takes each block's largest holder key, k_rs_scan_chunks checks the plan with them
+// the carried plan and takes its largest holder key, k_rs_scan_chunks checks the plan with it
 // before the first scatter, and a plan that no longer fits (keys below kmin, or a span of another bit
 // length) makes every later kernel return; the call then runs the min / max pass and goes on as a call
 // without a carried plan. Shared by every caller (a race only costs a failed check).
@@ -1064,8 +1064,9 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   uint64_t* part = red + 4;  // red[0..1] min / max, red[2..3] the speculative plan
   const size_t pb = (n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows);
   // MSD bucket table (MsdRuns layout), then the control words and the big-bucket list (part: the prep
-  // blocks' bounds, or the first histogram's under a carried plan)
-  uint32_t* mtab = (uint32_t*)(((uintptr_t)(part + 2 * std::max(pb, nb)) + 255) & ~(uintptr_t)255);
+  // blocks' bounds; cword: the carried plan's max word)
+  uint64_t* cword = part + 2 * std::max(pb, nb);  // the carried plan's max words (nothing else writes them)
+  uint32_t* mtab = (uint32_t*)(((uintptr_t)(cword + kCarryWords) + 255) & ~(uintptr_t)255);
   MsdRuns runs{mtab, (unsigned long long*)(mtab + kMsdBuckets), mtab + 3 * kMsdBuckets,
                (unsigned long long*)(mtab + 4 * kMsdBuckets), mtab + 6 * kMsdBuckets, 0};
   uint32_t* mctl = mtab + 7 * kMsdBuckets;
@@ -1141,7 +1142,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
     if (hw && carry_env && spec_env && split_env && msd_enabled(n, kSpecLo) && cpl.s1 >= 0 && cpl.desc == desc) {
       const uint64_t* plan = red + 2;
       CarryPass cp;
-      cp.mm = part;
+      cp.mm = cword;
       cp.red = red;
       cp.kmin = cpl.kmin;
       cp.s1 = cpl.s1;
