@@ -721,15 +721,19 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 // ballot, the next larger key found on the way. The first round takes cur = the bucket's first key
 // (a one-key bucket is then a single copy); a smaller key seen in it restarts from the smallest.
 constexpr int kPartRows = 16;  // rows per lane in flight (8: the same kernel time within noise)
-__device__ __forceinline__ bool msd_wave_partition(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ src,
+// fuse: the bucket's ids are still only in ids[] (not copied to src yet): round 0 reads them there and
+// writes the copy to src as it goes. Its compacted writes land at positions it has already read (out never
+// passes the rows loaded so far), and later rounds read src.
+__device__ __forceinline__ bool msd_wave_partition(const uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
                                                    uint32_t* __restrict__ ids, uint32_t lo, uint32_t m, int lane,
-                                                   int max_rounds) {
+                                                   int max_rounds, bool fuse = false) {
   const uint64_t lt = (1ull << lane) - 1ull;
   uint64_t cur = keys[lo];
   uint32_t out = lo;
   bool restarted = false;
   for (int round = 0; round < max_rounds; ++round) {
     uint64_t nxt = ~0ull, below = ~0ull;
+    const bool copy = fuse && round == 0;
     for (uint32_t p0 = 0; p0 < m; p0 += 64 * kPartRows) {
       uint64_t k[kPartRows];
       uint32_t id[kPartRows];
@@ -737,7 +741,14 @@ __device__ __forceinline__ bool msd_wave_partition(const uint64_t* __restrict__ 
       for (int r = 0; r < kPartRows; ++r) {
         const uint32_t pos = min(p0 + (uint32_t)(r * 64 + lane), m - 1);
         k[r] = keys[lo + pos];
-        id[r] = src[lo + pos];
+        id[r] = copy ? ids[lo + pos] : src[lo + pos];
+      }
+      if (copy) {
+#pragma unroll
+        for (int r = 0; r < kPartRows; ++r) {
+          const uint32_t pos = p0 + (uint32_t)(r * 64 + lane);
+          if (pos < m) src[lo + pos] = id[r];
+        }
       }
 #pragma unroll
       for (int r = 0; r < kPartRows; ++r) {
@@ -750,6 +761,7 @@ __device__ __forceinline__ bool msd_wave_partition(const uint64_t* __restrict__ 
         if (in && k[r] < below) below = k[r];
       }
     }
+    if (copy) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the copy lands before later rounds read it
     if (!restarted) {
       restarted = true;
       below = wave_min_u64(below);
@@ -789,10 +801,13 @@ __device__ __forceinline__ void msd_wave_sort(const uint64_t* __restrict__ keys,
 __device__ __forceinline__ void msd_bucket(const int64_t* __restrict__ col, int desc, uint64_t kmin,
                                            uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
                                            uint32_t* __restrict__ ids, uint32_t b, uint32_t lo, uint32_t m, int s1,
-                                           uint32_t* __restrict__ ctl, uint32_t* __restrict__ big, int lane) {
+                                           uint32_t* __restrict__ ctl, uint32_t* __restrict__ big, int lane,
+                                           bool fuse_copy) {
   // this bucket's grouped ids to the side buffer (free after the last pass), and (gather mode) their keys
-  // gathered from the column by id, read from there below
-  for (uint32_t p0 = 0; p0 < m; p0 += 512) {  // 8 loads in flight per lane, then their stores
+  // gathered from the column by id, read from there below; with the sorted keys written by the last pass
+  // the copy rides on the first partition round instead (DDSHE_ORDER_FUSECOPY=0: this loop, A/B)
+  const bool fuse = col == nullptr && fuse_copy;
+  for (uint32_t p0 = 0; p0 < (fuse ? 0u : m); p0 += 512) {  // 8 loads in flight per lane, then their stores
     uint32_t v[8];
     int64_t c[8];
 #pragma unroll
@@ -814,7 +829,7 @@ __device__ __forceinline__ void msd_bucket(const int64_t* __restrict__ col, int 
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's copies land before its lanes read them
-  if (msd_wave_partition(keys, src, ids, lo, m, lane, m <= kMsdWaveMax ? 2 : 16)) return;
+  if (msd_wave_partition(keys, src, ids, lo, m, lane, m <= kMsdWaveMax ? 2 : 16, fuse)) return;
   if (m > kMsdWaveMax) {
     if (lane == 0) big[atomicAdd(&ctl[kMsdCtlBig], 1u)] = b;
     return;
@@ -838,7 +853,8 @@ __global__ void __launch_bounds__(256) k_msd_local(const int64_t* __restrict__ c
                                                    uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
                                                    uint32_t* __restrict__ ids, MsdRuns runs,
                                                    uint32_t* __restrict__ ctl, uint32_t* __restrict__ big,
-                                                   const uint64_t* __restrict__ plan, uint32_t per_wave) {
+                                                   const uint64_t* __restrict__ plan, uint32_t per_wave,
+                                                   bool fuse_copy) {
   if (plan) {
     const uint64_t s1 = plan[1];
     if (s1 == kRsNoPlan) return;
@@ -859,7 +875,7 @@ __global__ void __launch_bounds__(256) k_msd_local(const int64_t* __restrict__ c
     // wave-uniform (SGPRs): the bucket's addressing stays scalar in msd_bucket
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)lo_l, j));
     const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)m_l, j));
-    msd_bucket(col, desc, kmin, keys, src, ids, b0 + (uint32_t)j, lo, m, runs.s1, ctl, big, lane);
+    msd_bucket(col, desc, kmin, keys, src, ids, b0 + (uint32_t)j, lo, m, runs.s1, ctl, big, lane, fuse_copy);
   }
 }
 
@@ -1105,12 +1121,13 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
   };
   static const int publish_env = order_env("DDSHE_ORDER_PUBLISH", 0);  // 1: k_rs_publish launch (A/B)
   auto msd_tail = [&](uint64_t kmin, const uint64_t* plan) {
+    static const int fuse_copy = order_env("DDSHE_ORDER_FUSECOPY", 1);
     static const uint32_t per_wave = [] {
       const int v = order_env("DDSHE_ORDER_MSDWAVE", 2);
       return (v >= 1 && v <= 64 && (v & (v - 1)) == 0) ? (uint32_t)v : 2u;
     }();
     hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / (4 * per_wave)), dim3(256), 0, st, keys2 ? nullptr : col, desc,
-                       kmin, kb, ib, out_ids, runs, mctl, mbig, plan, per_wave);
+                       kmin, kb, ib, out_ids, runs, mctl, mbig, plan, per_wave, fuse_copy != 0);
     hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, kb, ib, out_ids, runs, mctl, mbig, plan,
                        (hw && !publish_env) ? hw->d : nullptr);
   };
