@@ -6,7 +6,7 @@ exact sequence bench.py's N > 1 ranks run (DDSRestServer.scala:412-430 folded by
 must equal the resident fold and, on a prefix, the oracle's fold; the worker also reports that librccl
 is mapped into it, so the test cannot pass on gloo by accident."""
 import os
-import random
+import socket
 
 import pytest
 import torch.multiprocessing as mp
@@ -60,7 +60,9 @@ def test_rccl_device_gather_combine(keys):
     key = keys["paillier2048_committed"]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 31500 + random.Random(7).randrange(1000)
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:  # a free port for the TCP store
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
     p = ctx.Process(target=_worker, args=(port, key, 100_000, 1500, q))
     p.start()
     try:
