@@ -1398,10 +1398,10 @@ class EntrySearchWorkload(_Workload):
                 print("VERIFY FAILED", file=sys.stderr)
         _, _, dev_ms, _ = self.eng.timing()
         scan_s = dev_ms / 1e3 / (2 * a.steps)
-        # per scan: the 4-byte fingerprints of the elements it must look at (OR: all; Eq: one per
-        # row + that row's 8-byte offset) + one 4-byte id per match
-        alg_or = self.mine * 4 * self.ELEMS + 4 * len(res[0])
-        alg_eq = self.mine * (8 + 4) + 4 * len(res[1])
+        # per scan: the 2-byte fingerprints of the elements it must look at (OR: all; Eq: the element at
+        # the position, through the position index, + its present bit) + one 4-byte id per match
+        alg_or = self.mine * 2 * self.ELEMS + 4 * len(res[0])
+        alg_eq = self.mine * (2 + 1 / 8) + 4 * len(res[1])
         alg = (alg_or + alg_eq) / 2
         roof = {"bound": "hbm", "kernel": "k_str_any + k_byte_count/k_ope_scatter (OR), k_str_eq_count + k_ope_scatter (Eq); device time",
                 "achieved": alg / scan_s / 1e9, "peak": 8000.0, "unit": "GB/s", "frac": alg / scan_s / 1e9 / 8000.0,

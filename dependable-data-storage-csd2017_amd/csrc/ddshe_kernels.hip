@@ -733,9 +733,9 @@ __global__ void __launch_bounds__(kOpeBlock) k_ope_count(const int64_t* __restri
 
 // SearchEq/NEq front end (ddshe_strscan.hip's position index): same tile layout and masks as
 // k_ope_count; row r = row0 + i matches iff its present bit is set (length - 1 > position) and its
-// fingerprint equals the needle's (bytes verified on a hit), xor negate. Reads 4 B + 1 bit per row and
+// fingerprint equals the needle's (bytes verified on a hit), xor negate. Reads 2 B + 1 bit per row and
 // writes no per-row flags.
-__global__ void __launch_bounds__(kOpeBlock) k_str_eq_count(const uint32_t* __restrict__ posfp,
+__global__ void __launch_bounds__(kOpeBlock) k_str_eq_count(const StrFp* __restrict__ posfp,
                                                             const uint64_t* __restrict__ present, size_t row0, size_t n,
                                                             const uint64_t* __restrict__ row_beg,
                                                             const uint64_t* __restrict__ elem_off,
@@ -745,19 +745,19 @@ __global__ void __launch_bounds__(kOpeBlock) k_str_eq_count(const uint32_t* __re
                                                             uint32_t* __restrict__ masks,
                                                             uint32_t* __restrict__ counts) {
   const size_t t0 = (size_t)blockIdx.x * kOpeTile + 4 * (size_t)threadIdx.x;
-  const uint32_t want = (uint32_t)(nd.h[0] >> 32);
+  const uint32_t want = str_fp(nd.h[0]);
   uint32_t f[kOpeItems];
   uint32_t pb[kOpeGroups];
   const bool vec = (row0 % 4 == 0) && t0 + (kOpeGroups - 1) * 4 * kOpeBlock + 3 < n;
 #pragma unroll
   for (int k = 0; k < kOpeGroups; ++k) {
     const size_t i = t0 + (size_t)k * 4 * kOpeBlock;
-    if (vec) {
-      const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(posfp + row0 + i));
-      f[4 * k] = x.x;
-      f[4 * k + 1] = x.y;
-      f[4 * k + 2] = x.z;
-      f[4 * k + 3] = x.w;
+    if (vec) {  // 4 fingerprints in one 8-byte load
+      const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(posfp + row0 + i));
+      f[4 * k] = (uint32_t)x & 0xFFFFu;
+      f[4 * k + 1] = (uint32_t)(x >> 16) & 0xFFFFu;
+      f[4 * k + 2] = (uint32_t)(x >> 32) & 0xFFFFu;
+      f[4 * k + 3] = (uint32_t)(x >> 48);
       const size_t r = row0 + i;  // 4 rows inside one present word (r % 4 == 0)
       pb[k] = (uint32_t)(present[r >> 6] >> (r & 63)) & 0xFu;
     } else {
@@ -1423,7 +1423,7 @@ size_t ope_blocks(size_t n) { return (n + kOpeTile - 1) / kOpeTile; }
 
 size_t ope_scratch_bytes(size_t n) { return ope_blocks(n) * (4 + 4 * kOpeBlock) + 8; }
 
-hipError_t launch_str_eq_compact(const uint32_t* posfp, const uint64_t* present, size_t row0, size_t nrows,
+hipError_t launch_str_eq_compact(const StrFp* posfp, const uint64_t* present, size_t row0, size_t nrows,
                                  const uint64_t* row_beg, const uint64_t* elem_off, const uint8_t* chars,
                                  const uint8_t* nchars, const StrNeedles& nd, uint64_t position, int negate,
                                  void* scratch, uint64_t* total, uint32_t* out, hipStream_t st) {

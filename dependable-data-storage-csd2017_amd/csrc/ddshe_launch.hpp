@@ -161,7 +161,10 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
                             const MappedWords* hw = nullptr);
 // deterministic-equality scans (ddshe_strscan.hip)
 // 64-bit digest of an element string (FNV-1a over the bytes, splitmix finaliser); identical on
-// host (needles) and device (table). The table keeps its top 32 bits as a per-element fingerprint.
+// host (needles) and device (table). The table keeps its top 16 bits as a per-element fingerprint
+// (str_fp): a scan streams 2 B per element, and a fingerprint hit is always confirmed on the bytes, so
+// the wider digest only changes how often that happens (round 5: 32 bits, 4 B per element).
+using StrFp = uint16_t;
 __host__ __device__ inline uint64_t str_digest(const uint8_t* p, uint64_t len) {
   uint64_t h = 0xcbf29ce484222325ull ^ len;
   for (uint64_t i = 0; i < len; ++i) h = (h ^ p[i]) * 0x100000001b3ull;
@@ -171,6 +174,7 @@ __host__ __device__ inline uint64_t str_digest(const uint8_t* p, uint64_t len) {
   h *= 0x94d049bb133111ebull;
   return h ^ (h >> 31);
 }
+__host__ __device__ inline StrFp str_fp(uint64_t digest) { return (StrFp)(digest >> 48); }
 struct StrNeedles {  // up to 3 items (SearchEntryAND/OR triplets), bytes in a device buffer or inline
   uint64_t h[3];
   uint64_t len[3];
@@ -181,7 +185,7 @@ struct StrNeedles {  // up to 3 items (SearchEntryAND/OR triplets), bytes in a d
   static constexpr int kStrInline = 128;
   uint8_t inl[kStrInline];
 };
-hipError_t launch_str_digest(const uint8_t* chars, const uint64_t* elem_off, size_t nelems, uint32_t* fp,
+hipError_t launch_str_digest(const uint8_t* chars, const uint64_t* elem_off, size_t nelems, StrFp* fp,
                              hipStream_t st);
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
 __device__ __forceinline__ bool str_equal(const uint8_t* __restrict__ x, const uint8_t* __restrict__ y, uint64_t len) {
@@ -202,7 +206,7 @@ constexpr uint32_t kStrDead = 0xFFFFFFFFu;  // elem_row of a superseded element 
 // SearchEq/NEq over a position index straight into the compaction masks (k_str_eq_count, the tile
 // layout of k_ope_count) + k_ope_scatter: ascending row ids (relative to row0) of the matching rows;
 // row_beg[r]: the first heap element of row r's current version
-hipError_t launch_str_eq_compact(const uint32_t* posfp, const uint64_t* present, size_t row0, size_t nrows,
+hipError_t launch_str_eq_compact(const StrFp* posfp, const uint64_t* present, size_t row0, size_t nrows,
                                  const uint64_t* row_beg, const uint64_t* elem_off, const uint8_t* chars,
                                  const uint8_t* nchars, const StrNeedles& nd, uint64_t position, int negate,
                                  void* scratch, uint64_t* total, uint32_t* out, hipStream_t st);
@@ -210,10 +214,10 @@ hipError_t launch_str_eq_compact(const uint32_t* posfp, const uint64_t* present,
 // and a present bit (live and length - 1 > position) for rows [r_first, r_first + count) (r_first a
 // multiple of 64), or patched for the distinct rows ids[0..n)
 hipError_t launch_str_posfp(const uint64_t* row_beg, const uint32_t* row_len, const uint8_t* live, size_t r_first,
-                            size_t count, const uint32_t* fp, uint64_t position, uint32_t* posfp, uint64_t* present,
+                            size_t count, const StrFp* fp, uint64_t position, StrFp* posfp, uint64_t* present,
                             hipStream_t st);
 hipError_t launch_str_posfp_ids(const uint32_t* ids, size_t n, const uint64_t* row_beg, const uint32_t* row_len,
-                                const uint8_t* live, const uint32_t* fp, uint64_t position, uint32_t* posfp,
+                                const uint8_t* live, const StrFp* fp, uint64_t position, StrFp* posfp,
                                 uint64_t* present, hipStream_t st);
 // string-table mutations: row descriptors of distinct rows ids[i] <- (beg[i], len[i]), live; heap
 // elements of superseded versions killed; heap compaction into fresh buffers (one wave per row)
@@ -221,13 +225,13 @@ hipError_t launch_str_rows_set(const uint32_t* ids, const uint64_t* beg, const u
                                uint64_t* row_beg, uint32_t* row_len, uint8_t* live, hipStream_t st);
 hipError_t launch_str_kill(const uint64_t* beg, const uint32_t* len, size_t n, uint32_t* elem_row, hipStream_t st);
 hipError_t launch_str_compact(size_t nrows, const uint64_t* old_beg, const uint32_t* len, const uint64_t* new_beg,
-                              const uint64_t* new_cbeg, const uint64_t* elem_off, const uint32_t* fp,
-                              const uint8_t* chars, uint64_t* nelem_off, uint32_t* nfp, uint32_t* nelem_row,
+                              const uint64_t* new_cbeg, const uint64_t* elem_off, const StrFp* fp,
+                              const uint8_t* chars, uint64_t* nelem_off, StrFp* nfp, uint32_t* nelem_row,
                               uint8_t* nchars, hipStream_t st);
 // SearchEntry/OR/AND/IsElement: flag byte r - row0 |= bit j for every heap element in [e_first,
 // e_first + nelems) equal to needle j whose owner r is live and in [row0, row0 + nrows) (flags zeroed by
 // the launcher unless flags_zeroed, 4-byte aligned)
-hipError_t launch_str_any(const uint32_t* fp, uint64_t e_first, size_t nelems, const uint32_t* elem_row,
+hipError_t launch_str_any(const StrFp* fp, uint64_t e_first, size_t nelems, const uint32_t* elem_row,
                           const uint8_t* live, size_t row0, size_t nrows, const uint64_t* elem_off, const uint8_t* chars,
                           const uint8_t* nchars, const StrNeedles& nd, uint8_t* flags, hipStream_t st,
                           bool flags_zeroed = false);

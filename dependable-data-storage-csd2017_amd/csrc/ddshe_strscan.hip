@@ -5,14 +5,15 @@
 // HomoDet.compare (hlib, absent) is taken as equality of the ciphertext strings.
 //
 // Layout in HBM (dds_strtab, ddshe_strtab.cpp): an element heap -- chars (element strings back to back),
-// elem_off[nheap+1] (u64 byte offsets), a resident 32-bit fingerprint per element (k_str_digest: top
-// half of str_digest) and the row owning each element (elem_row; kStrDead for a superseded version) --
+// elem_off[nheap+1] (u64 byte offsets), a resident 16-bit fingerprint per element (k_str_digest: top
+// 16 bits of str_digest) and the row owning each element (elem_row; kStrDead for a superseded version) --
 // and per row its current version: row_beg (first heap element), row_len (element count) and a live
 // byte (0: the set was removed, RemoveSet writes None). A row write appends a new version to the heap
 // and kills the old one; the heap is compacted (k_str_compact) when it runs out of room. A scan
-// streams 4 B of fingerprint per element it must look at; bytes are compared only on a fingerprint hit
-// (about nelems * needles / 2^32 false hits per scan), so results stay exact.
-//   k_str_any: four 16-byte fingerprint loads per thread (block-interleaved quads); a verified
+// streams 2 B of fingerprint per element it must look at; bytes are compared only on a fingerprint hit
+// (about nelems * needles / 2^16 false hits per scan: ~3,700 for SearchEntryOR's 3 needles over 80M
+// elements, each a row lookup and a 32-byte compare), so results stay exact.
+//   k_str_any: four 16-byte loads of 8 fingerprints per thread (block-interleaved octets); a verified
 //              hit of a live row's current version ORs the needle bit into the row's flag byte;
 //   SearchEq: the position index below (k_str_posfp) read by k_str_eq_count (ddshe_kernels.hip),
 //              which writes the compaction masks directly; writes patch it (k_str_posfp_ids);
@@ -25,34 +26,34 @@
 namespace ddshe {
 
 __global__ void k_str_digest(const uint8_t* __restrict__ chars, const uint64_t* __restrict__ elem_off, size_t nelems,
-                             uint32_t* __restrict__ fp) {
+                             StrFp* __restrict__ fp) {
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= nelems) return;
   const uint64_t a = elem_off[e], b = elem_off[e + 1];
-  fp[e] = (uint32_t)(str_digest(chars + a, b - a) >> 32);
+  fp[e] = str_fp(str_digest(chars + a, b - a));
 }
 
 // SearchEq's position-major index (built on the first query at a position, kept with the table and
 // patched by every write): posfp[r] = fingerprint of row r's element `position`, present bit r = the
 // row is live and passes the route's strict guard (length - 1 > position, DDSRestServer.scala:615). A
-// query (k_str_eq_count) reads 4 B per row, coalesced, instead of gathering one 4-byte fingerprint per
+// query (k_str_eq_count) reads 2 B per row, coalesced, instead of gathering one fingerprint per
 // 32-byte sector; only fingerprint hits touch the row descriptors and the bytes.
 __device__ __forceinline__ bool str_present(const uint64_t* __restrict__ row_beg, const uint32_t* __restrict__ row_len,
-                                            const uint8_t* __restrict__ live, const uint32_t* __restrict__ fp,
-                                            size_t r, uint64_t position, uint32_t* f) {
+                                            const uint8_t* __restrict__ live, const StrFp* __restrict__ fp,
+                                            size_t r, uint64_t position, StrFp* f) {
   const bool pres = live[r] != 0 && (uint64_t)row_len[r] > position + 1;
-  *f = pres ? fp[row_beg[r] + position] : 0u;
+  *f = pres ? fp[row_beg[r] + position] : (StrFp)0;
   return pres;
 }
 // rows [r_first, r_first + count), r_first a multiple of 64: whole present words
 __global__ void k_str_posfp(const uint64_t* __restrict__ row_beg, const uint32_t* __restrict__ row_len,
                             const uint8_t* __restrict__ live, size_t r_first, size_t count,
-                            const uint32_t* __restrict__ fp, uint64_t position, uint32_t* __restrict__ posfp,
+                            const StrFp* __restrict__ fp, uint64_t position, StrFp* __restrict__ posfp,
                             uint64_t* __restrict__ present) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x, r = r_first + i;
   bool pres = false;
   if (i < count) {
-    uint32_t f;
+    StrFp f;
     pres = str_present(row_beg, row_len, live, fp, r, position, &f);
     posfp[r] = f;
   }
@@ -62,12 +63,12 @@ __global__ void k_str_posfp(const uint64_t* __restrict__ row_beg, const uint32_t
 // distinct rows ids[0..n) (after a write / live change): their entries and present bits
 __global__ void k_str_posfp_ids(const uint32_t* __restrict__ ids, size_t n, const uint64_t* __restrict__ row_beg,
                                 const uint32_t* __restrict__ row_len, const uint8_t* __restrict__ live,
-                                const uint32_t* __restrict__ fp, uint64_t position, uint32_t* __restrict__ posfp,
+                                const StrFp* __restrict__ fp, uint64_t position, StrFp* __restrict__ posfp,
                                 uint64_t* __restrict__ present) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const size_t r = ids[i];
-  uint32_t f;
+  StrFp f;
   const bool pres = str_present(row_beg, row_len, live, fp, r, position, &f);
   posfp[r] = f;
   const unsigned long long bit = 1ull << (r & 63);
@@ -105,8 +106,8 @@ __global__ void __launch_bounds__(256) k_str_compact(size_t nrows, const uint64_
                                                      const uint64_t* __restrict__ new_beg,
                                                      const uint64_t* __restrict__ new_cbeg,
                                                      const uint64_t* __restrict__ elem_off,
-                                                     const uint32_t* __restrict__ fp, const uint8_t* __restrict__ chars,
-                                                     uint64_t* __restrict__ nelem_off, uint32_t* __restrict__ nfp,
+                                                     const StrFp* __restrict__ fp, const uint8_t* __restrict__ chars,
+                                                     uint64_t* __restrict__ nelem_off, StrFp* __restrict__ nfp,
                                                      uint32_t* __restrict__ nelem_row, uint8_t* __restrict__ nchars) {
   const size_t r = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
@@ -123,41 +124,45 @@ __global__ void __launch_bounds__(256) k_str_compact(size_t nrows, const uint64_
   for (uint64_t b = lane; b < c1 - c0; b += 64) nchars[cb + b] = chars[c0 + b];
 }
 
-// one thread per kStrQuads element quads, block-interleaved (quad b*256*kStrQuads + k*256 + tid: each
-// 16-byte load instruction of a wave covers 1 KiB contiguous; all kStrQuads loads in flight together);
+// one thread per kStrOcts element octets, block-interleaved (octet b*256*kStrOcts + k*256 + tid: each
+// 16-byte load instruction of a wave covers 1 KiB contiguous; all kStrOcts loads in flight together);
 // a verified hit of a live row r in [row0, row0 + nrows) ORs the needle bit into flag byte r - row0 (a
 // 32-bit atomic on the byte's word: hits are rare)
-constexpr int kStrQuads = 4;
-__global__ void __launch_bounds__(256) k_str_any(const uint32_t* __restrict__ fp, uint64_t e_first, size_t nelems,
+constexpr int kStrOcts = 2;
+__global__ void __launch_bounds__(256) k_str_any(const StrFp* __restrict__ fp, uint64_t e_first, size_t nelems,
                                                  const uint32_t* __restrict__ elem_row,
                                                  const uint8_t* __restrict__ live, size_t row0, size_t nrows,
                                                  const uint64_t* __restrict__ elem_off, const uint8_t* __restrict__ chars,
                                                  const uint8_t* __restrict__ nchars, StrNeedles nd,
                                                  uint8_t* __restrict__ flags) {
-  const size_t qb = (size_t)blockIdx.x * 256 * kStrQuads + threadIdx.x;  // quad of k = 0
-  uint32_t f[4 * kStrQuads];
+  const size_t ob = (size_t)blockIdx.x * 256 * kStrOcts + threadIdx.x;  // octet of k = 0
+  uint32_t f[4 * kStrOcts];  // two fingerprints per word
 #pragma unroll
-  for (int k = 0; k < kStrQuads; ++k) {
-    const size_t q = qb + (size_t)k * 256;
-    const uint64_t e0 = e_first + 4 * q;
-    if (e_first % 4 == 0 && 4 * q + 3 < nelems) {
+  for (int k = 0; k < kStrOcts; ++k) {
+    const size_t o = ob + (size_t)k * 256;
+    const uint64_t e0 = e_first + 8 * o;
+    if (e_first % 8 == 0 && 8 * o + 7 < nelems) {
       const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(fp + e0));
       f[4 * k] = x.x;
       f[4 * k + 1] = x.y;
       f[4 * k + 2] = x.z;
       f[4 * k + 3] = x.w;
     } else {
-      for (int i = 0; i < 4; ++i) f[4 * k + i] = 4 * q + i < nelems ? fp[e0 + i] : 0u;
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t lo = 8 * o + 2 * i < nelems ? fp[e0 + 2 * i] : 0u;
+        const uint32_t hi = 8 * o + 2 * i + 1 < nelems ? fp[e0 + 2 * i + 1] : 0u;
+        f[4 * k + i] = lo | (hi << 16);
+      }
     }
   }
-  const uint32_t h0 = (uint32_t)(nd.h[0] >> 32), h1 = (uint32_t)(nd.h[1] >> 32), h2 = (uint32_t)(nd.h[2] >> 32);
+  const uint32_t h0 = str_fp(nd.h[0]), h1 = str_fp(nd.h[1]), h2 = str_fp(nd.h[2]);
 #pragma unroll
-  for (int k = 0; k < kStrQuads; ++k)
+  for (int k = 0; k < kStrOcts; ++k)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const size_t ei = 4 * (qb + (size_t)k * 256) + i;  // element index relative to e_first
+    for (int i = 0; i < 8; ++i) {
+      const size_t ei = 8 * (ob + (size_t)k * 256) + i;  // element index relative to e_first
       if (ei >= nelems) continue;
-      const uint32_t v = f[4 * k + i];
+      const uint32_t v = (f[4 * k + i / 2] >> (16 * (i & 1))) & 0xFFFFu;
       const bool c0 = v == h0, c1 = nd.n > 1 && v == h1, c2 = nd.n > 2 && v == h2;
       if (!(c0 | c1 | c2)) continue;  // the common case: no fingerprint hit
       const uint64_t e = e_first + ei;
@@ -174,7 +179,7 @@ __global__ void __launch_bounds__(256) k_str_any(const uint32_t* __restrict__ fp
     }
 }
 
-hipError_t launch_str_digest(const uint8_t* chars, const uint64_t* elem_off, size_t nelems, uint32_t* fp,
+hipError_t launch_str_digest(const uint8_t* chars, const uint64_t* elem_off, size_t nelems, StrFp* fp,
                              hipStream_t st) {
   if (nelems == 0) return hipSuccess;
   hipLaunchKernelGGL(k_str_digest, dim3((unsigned)((nelems + 255) / 256)), dim3(256), 0, st, chars, elem_off, nelems,
@@ -183,7 +188,7 @@ hipError_t launch_str_digest(const uint8_t* chars, const uint64_t* elem_off, siz
 }
 
 hipError_t launch_str_posfp(const uint64_t* row_beg, const uint32_t* row_len, const uint8_t* live, size_t r_first,
-                            size_t count, const uint32_t* fp, uint64_t position, uint32_t* posfp, uint64_t* present,
+                            size_t count, const StrFp* fp, uint64_t position, StrFp* posfp, uint64_t* present,
                             hipStream_t st) {
   if (count == 0) return hipSuccess;
   if (r_first % 64) return hipErrorInvalidValue;
@@ -193,7 +198,7 @@ hipError_t launch_str_posfp(const uint64_t* row_beg, const uint32_t* row_len, co
 }
 
 hipError_t launch_str_posfp_ids(const uint32_t* ids, size_t n, const uint64_t* row_beg, const uint32_t* row_len,
-                                const uint8_t* live, const uint32_t* fp, uint64_t position, uint32_t* posfp,
+                                const uint8_t* live, const StrFp* fp, uint64_t position, StrFp* posfp,
                                 uint64_t* present, hipStream_t st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_str_posfp_ids, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ids, n, row_beg, row_len,
@@ -216,8 +221,8 @@ hipError_t launch_str_kill(const uint64_t* beg, const uint32_t* len, size_t n, u
 }
 
 hipError_t launch_str_compact(size_t nrows, const uint64_t* old_beg, const uint32_t* len, const uint64_t* new_beg,
-                              const uint64_t* new_cbeg, const uint64_t* elem_off, const uint32_t* fp,
-                              const uint8_t* chars, uint64_t* nelem_off, uint32_t* nfp, uint32_t* nelem_row,
+                              const uint64_t* new_cbeg, const uint64_t* elem_off, const StrFp* fp,
+                              const uint8_t* chars, uint64_t* nelem_off, StrFp* nfp, uint32_t* nelem_row,
                               uint8_t* nchars, hipStream_t st) {
   if (nrows == 0) return hipSuccess;
   hipLaunchKernelGGL(k_str_compact, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, st, nrows, old_beg, len, new_beg,
@@ -225,15 +230,15 @@ hipError_t launch_str_compact(size_t nrows, const uint64_t* old_beg, const uint3
   return hipGetLastError();
 }
 
-hipError_t launch_str_any(const uint32_t* fp, uint64_t e_first, size_t nelems, const uint32_t* elem_row,
+hipError_t launch_str_any(const StrFp* fp, uint64_t e_first, size_t nelems, const uint32_t* elem_row,
                           const uint8_t* live, size_t row0, size_t nrows, const uint64_t* elem_off, const uint8_t* chars,
                           const uint8_t* nchars, const StrNeedles& nd, uint8_t* flags, hipStream_t st,
                           bool flags_zeroed) {
   if (nrows == 0) return hipSuccess;
   hipError_t e = flags_zeroed ? hipSuccess : hipMemsetAsync(flags, 0, (nrows + 3) & ~(size_t)3, st);  // whole words
   if (e != hipSuccess || nelems == 0) return e;
-  const size_t quads = (nelems + 3) / 4, per_block = (size_t)256 * kStrQuads;
-  hipLaunchKernelGGL(k_str_any, dim3((unsigned)((quads + per_block - 1) / per_block)), dim3(256), 0, st, fp, e_first,
+  const size_t octs = (nelems + 7) / 8, per_block = (size_t)256 * kStrOcts;
+  hipLaunchKernelGGL(k_str_any, dim3((unsigned)((octs + per_block - 1) / per_block)), dim3(256), 0, st, fp, e_first,
                      nelems, elem_row, live, row0, nrows, elem_off, chars, nchars, nd, flags);
   return hipGetLastError();
 }

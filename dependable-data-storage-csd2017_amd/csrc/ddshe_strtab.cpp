@@ -39,7 +39,7 @@ void dfree(T*& p) {
 
 struct PosIdx {
   uint64_t position = 0;
-  uint32_t* fp = nullptr;
+  StrFp* fp = nullptr;
   uint64_t* present = nullptr;
   ~PosIdx() {
     dfree(fp);
@@ -63,7 +63,7 @@ struct dds_strtab {
   size_t vel = 0, vch = 0;  // elements / bytes of the rows' current versions (dead rows' included)
   uint8_t* chars = nullptr;
   uint64_t* elem_off = nullptr;  // nheap + 1 entries in use (elem_off[nheap] == nchars)
-  uint32_t* fp = nullptr;
+  StrFp* fp = nullptr;
   uint32_t* elem_row = nullptr;
   uint64_t compactions = 0;
   // SearchEq position indexes, most recent last (sized rcap)
@@ -122,7 +122,8 @@ int grow_rows(dds_strtab* t, size_t need, hipStream_t st) {
 int compact(dds_strtab* t, size_t ecap, size_t ccap, Worker* w, hipStream_t st) {
   uint8_t* ch = nullptr;
   uint64_t* eo = nullptr;
-  uint32_t *f = nullptr, *er = nullptr;
+  StrFp* f = nullptr;
+  uint32_t* er = nullptr;
   if (dalloc(&ch, ccap) != hipSuccess || dalloc(&eo, ecap + 1) != hipSuccess || dalloc(&f, ecap) != hipSuccess ||
       dalloc(&er, ecap) != hipSuccess) {
     dfree(ch);
