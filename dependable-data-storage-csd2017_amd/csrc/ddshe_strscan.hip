@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(256) k_str_compact(size_t nrows, const uint64_
 // 16-byte load instruction of a wave covers 1 KiB contiguous; all kStrOcts loads in flight together);
 // a verified hit of a live row r in [row0, row0 + nrows) ORs the needle bit into flag byte r - row0 (a
 // 32-bit atomic on the byte's word: hits are rare)
-constexpr int kStrOcts = 2;
+constexpr int kStrOcts = 4;
 __global__ void __launch_bounds__(256) k_str_any(const StrFp* __restrict__ fp, uint64_t e_first, size_t nelems,
                                                  const uint32_t* __restrict__ elem_row,
                                                  const uint8_t* __restrict__ live, size_t row0, size_t nrows,
@@ -156,6 +156,27 @@ __global__ void __launch_bounds__(256) k_str_any(const StrFp* __restrict__ fp, u
     }
   }
   const uint32_t h0 = str_fp(nd.h[0]), h1 = str_fp(nd.h[1]), h2 = str_fp(nd.h[2]);
+  // the common case without per-element work: a zero-halfword test of (word ^ needle pair) per needle
+  // ((t - 0x00010001) & ~t & 0x80008000 is non-zero iff a half of t is zero), no bounds checks (padding
+  // reads as fingerprint 0; a hit on it drops to the exact loop below, which checks bounds)
+  {
+    uint32_t any = 0;
+    const uint32_t p0 = h0 | (h0 << 16), p1 = h1 | (h1 << 16), p2 = h2 | (h2 << 16);
+#pragma unroll
+    for (int w = 0; w < 4 * kStrOcts; ++w) {
+      uint32_t t = f[w] ^ p0;
+      any |= (t - 0x00010001u) & ~t;
+      if (nd.n > 1) {
+        t = f[w] ^ p1;
+        any |= (t - 0x00010001u) & ~t;
+      }
+      if (nd.n > 2) {
+        t = f[w] ^ p2;
+        any |= (t - 0x00010001u) & ~t;
+      }
+    }
+    if ((any & 0x80008000u) == 0) return;
+  }
 #pragma unroll
   for (int k = 0; k < kStrOcts; ++k)
 #pragma unroll
