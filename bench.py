@@ -810,7 +810,7 @@ def run_extra_configs(main_wl):
 
 
 # tools/gpurun/profile_all.sh passes, summarised by tools/pmc_summary.py (newest round first)
-PMC_FILE = next((f for f in ("r05_pmc.json", "r04_pmc.json", "r03_pmc.json", "r02_pmc_filter_order.json")
+PMC_FILE = next((f for f in ("r06_pmc.json", "r05_pmc.json", "r04_pmc.json", "r03_pmc.json", "r02_pmc_filter_order.json")
                  if os.path.exists(os.path.join(ROOT, "profiles", f))), "r02_pmc_filter_order.json")
 
 
