@@ -3,7 +3,7 @@
 bench (tool, not product).
 
 usage: tools/order_call_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> [out.json]
-Dispatches in launch order are cut into calls after each k_rs_publish (the last kernel of a call); per
+Dispatches in launch order are cut into calls after each k_msd_big (the last kernel of a call; k_rs_publish before round 6b); per
 call: kernels, read bytes = 2 x FETCH_SIZE x 1024 and write bytes = WRITE_SIZE x 1024 (the gfx950
 correction of MI355X_MICROARCH.md, as tools/pmc_summary.py)."""
 import csv
@@ -28,7 +28,7 @@ def calls(d):
     out, cur = [], []
     for k in sorted(d):
         cur.append((k, d[k][0], d[k][1]))
-        if d[k][0] == "k_rs_publish":
+        if d[k][0] in ("k_rs_publish", "k_msd_big"):
             out.append(cur)
             cur = []
     return out
