@@ -721,6 +721,8 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 // ballot, the next larger key found on the way. The first round takes cur = the bucket's first key
 // (a one-key bucket is then a single copy); a smaller key seen in it restarts from the smallest.
 constexpr int kPartRows = 16;  // rows per lane in flight (8: the same kernel time within noise)
+constexpr int kMsdBlkThreads = 256;  // k_msd_local_blk: a block per bucket,
+constexpr int kMsdBlkRows = 16;       // kMsdBlkRows rows per lane: up to 4,096 rows from registers
 // fuse: the bucket's ids are still only in ids[] (not copied to src yet): round 0 reads them there and
 // writes the copy to src as it goes. Its compacted writes land at positions it has already read (out never
 // passes the rows loaded so far), and later rounds read src.
@@ -777,6 +779,92 @@ __device__ __forceinline__ bool msd_wave_partition(const uint64_t* __restrict__ 
   return false;
 }
 
+// The same partition for a bucket of m <= 256E rows by a 256-thread block, the rows held in registers
+// (wave w: rows [64E w, 64E (w + 1)), element r of a lane at 64E w + 64 r + lane): one load phase (every
+// row's key and id in flight together), the smallest key by a block minimum (no restart round), then per
+// round each wave counts its rows of the key, a block prefix over the four counts gives the waves' output
+// offsets (one barrier, double-buffered counts), and the waves store their ids by ballot compaction. The
+// memory rounds pay one load latency per 1024-row chunk and round on one wave (the bench column's
+// buckets: 2 keys ~1,900 rows, 3 keys ~2,900, up to ~3,950 with 4). Rows past m read as key ~0: they never
+// lower the minimum or the next key, and as hits of a round whose key is ~0 (a real key only at a full
+// 64-bit span) they sit in the last positions, after every real row: their stores past the bucket are
+// dropped. fuse: ids[] is overwritten only after every wave holds its rows (a barrier); the side copy
+// src[] is written only if the rounds run out (k_msd_big reads it).
+template <int E, int NW>
+__device__ __forceinline__ bool msd_block_partition(const uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
+                                                    uint32_t* __restrict__ ids, uint32_t lo, uint32_t m,
+                                                    int max_rounds, bool fuse, uint32_t (*scnt)[NW],
+                                                    uint64_t (*smin)[NW]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t w0 = (uint32_t)wid * 64 * E;
+  uint64_t k[E];
+  uint32_t id[E];
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const uint32_t pos = min(w0 + (uint32_t)(r * 64 + lane), m - 1);
+    k[r] = keys[lo + pos];
+    id[r] = fuse ? ids[lo + pos] : src[lo + pos];
+  }
+  uint64_t below = ~0ull;
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    if (w0 + (uint32_t)(r * 64 + lane) >= m) k[r] = ~0ull;
+    below = k[r] < below ? k[r] : below;
+  }
+  below = wave_min_u64(below);
+  if (lane == 0) smin[1][wid] = below;
+  __syncthreads();  // every row in registers (ids[] may be written from here) and the four minima
+  uint64_t cur = smin[1][0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) cur = smin[1][w] < cur ? smin[1][w] : cur;
+  uint32_t out = lo;
+  const uint32_t end = lo + m;
+  for (int round = 0; round < max_rounds; ++round) {
+    const int buf = round & 1;
+    uint64_t nxt = ~0ull;
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      c += (uint32_t)__popcll(__ballot(k[r] == cur));
+      if (k[r] > cur && k[r] < nxt) nxt = k[r];
+    }
+    nxt = wave_min_u64(nxt);
+    if (lane == 0) {
+      scnt[buf][wid] = c;
+      smin[buf][wid] = nxt;
+    }
+    __syncthreads();
+    uint32_t base = out, tot = 0;
+    uint64_t nb = ~0ull;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      base += w < wid ? scnt[buf][w] : 0u;
+      tot += scnt[buf][w];
+      nb = smin[buf][w] < nb ? smin[buf][w] : nb;
+    }
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      const bool hit = k[r] == cur;
+      const uint64_t bal = __ballot(hit);
+      const uint32_t dst = base + (uint32_t)__popcll(bal & lt);
+      if (hit && dst < end) ids[dst] = id[r];
+      base += (uint32_t)__popcll(bal);
+    }
+    out += tot;
+    if (out >= end) return true;  // block-uniform
+    cur = nb;
+  }
+  if (fuse) {
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      const uint32_t pos = w0 + (uint32_t)(r * 64 + lane);
+      if (pos < m) src[lo + pos] = id[r];
+    }
+  }
+  return false;
+}
+
 // one wave sorts a bucket of m <= 64E rows by bitonic network (input positions r*64 + lane: coalesced)
 template <int E, int LOGP>
 __device__ __forceinline__ void msd_wave_sort(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ src,
@@ -829,7 +917,9 @@ __device__ __forceinline__ void msd_bucket(const int64_t* __restrict__ col, int 
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's copies land before its lanes read them
-  if (msd_wave_partition(keys, src, ids, lo, m, lane, m <= kMsdWaveMax ? 2 : 16, fuse)) return;
+  const int rounds = m <= kMsdWaveMax ? 2 : 16;
+  const bool done = msd_wave_partition(keys, src, ids, lo, m, lane, rounds, fuse);
+  if (done) return;
   if (m > kMsdWaveMax) {
     if (lane == 0) big[atomicAdd(&ctl[kMsdCtlBig], 1u)] = b;
     return;
@@ -841,7 +931,8 @@ __device__ __forceinline__ void msd_bucket(const int64_t* __restrict__ col, int 
   else msd_wave_sort<8, 9>(keys, src, ids, lo, m, rmask, lane);
 }
 
-// One wave per `per_wave` consecutive buckets: the wave's first lanes read their buckets' table entries
+// Bucket ranges (DDSHE_ORDER_MSDLIST=0, round 6's A/B path): one wave per `per_wave` consecutive buckets:
+// the wave's first lanes read their buckets' table entries
 // together, a ballot marks the buckets holding two distinct keys, and the wave orders those one after
 // another (bucket bounds made wave-uniform, so its addressing stays scalar). Round 5 ran one wave per
 // bucket: 65,536 waves, most reading one word and exiting. Same box, k_msd_local per 10M-row call on the
@@ -849,12 +940,82 @@ __device__ __forceinline__ void msd_bucket(const int64_t* __restrict__ col, int 
 // (neighbouring multi-key buckets serialise); uniform 54-bit keys (every bucket multi-key): call 0.709 ->
 // 0.683 ms at 2.
 // (per_wave: DDSHE_ORDER_MSDWAVE, 2 by default; 1 is round 5's one wave per bucket, A/B; a power of 2 <= 64)
+// Lists (DDSHE_ORDER_MSDLIST=1, default; same box, profiles/r06_msdlist_ab.txt: raw call 0.270 -> 0.257 ms
+// on the bench column, uniform 54-bit keys within 1 %): k_msd_list first gathers the multi-key buckets, block i of 64
+// (1024 threads, one per bucket) writing its buckets of <= kMsdWaveMax rows to the front of list[1024 i ..
+// 1024 i + 1024), the larger ones to the back, and the two counts to count[i] / count[64 + i] (no atomics:
+// one atomic counter serialised 1,024 waves, 7.4 us). Then k_msd_local's waves take the small entries
+// (wave w: entries w, w + waves, ...; each wave scans the 64 counts itself to find entry w) and
+// k_msd_local_blk's blocks the large ones, one 256-thread block per bucket partitioning from registers up
+// to 4,096 rows (msd_block_partition; wave 0 on the memory rounds above that). The bench column's ~600
+// multi-key buckets of ~1,900 (2 keys) to ~3,950 rows (4 keys) then run one per block instead of one per
+// wave on the memory rounds, queued behind the 65,536 / per_wave bucket ranges, most of which find nothing.
+constexpr int kMsdListBlocks = 64;
+constexpr int kMsdSmallBlocks = 1024;  // small list: 4,096 waves
+constexpr int kMsdLargeBlocks = 768;   // large list: 3 blocks per CU, one bucket each at a time
+// counts (small, large), then the small and the large segments (uint4 {bucket, first row, rows, 0} entries)
+constexpr uint32_t kMsdListWords = 2 * kMsdListBlocks + 8 * kMsdBuckets;
+static_assert(kMsdListBlocks * 1024 == (int)kMsdBuckets, "k_msd_list: one thread per bucket");
+__global__ void __launch_bounds__(1024) k_msd_list(MsdRuns runs, uint32_t* __restrict__ list,
+                                                   const uint64_t* __restrict__ plan) {
+  if (plan && plan[1] == kRsNoPlan) return;
+  __shared__ uint32_t wsmall[16], wlarge[16];
+  const uint32_t b = blockIdx.x * 1024 + threadIdx.x;
+  const uint32_t lo = runs.first[b];
+  const bool need = lo != ~0u && (runs.multi[b] != 0u || runs.kmin[b] != runs.kmax[b]);
+  const bool large = need && runs.end[b] - lo > kMsdWaveMax;
+  const uint64_t bs = __ballot(need && !large), bl = __ballot(large);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    wsmall[wid] = (uint32_t)__popcll(bs);
+    wlarge[wid] = (uint32_t)__popcll(bl);
+  }
+  __syncthreads();
+  uint32_t ps = 0, pl = 0, ts = 0, tl = 0;
+  for (int w = 0; w < 16; ++w) {
+    ps += w < wid ? wsmall[w] : 0u;
+    pl += w < wid ? wlarge[w] : 0u;
+    ts += wsmall[w];
+    tl += wlarge[w];
+  }
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint4* segs = reinterpret_cast<uint4*>(list + 2 * kMsdListBlocks) + blockIdx.x * 1024;
+  if (large) segs[kMsdBuckets + pl + (uint32_t)__popcll(bl & lt)] = make_uint4(b, lo, runs.end[b] - lo, 0u);
+  else if (need) segs[ps + (uint32_t)__popcll(bs & lt)] = make_uint4(b, lo, runs.end[b] - lo, 0u);
+  if (threadIdx.x == 0) {
+    list[blockIdx.x] = ts;
+    list[kMsdListBlocks + blockIdx.x] = tl;
+  }
+}
+
+// entry q of one kind of k_msd_list's output (uint4 {bucket, first row, rows, 0}: the bucket's bounds ride
+// in its entry, no dependent load for them), by one wave: the 64 counts' prefix, kept in registers across
+// the wave's entries
+struct MsdListView {
+  uint32_t incl, c, n;
+  const uint4* segs;
+  __device__ MsdListView(const uint32_t* list, bool large, int lane) {
+    c = list[(large ? kMsdListBlocks : 0) + lane];
+    segs = reinterpret_cast<const uint4*>(list + 2 * kMsdListBlocks) + (large ? kMsdBuckets : 0u);
+    incl = c;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
+      if (lane >= off) incl += y;
+    }
+    n = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)incl, 63));
+  }
+  __device__ uint4 entry(uint32_t q) const {  // q < n, wave-uniform
+    const int seg = __popcll(__ballot(incl <= q));
+    return segs[(uint32_t)seg * 1024 + q - (uint32_t)__shfl((int)(incl - c), seg)];
+  }
+};
+
 __global__ void __launch_bounds__(256) k_msd_local(const int64_t* __restrict__ col, int desc, uint64_t kmin,
                                                    uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
                                                    uint32_t* __restrict__ ids, MsdRuns runs,
                                                    uint32_t* __restrict__ ctl, uint32_t* __restrict__ big,
                                                    const uint64_t* __restrict__ plan, uint32_t per_wave,
-                                                   bool fuse_copy) {
+                                                   bool fuse_copy, const uint32_t* __restrict__ list = nullptr) {
   if (plan) {
     const uint64_t s1 = plan[1];
     if (s1 == kRsNoPlan) return;
@@ -862,6 +1023,23 @@ __global__ void __launch_bounds__(256) k_msd_local(const int64_t* __restrict__ c
     runs.s1 = (int)s1;
   }
   const int lane = threadIdx.x & 63;
+  if (list) {  // the small entries of k_msd_list
+    const MsdListView lv(list, false, lane);
+    const uint32_t step = gridDim.x * 4;
+    uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    uint4 e = q < lv.n ? lv.entry(q) : make_uint4(0, 0, 0, 0);
+    while (q < lv.n) {  // the next entry's load in flight behind this bucket's work
+      const uint32_t qn = q + step;
+      const uint4 en = qn < lv.n ? lv.entry(qn) : make_uint4(0, 0, 0, 0);
+      const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)e.x);
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)e.y);
+      const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)e.z);
+      msd_bucket(col, desc, kmin, keys, src, ids, b, lo, m, runs.s1, ctl, big, lane, fuse_copy);
+      e = en;
+      q = qn;
+    }
+    return;
+  }
   const uint32_t b0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * per_wave;
   const uint32_t bl = b0 + ((uint32_t)lane & (per_wave - 1));
   const uint32_t lo_l = runs.first[bl];
@@ -876,6 +1054,43 @@ __global__ void __launch_bounds__(256) k_msd_local(const int64_t* __restrict__ c
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)lo_l, j));
     const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)m_l, j));
     msd_bucket(col, desc, kmin, keys, src, ids, b0 + (uint32_t)j, lo, m, runs.s1, ctl, big, lane, fuse_copy);
+  }
+}
+
+// the large entries of k_msd_list (> kMsdWaveMax rows), one block per bucket: the register partition up to
+// 256 x kMsdBlkRows rows with the fused side copy (the default); above that, or with the copy loop (gather
+// mode, DDSHE_ORDER_FUSECOPY=0), wave 0 alone as k_msd_local would; a bucket whose 16 rounds run out goes
+// to k_msd_big's list
+__global__ void __launch_bounds__(kMsdBlkThreads) k_msd_local_blk(const int64_t* __restrict__ col, int desc, uint64_t kmin,
+                                                       uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
+                                                       uint32_t* __restrict__ ids, MsdRuns runs,
+                                                       uint32_t* __restrict__ ctl, uint32_t* __restrict__ big,
+                                                       const uint64_t* __restrict__ plan, bool fuse_copy,
+                                                       const uint32_t* __restrict__ list) {
+  if (plan) {
+    const uint64_t s1 = plan[1];
+    if (s1 == kRsNoPlan) return;
+    kmin = plan[0];
+    runs.s1 = (int)s1;
+  }
+  constexpr int NW = kMsdBlkThreads / 64;
+  __shared__ uint32_t scnt[2][NW];
+  __shared__ uint64_t smin[2][NW];
+  const int lane = threadIdx.x & 63;
+  const bool fuse = col == nullptr && fuse_copy;
+  const MsdListView lv(list, true, lane);  // every wave of the block: the same entries
+  for (uint32_t q = blockIdx.x; q < lv.n; q += gridDim.x) {
+    const uint4 e = lv.entry(q);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)e.x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)e.y);
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)e.z);
+    if (fuse && m <= (uint32_t)kMsdBlkThreads * kMsdBlkRows) {
+      if (!msd_block_partition<kMsdBlkRows, NW>(keys, src, ids, lo, m, 16, true, scnt, smin) && threadIdx.x == 0)
+        big[atomicAdd(&ctl[kMsdCtlBig], 1u)] = b;
+      __syncthreads();  // scnt / smin free for the next bucket
+    } else if (threadIdx.x < 64) {
+      msd_bucket(col, desc, kmin, keys, src, ids, b, lo, m, runs.s1, ctl, big, lane, fuse_copy);
+    }
   }
 }
 
@@ -958,7 +1173,7 @@ size_t rs_scratch_bytes(size_t n) {
   return 2 * n * 8 + 32 + n * 4 + (size_t)kRsDigits * (rs_blocks(n) + 2) * 4 + 1024 +
          (size_t)kRsDigits * ((rs_blocks(n) + kScanTiles - 1) / kScanTiles) * 4 + 256 +
          16 * std::max((n + 256 * kRsPrepRows - 1) / (256 * kRsPrepRows), rs_blocks(n)) + 8 * kCarryWords + 800 +
-         (8 * (size_t)kMsdBuckets + 8) * 4;
+         (8 * (size_t)kMsdBuckets + 8 + kMsdListWords) * 4;
 }
 
 // the MSD path pays off from 4 LSD passes on (a span of > 24 bits) and enough rows to fill the buckets
@@ -1087,6 +1302,7 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
                (unsigned long long*)(mtab + 4 * kMsdBuckets), mtab + 6 * kMsdBuckets, 0};
   uint32_t* mctl = mtab + 7 * kMsdBuckets;
   uint32_t* mbig = mctl + 8;
+  uint32_t* mlist = mbig + kMsdBuckets;  // k_msd_list's counts, then its multi-key buckets (kMsdListWords)
   hipError_t e = hipSuccess;
   // the last pass writes the sorted keys too (DDSHE_ORDER_KEYS2=0: k_msd_local gathers its buckets' keys
   // from the column by id instead: 80 MB less written, but k_msd_local 42 -> 59 us against scatter 76 -> 66)
@@ -1126,8 +1342,17 @@ hipError_t launch_ope_order(const int64_t* col, const uint8_t* valid, size_t n, 
       const int v = order_env("DDSHE_ORDER_MSDWAVE", 2);
       return (v >= 1 && v <= 64 && (v & (v - 1)) == 0) ? (uint32_t)v : 2u;
     }();
-    hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / (4 * per_wave)), dim3(256), 0, st, keys2 ? nullptr : col, desc,
-                       kmin, kb, ib, out_ids, runs, mctl, mbig, plan, per_wave, fuse_copy != 0);
+    static const int list_env = order_env("DDSHE_ORDER_MSDLIST", 1);  // 0: bucket ranges per wave (A/B)
+    if (list_env) {
+      hipLaunchKernelGGL(k_msd_list, dim3(kMsdListBlocks), dim3(1024), 0, st, runs, mlist, plan);
+      hipLaunchKernelGGL(k_msd_local, dim3(kMsdSmallBlocks), dim3(256), 0, st, keys2 ? nullptr : col, desc, kmin, kb,
+                         ib, out_ids, runs, mctl, mbig, plan, per_wave, fuse_copy != 0, mlist);
+      hipLaunchKernelGGL(k_msd_local_blk, dim3(kMsdLargeBlocks), dim3(kMsdBlkThreads), 0, st, keys2 ? nullptr : col, desc, kmin,
+                         kb, ib, out_ids, runs, mctl, mbig, plan, fuse_copy != 0, mlist);
+    } else {
+      hipLaunchKernelGGL(k_msd_local, dim3(kMsdBuckets / (4 * per_wave)), dim3(256), 0, st, keys2 ? nullptr : col,
+                         desc, kmin, kb, ib, out_ids, runs, mctl, mbig, plan, per_wave, fuse_copy != 0, nullptr);
+    }
     hipLaunchKernelGGL(k_msd_big, dim3(kMsdBigBlocks), dim3(1024), 0, st, kb, ib, out_ids, runs, mctl, mbig, plan,
                        (hw && !publish_env) ? hw->d : nullptr);
   };

@@ -402,3 +402,42 @@ def test_order_msd_tile_edges(eng, n):
         for _ in range(2):
             assert np.array_equal(eng.ope_order(col, valid, desc), want), (n, desc)
     assert np.array_equal(eng.ope_order(col, None, False), np.argsort(col, kind="stable"))
+
+
+@pytest.mark.parametrize("span_bits", [44, 64])
+def test_order_msd_partition_sizes(eng, span_bits):
+    """Multi-key buckets at the edges of k_msd_local's paths (round 6: a list of the multi-key buckets,
+    register-resident partition by 8 / 16 / 32 / 48 rows per lane up to 3,072 rows, memory rounds above,
+    bitonic / workgroup sorts when the rounds run out): 300 .. 4,000 rows with 2 .. 17 distinct keys and
+    ties, and at a full 64-bit span a crowded top bucket holding the largest key (~0 after the offset:
+    the register partition's padding value) in both directions."""
+    rng = np.random.default_rng(span_bits)
+    n = 200_003
+    if span_bits == 64:
+        col = rng.integers(-2**63, 2**63 - 1, size=n, dtype=np.int64)
+        col[:2] = [-2**63, 2**63 - 1]
+        top, bot = np.int64(2**63 - 1), np.int64(-2**63)
+        hi_rows = rng.choice(np.arange(2, n), size=1900, replace=False)
+        col[hi_rows] = top - rng.choice([0, 1, 1 << 20], size=1900)      # top bucket: 3 keys, the max among them
+        lo_rows = rng.choice(np.setdiff1d(np.arange(2, n), hi_rows), size=2500, replace=False)
+        col[lo_rows] = bot + rng.choice([0, 7, 1 << 30, 1 << 40], size=2500)  # bottom bucket: 4 keys, the min
+    else:
+        col = rng.integers(0, 1 << span_bits, size=n, dtype=np.int64) - (1 << (span_bits - 1))
+        col[:2] = [-(1 << (span_bits - 1)), (1 << (span_bits - 1)) - 1]
+        free = np.arange(2, n)
+        rng.shuffle(free)
+        at = 0
+        s1 = span_bits - 16
+        for j, (sz, nk) in enumerate([(300, 2), (513, 3), (1024, 2), (1025, 4), (2048, 3), (2049, 2), (3072, 3),
+                                      (3073, 2), (2000, 17), (4000, 5)]):
+            bucket = 1000 + 3000 * j
+            rows = free[at: at + sz]
+            at += sz
+            keys = (bucket << s1) + rng.choice(1 << s1, size=nk, replace=False) - (1 << (span_bits - 1))
+            col[rows] = keys[rng.integers(0, nk, size=sz)]
+    valid = (rng.random(n) > 0.05).astype(np.uint8)
+    for desc in (True, False):
+        want = expected(col, valid, desc)
+        for _ in range(2):  # the second raw call runs the carried plan
+            assert np.array_equal(eng.ope_order(col, valid, desc), want), (span_bits, desc)
+        assert np.array_equal(eng.ope_order(col, None, desc), expected(col, np.ones(n, np.uint8), desc)), span_bits
