@@ -162,6 +162,35 @@ def test_sum_all_dec_string_rows_parallel_chunks(eng, keys):
     assert eng.sum_all_dec(rows, str(N)) == str(want)
 
 
+def test_sum_all_dec_string_rows_growing_lengths(eng, keys):
+    """String[] rows are measured and copied by the host pool into per-thread regions of the pinned
+    chunk, with rows per chunk sized by the longest row seen so far: rows that suddenly grow (short
+    rows, then ~4.6 KB rows, then rows wider than one thread's region but narrower than a chunk) make
+    regions run out of room mid-chunk; the chunk is cut at the first row that did not fit and the rest
+    is redone, so every row still folds exactly once, in order."""
+    k = keys["paillier1024_seed1"]
+    N = k["nsquare"]
+    rng = random.Random(33)
+    xs = [rng.randrange(N) for _ in range(40_000)]
+    rows = [str(x) for x in xs]              # 24 MB: the fused fill (requests of >= 16 MiB)
+    for i in range(30_000, 40_000):          # 4 KB of leading zeros each: regions overflow mid-chunk
+        rows[i] = "0" * 4_000 + rows[i]
+    for i in (33_000, 36_789):               # wider than a region (64 MiB / pool threads), < a chunk
+        rows[i] = "0" * (9 << 20) + rows[i]
+    xs[77] = -xs[77]
+    rows[77] = "-" + rows[77]
+    want = 1
+    for x in xs:
+        want = want * (x % N) % N
+    assert eng.sum_all_dec(rows, str(N)) == str(want)
+    bad = list(rows)
+    bad[35_000] = bad[35_000][:-3] + "x12"
+    with pytest.raises(ddshe.DDSError) as ei:
+        eng.sum_all_dec(bad, str(N))
+    assert ei.value.status == ddshe.DDS_E_FORMAT
+    assert "35000" in str(ei.value)
+
+
 def test_sum_all_dec_two_chunks(eng, keys):
     """dds_sum_all_dec splits a request of fewer than 2^19 rows into two chunks (the second one's
     copies overlap the first one's parse, 4 lanes per row for these small batches): the fold over
