@@ -707,15 +707,6 @@ int dec_table(ModConsts& mc) {
   return DDS_OK;
 }
 
-// DDSHE_DEC_FUSE=0/1: the String[] fill of large requests by fused per-region length + copy (A/B switch)
-static bool dec_fuse_on() {
-  static const bool on = [] {
-    const char* e = getenv("DDSHE_DEC_FUSE");
-    return e ? atoi(e) != 0 : false;
-  }();
-  return on;
-}
-
 // Parse rows [0, count) into X (stride) on the GPU: chunks are packed into pinned buffers
 // (host, overlapping the previous chunk's copy + parse), copied, parsed by k_dec_parse, then
 // negative / >= 2N rows are fixed by k_dec_fix. *orflags = OR of the row status bits
@@ -739,17 +730,8 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
   const size_t crows = std::min(kDecChunkRows, std::max<size_t>(4096, (count + 1) / 2));
   bool used[2] = {false, false};
   int slot = 0;
-  // String[] rows: the longest row seen so far sizes the next chunk; per-region state of a fused fill
-  size_t lmax = 0;
-  struct Region {
-    size_t used, stop, maxlen;
-    std::vector<size_t> longr;
-  };
-  std::vector<Region> regs;
-  std::vector<uint32_t> rel;  // row start inside its region
-  std::unique_ptr<uint32_t[]> lens;  // small String[] requests: lens[i] valid for i < lens_hi
+  std::unique_ptr<uint32_t[]> lens;  // String[] rows: lens[i] valid for i < lens_hi (uninitialised beyond)
   size_t lens_hi = 0;
-  int fuse = -1;  // String[] fill of this request: fused regions (1) or length pass + copy pass (0)
   for (size_t b = 0; b < count;) {
     if (used[slot]) HIP_TRY(hipEventSynchronize(w->ev_copy[slot]));  // the H2D out of this host slot is done
     HIP_TRY(w->hch[slot].ensure(kDecChunkBytes + 64));
@@ -773,107 +755,35 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
         for (size_t i = b; i <= e; ++i) o[i - b] = src.offs[i] - base;
       }
     }
-    // String[] regions filled this chunk (0: packed chunk, one H2D copy)
-    size_t nreg = 0;
-    const size_t rb = (kDecChunkBytes / std::max<size_t>(1, CopyPool::get().threads())) & ~(size_t)63;
     if (src.strs && std::min(count - b, crows) >= 1024) {
-      // NUL-terminated rows (JNA String[]): each pool thread takes a contiguous share of the chunk's
-      // rows and its own region of the pinned chunk, and measures and copies each row while the row is
-      // in its core's cache: one read of the row text (a length pass and then a copy pass read every
-      // row twice from memory). The regions go to the device as back-to-back pieces, so the device
-      // chunk is packed as before. Rows per chunk follow the longest row seen so far; a region that runs
-      // out of room ends the chunk at its first row that did not fit (later rows are redone next chunk).
-      // A request of less than kDecFuseBytes (config 1: 6 MB) keeps one packed chunk and one H2D copy:
-      // its rows stay in the host caches between the length and the copy pass, and one copy per region
-      // would cost more DMA launches than the second read saves.
-      CopyPool& pool = CopyPool::get();
-      const size_t T = pool.threads();
-      if (lmax == 0)
-        for (size_t i = b; i < std::min(count, b + 256); ++i)
-          lmax = std::max(lmax, std::min<size_t>(strlen(src.strs[i]), kDecChunkBytes));
-      if (fuse < 0) fuse = count * (lmax + 1) >= kDecFuseBytes && T > 1 && dec_fuse_on();  // once per request: the two
-      if (!fuse) {                                                           // paths keep different state
-        // lengths measured in blocks as the chunk cut reaches them and kept for the next chunk, copies
-        // spread over the host pool; the cut and the offsets are one sequential pass over the lengths
-        const size_t hi = std::min(count, b + crows);
-        if (!lens) lens.reset(new uint32_t[count]);
-        while (e < hi) {
-          if (e == lens_hi) {
-            const size_t lb = lens_hi, le = std::min(count, lb + kDecLenBlock);
-            pool.parallel_for(le - lb, 256, [&](size_t x, size_t y) {
-              for (size_t i = lb + x; i < lb + y; ++i)  // past the chunk budget: a long row either way
-                lens[i] = (uint32_t)std::min<size_t>(strlen(src.strs[i]), kDecChunkBytes);
-            });
-            lens_hi = le;
-          }
-          const size_t n = lens[e] > kDecChunkBytes - 64 ? 1 : lens[e];
-          if (pos + n > kDecChunkBytes) break;
-          if (n != lens[e]) long_rows->push_back(e);
-          pos += n;
-          o[++e - b] = pos;
+      // NUL-terminated rows (JNA String[]): lengths and copies spread over the host pool; the
+      // chunk cut and the offsets are one sequential pass over the lengths. Lengths are measured
+      // in blocks as the cut reaches them and kept for the next chunk (a chunk ends on its byte
+      // budget long before crows rows of ciphertext text: measuring [b, b + crows) per chunk read
+      // every row ~5 times for 4096-bit rows)
+      const size_t hi = std::min(count, b + crows);
+      if (!lens) lens.reset(new uint32_t[count]);
+      while (e < hi) {
+        if (e == lens_hi) {
+          const size_t lb = lens_hi, le = std::min(count, lb + kDecLenBlock);
+          CopyPool::get().parallel_for(le - lb, 256, [&](size_t x, size_t y) {
+            for (size_t i = lb + x; i < lb + y; ++i)  // past the chunk budget: a long row either way
+              lens[i] = (uint32_t)std::min<size_t>(strlen(src.strs[i]), kDecChunkBytes);
+          });
+          lens_hi = le;
         }
-        pool.parallel_for(e - b, 256, [&](size_t x, size_t y) {
-          for (size_t i = x; i < y; ++i)
-            memcpy(dst + o[i], o[i + 1] - o[i] == lens[b + i] ? src.strs[b + i] : "0", o[i + 1] - o[i]);
-        });
-        goto packed;
+        const size_t n = lens[e] > kDecChunkBytes - 64 ? 1 : lens[e];
+        if (pos + n > kDecChunkBytes) break;
+        if (n != lens[e]) long_rows->push_back(e);
+        pos += n;
+        o[++e - b] = pos;
       }
-      const size_t per = std::max<size_t>(1, rb / (lmax + lmax / 16 + 8));
-      const size_t R = std::min({count - b, crows, per * T}), pt = (R + T - 1) / T;
-      regs.resize(T);
-      if (rel.size() < R) rel.resize(R);
-      pool.parallel_for(T, 1, [&](size_t x, size_t y) {
-        for (size_t t = x; t < y; ++t) {
-          Region& g = regs[t];
-          g.longr.clear();
-          const size_t r0 = std::min(R, t * pt), r1 = std::min(R, r0 + pt);
-          char* base = dst + t * rb;
-          size_t p = 0, i = r0, ml = 0;
-          for (; i < r1; ++i) {
-            const char* s = src.strs[b + i];
-            const size_t n = strlen(s);
-            ml = std::max(ml, n);
-            const bool longrow = n > kDecChunkBytes - 64;  // parsed as "0" here, on the host by the caller
-            const size_t m = longrow ? 1 : n;
-            if (p + m > rb) break;
-            if (longrow) g.longr.push_back(b + i);
-            memcpy(base + p, longrow ? "0" : s, m);
-            rel[i] = (uint32_t)p;
-            p += m;
-          }
-          g.used = p;
-          g.stop = i;
-          g.maxlen = ml;
-        }
+      CopyPool::get().parallel_for(e - b, 256, [&](size_t x, size_t y) {
+        for (size_t i = x; i < y; ++i)
+          memcpy(dst + o[i], o[i + 1] - o[i] == lens[b + i] ? src.strs[b + i] : "0", o[i + 1] - o[i]);
       });
-      // the chunk ends at the first row a region could not take
-      size_t stop = R;
-      for (size_t t = 0; t < T; ++t) {
-        lmax = std::max(lmax, regs[t].maxlen);
-        const size_t r1 = std::min(R, std::min(R, t * pt) + pt);
-        if (regs[t].stop < r1) {
-          stop = regs[t].stop;
-          break;
-        }
-      }
-      if (stop > 0) {  // else a row wider than a region: the row-at-a-time loop below takes it
-        nreg = (stop + pt - 1) / pt;
-        size_t dbase = 0;
-        for (size_t t = 0; t < nreg; ++t) {
-          const size_t r0 = t * pt, r1 = std::min(stop, r0 + pt);  // the cut region broke at `stop`: used ends there
-          for (size_t i = r0; i < r1; ++i) o[i] = dbase + rel[i];
-          for (size_t lr : regs[t].longr)
-            if (lr < b + r1) long_rows->push_back(lr);
-          regs[t].stop = dbase;  // now: the region's place in the packed device chunk
-          dbase += regs[t].used;
-        }
-        e = b + stop;
-        pos = dbase;
-        o[stop] = pos;
-      }
     }
-  packed:
-    while (nreg == 0 && e < count && e - b < crows) {
+    while (e < count && e - b < crows) {
       size_t n = src.len(e);
       const bool longrow = n > kDecChunkBytes - 64;
       if (longrow) n = 1;
@@ -884,9 +794,7 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
       o[++e - b] = pos;
     }
     const size_t nrows = e - b, bytes = (16 + pos + 16 + 3) & ~(size_t)3;
-    // zero tail after the last row: in place, or (regions) from a zeroed scratch past the regions
-    char* tail = nreg ? dst + kDecChunkBytes : dst + pos;
-    memset(tail, 0, bytes - 16 - pos);
+    memset(dst + pos, 0, bytes - 16 - pos);
     // the device slot is free once the parse of its previous chunk has run (a growing buffer is
     // reallocated only after that parse, host-side)
     if (used[slot] && (w->dch[slot].cap < bytes || w->doff[slot].cap < (nrows + 1) * 8))
@@ -894,15 +802,7 @@ int ingest_dec(Worker* w, hipStream_t st, ModConsts& mc, const DecRows& src, siz
     HIP_TRY(w->dch[slot].ensure(bytes));
     HIP_TRY(w->doff[slot].ensure((nrows + 1) * 8));
     if (used[slot]) HIP_TRY(hipStreamWaitEvent(cs, w->ev_dec[slot], 0));
-    if (!nreg) {
-      HIP_TRY(hipMemcpyAsync(w->dch[slot].p, w->hch[slot].p, bytes, hipMemcpyHostToDevice, cs));
-    } else {  // the regions back to back (regs[t].stop = the region's place), then the zero tail
-      char* dd = (char*)w->dch[slot].p + 16;
-      for (size_t t = 0; t < nreg; ++t)
-        if (regs[t].used)
-          HIP_TRY(hipMemcpyAsync(dd + regs[t].stop, dst + t * rb, regs[t].used, hipMemcpyHostToDevice, cs));
-      HIP_TRY(hipMemcpyAsync(dd + pos, tail, bytes - 16 - pos, hipMemcpyHostToDevice, cs));
-    }
+    HIP_TRY(hipMemcpyAsync(w->dch[slot].p, w->hch[slot].p, bytes, hipMemcpyHostToDevice, cs));
     HIP_TRY(hipMemcpyAsync(w->doff[slot].p, o, (nrows + 1) * 8, hipMemcpyHostToDevice, cs));
     HIP_TRY(hipEventRecord(w->ev_copy[slot], cs));
     HIP_TRY(hipStreamWaitEvent(st, w->ev_copy[slot], 0));

@@ -468,8 +468,6 @@ class CopyPool {
     std::unique_lock<std::mutex> lk(mu_);
     done_.wait(lk, [&] { return pending_ == 0; });
   }
-  // slices parallel_for deals out (the calling thread's included)
-  size_t threads() const { return (th_.empty() || getpid() != owner_) ? 1 : th_.size() + 1; }
   void copy(void* dst, const void* src, size_t n) {
     if (n < ((size_t)4 << 20)) {
       memcpy(dst, src, n);
@@ -536,8 +534,7 @@ struct DecRows {
 
 constexpr size_t kDecChunkBytes = (size_t)64 << 20;  // chars per pinned chunk
 constexpr size_t kDecChunkRows = (size_t)1 << 18;
-constexpr size_t kDecLenBlock = (size_t)1 << 14;  // String[] rows measured per host-pool pass (small requests)
-constexpr size_t kDecFuseBytes = (size_t)16 << 20;  // String[] requests from this size: fused length + copy per region
+constexpr size_t kDecLenBlock = (size_t)1 << 14;  // String[] rows measured per host-pool pass
 
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // rows of one rW matrix of this modulus' shape must stay addressable by the kernels (max_stride)
