@@ -545,15 +545,22 @@ __global__ void __launch_bounds__(BLK) k_rs_scatter(const uint64_t* __restrict__
     const size_t i = T::row(tile, wid, k, lane);
     dr[k] = i < n ? rs_digit(key[k], id[k], valid, shift, last, desc, vbit, kbit) : kRsNone;
   }
+  // bit 8 of a digit is set only by the last pass's validity bucket and by lanes past the column's end
+  // (kRsNone): a full tile of another pass ranks on 8 ballots
+  const bool nine = (last && valid) || (tile + 1) * T::kRows > n;
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
     const uint32_t d = dr[k];
-    // lanes holding the same digit: AND of 9 bit-ballots (bit 8 only set in the last pass)
+    // lanes holding the same digit: AND of the bit-ballots
     uint64_t peers = ~0ull;
 #pragma unroll
-    for (int b = 0; b < 9; ++b) {
+    for (int b = 0; b < 8; ++b) {
       const uint64_t bal = __ballot((d >> b) & 1u);
       peers &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    if (nine) {
+      const uint64_t bal = __ballot((d >> 8) & 1u);
+      peers &= ((d >> 8) & 1u) ? bal : ~bal;
     }
     uint32_t rank = 0;
     if (d != kRsNone) {
