@@ -441,3 +441,36 @@ def test_order_msd_partition_sizes(eng, span_bits):
         for _ in range(2):  # the second raw call runs the carried plan
             assert np.array_equal(eng.ope_order(col, valid, desc), want), (span_bits, desc)
         assert np.array_equal(eng.ope_order(col, None, desc), expected(col, np.ones(n, np.uint8), desc)), span_bits
+
+
+@pytest.mark.parametrize("n", [65_536, 70_001, 1_000_003])
+def test_order_low_cardinality_extremes(eng, n):
+    """A few thousand distinct keys spread over the whole int64 range (so the MSD split's buckets mix
+    single- and multi-key ones), INT64_MIN / INT64_MAX among them (order keys 0 and ~0 in one direction
+    or the other), ties, rows lacking the position, no valid array, and every row lacking the position:
+    equal to numpy's stable argsort in both directions."""
+    rng = np.random.default_rng(n + 7)
+    vals = np.concatenate([rng.integers(-2**63, 2**63 - 1, size=3000, dtype=np.int64),
+                           np.array([-2**63, 2**63 - 1, 0, -1], dtype=np.int64)])
+    col = vals[rng.integers(0, len(vals), size=n)]
+    col[:4] = [-2**63, 2**63 - 1, -2**63, 2**63 - 1]
+    valid = (rng.random(n) > 0.2).astype(np.uint8)
+    for desc in (True, False):
+        assert np.array_equal(eng.ope_order(col, valid, desc), expected(col, valid, desc)), desc
+    assert np.array_equal(eng.ope_order(col, None, True), expected(col, np.ones(n, np.uint8), True))
+    assert np.array_equal(eng.ope_order(col, np.zeros(n, np.uint8), True), np.arange(n))
+
+
+@pytest.mark.parametrize("distinct", [16_384, 50_000])
+def test_order_many_distinct_keys_40_bit_span(eng, distinct):
+    """Tens of thousands of distinct keys over a 2^40 span, each repeated: buckets of the MSD split holding
+    one key and several; equal to numpy's stable argsort."""
+    rng = np.random.default_rng(distinct)
+    n = 200_003
+    vals = rng.choice(np.arange(1, 2**40, 2**40 // (4 * distinct), dtype=np.int64), size=distinct, replace=False)
+    col = np.concatenate([vals, vals[rng.integers(0, distinct, size=n - distinct)]])
+    rng.shuffle(col)
+    col[5] = -2**63
+    valid = (rng.random(n) > 0.05).astype(np.uint8)
+    for desc in (True, False):
+        assert np.array_equal(eng.ope_order(col, valid, desc), expected(col, valid, desc)), desc
